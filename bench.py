@@ -1,0 +1,158 @@
+#!/usr/bin/env python
+"""Headline benchmark: ResNet-50 bf16 data-parallel training throughput (images/s,
+whole job) on synthetic ImageNet-shaped data, 1..8 MI355X (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Every timed step is a full training step through the framework's own engine:
+GPU input pipeline (uint8 -> random flip + normalize -> bf16 NHWC), forward
+(MFMA implicit-GEMM convs, fused BN/ReLU/residual, maxpool, GAP, fc), fused
+cross-entropy, backward (dgrad/wgrad MFMA kernels, BN backward), bucketed
+gradient all-reduce over RCCL overlapped with backward, fused flat SGD
+(momentum 0.9, weight decay 1e-4).  Weak scaling: fixed per-GPU batch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--model", default="resnet50")
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--num-classes", type=int, default=1000)
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--backend", default=os.environ.get("MI355X_DP_BACKEND", "nccl"))
+    p.add_argument("--bucket-mb", type=float, default=None)
+    p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        if args.backend == "smddp":
+            import smdistributed.dataparallel.torch.torch_smddp  # noqa: F401  (registers 'smddp')
+        dist.init_process_group(backend=args.backend, device_id=dev if args.backend == "nccl" else None)
+
+    from mi355x_dp.models import get_model
+    from mi355x_dp.ops import augment, cross_entropy
+    from mi355x_dp.parallel import DataParallel, FlatSGD
+
+    torch.manual_seed(1234 + rank)
+    model = get_model(args.model, num_classes=args.num_classes).to(dev)
+    kw = {}
+    if args.bucket_mb:
+        kw["bucket_cap_mb"] = args.bucket_mb
+    engine = DataParallel(model, **kw)
+    opt = FlatSGD(engine, lr=args.lr, momentum=0.9, weight_decay=1e-4)
+
+    B, S = args.batch, args.image_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(rank)
+    images = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev, generator=g)
+    labels = torch.randint(0, args.num_classes, (B,), dtype=torch.int64, device=dev, generator=g)
+
+    def step(i):
+        x = augment(images, 3, IMAGENET_MEAN, IMAGENET_STD, pad=0, flip=True, seed=i)
+        engine.zero_grad()
+        out = engine(x)
+        loss = cross_entropy(out, labels)
+        loss.backward()
+        opt.step()
+        return loss
+
+    t_w0 = time.time()
+    for i in range(args.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    first_loss = float(loss.detach()) if args.warmup else float("nan")
+    t_w1 = time.time()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    last_loss = float(loss.detach())
+
+    for i in range(args.profile_steps):
+        step(10_000 + i)
+    torch.cuda.synchronize()
+
+    total_images = world * B * args.steps
+    value = total_images / elapsed
+    if rank == 0:
+        out = {
+            "metric": "images/sec (whole node) ResNet-50 DDP" if args.model == "resnet50"
+            else f"images/sec (whole node) {args.model} DDP",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random uint8 ImageNet-shaped images, random labels; GPU flip+normalize pipeline; "
+                    "random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "image_size": S,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "optimizer": "SGD(momentum=0.9, wd=1e-4), fp32 master weights, bf16 compute",
+                "backend": args.backend if world > 1 else "none",
+                "buckets": len(engine.buckets),
+            },
+            "loss_first_warmup": round(first_loss, 4),
+            "loss_last": round(last_loss, 4),
+            "warmup_s": round(t_w1 - t_w0, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,373 @@
+// Pooling, loss, optimizer and input-pipeline kernels for gfx950 (MI355X).
+//
+// Reference hot-path counterparts:
+//   K8  MaxPool2d 3x3/2 fwd/bwd       -> maxpool_fwd / maxpool_bwd (argmax kept as uint8 tap id)
+//   K9  AdaptiveAvgPool2d(1) fwd/bwd  -> gap_fwd / gap_bwd
+//   K11 CrossEntropy fwd/bwd          -> ce_fwd (row logsumexp + mean loss) / ce_bwd
+//   K12 SGD momentum (foreach)        -> sgd_flat: ONE launch over the flat fp32 master
+//                                        buffer, fused weight decay, 1/world gradient
+//                                        scaling, and the bf16 compute-copy refresh
+//   K18 CPU PIL augmentation          -> augment: uint8 NHWC -> random crop (zero pad) +
+//                                        hflip + normalize -> bf16 NHWC, on the GPU
+//   stem im2col (C=3 input)           -> im2col_nhwc
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+inline int ew_grid(int64_t n) {
+  int64_t g = (n + NT - 1) / NT;
+  return (int)(g < 8192 ? g : 8192);
+}
+
+// ------------------------------------------------------------------ maxpool
+__global__ __launch_bounds__(NT) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ idx, int Nb, int H, int W, int C, int P,
+                                                         int Q, int k, int s, int pad) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)Nb * P * Q * C8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int c8 = (int)(t % C8);
+    int64_t pix = t / C8;
+    const int q = (int)(pix % Q); pix /= Q;
+    const int p = (int)(pix % P);
+    const int n = (int)(pix / P);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < k; ++r) {
+      const int ih = p * s - pad + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int c = 0; c < k; ++c) {
+        const int iw = q * s - pad + c;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*(const uint4*)(x + (((size_t)n * H + ih) * W + iw) * C + c8 * 8), f);
+        const uint8_t tap = (uint8_t)(r * k + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > best[j] || (f[j] != f[j])) { best[j] = f[j]; bi[j] = tap; }
+      }
+    }
+    const size_t o = (size_t)t * 8;
+    *(uint4*)(y + o) = pack8(best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(uint2*)(idx + o) = packed;
+  }
+}
+
+// input-centric gather: deterministic, no atomics
+__global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                         bf16_t* __restrict__ dx, int Nb, int H, int W, int C, int P,
+                                                         int Q, int k, int s, int pad) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)Nb * H * W * C8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int c8 = (int)(t % C8);
+    int64_t pix = t / C8;
+    const int w = (int)(pix % W); pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // outputs p whose window covers h: p*s - pad <= h <= p*s - pad + k - 1
+    const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
+    const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h + pad - p * s;
+      if (r < 0 || r >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int c = w + pad - q * s;
+        if (c < 0 || c >= k) continue;
+        const size_t o = (((size_t)n * P + p) * Q + q) * C + c8 * 8;
+        const uint2 ii = *(const uint2*)(idx + o);
+        float g[8];
+        unpack8(*(const uint4*)(dy + o), g);
+        const uint8_t tap = (uint8_t)(r * k + c);
+        const uint32_t wds[2] = {ii.x, ii.y};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((wds[j >> 2] >> (8 * (j & 3))) & 0xff) == tap) acc[j] += g[j];
+      }
+    }
+    *(uint4*)(dx + (size_t)t * 8) = pack8(acc);
+  }
+}
+
+// ------------------------------------------------------- global average pool
+__global__ __launch_bounds__(NT) void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int Nb,
+                                                     int HW, int C) {
+  const int C8 = C / 8;
+  const int t = blockIdx.x * NT + threadIdx.x;
+  if (t >= Nb * C8) return;
+  const int n = t / C8, c8 = t % C8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16_t* base = x + (size_t)n * HW * C + c8 * 8;
+  for (int i = 0; i < HW; ++i) {
+    float f[8];
+    unpack8(*(const uint4*)(base + (size_t)i * C), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f[j];
+  }
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  *(uint4*)(y + (size_t)n * C + c8 * 8) = pack8(acc);
+}
+
+__global__ __launch_bounds__(NT) void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int Nb,
+                                                     int HW, int C) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)Nb * HW * C8;
+  const float inv = 1.f / HW;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int c8 = (int)(t % C8);
+    const int n = (int)(t / ((int64_t)HW * C8));
+    float f[8];
+    unpack8(*(const uint4*)(dy + (size_t)n * C + c8 * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= inv;
+    *(uint4*)(dx + (size_t)t * 8) = pack8(f);
+  }
+}
+
+// ------------------------------------------------------------ cross entropy
+// one 256-thread block per row; logits fp32 [N][ld]
+__global__ __launch_bounds__(NT) void ce_fwd_kernel(const float* __restrict__ logits, const int64_t* __restrict__ y,
+                                                    float* __restrict__ lse, float* __restrict__ loss, int ncls, int ld,
+                                                    float inv_n) {
+  __shared__ float red[NT / 64];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float* l = logits + (size_t)row * ld;
+  float m = -INFINITY;
+  for (int c = tid; c < ncls; c += NT) m = fmaxf(m, l[c]);
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int c = tid; c < ncls; c += NT) s += __expf(l[c] - m);
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    const float ls = m + __logf(tot);
+    lse[row] = ls;
+    atomicAdd(loss, (ls - l[y[row]]) * inv_n);
+  }
+}
+
+// dlogits[n][c] = g * inv_n * (softmax - onehot), bf16 [N][ldo] (zero in padding columns)
+__global__ __launch_bounds__(NT) void ce_bwd_kernel(const float* __restrict__ logits, const int64_t* __restrict__ y,
+                                                    const float* __restrict__ lse, const float* __restrict__ gout,
+                                                    bf16_t* __restrict__ dl, int ncls, int ld, int ldo, float inv_n) {
+  const int row = blockIdx.x;
+  const float g = gout[0] * inv_n;
+  const float ls = lse[row];
+  const int yy = (int)y[row];
+  const float* l = logits + (size_t)row * ld;
+  for (int c = threadIdx.x; c < ldo; c += NT) {
+    float v = 0.f;
+    if (c < ncls) v = g * (__expf(l[c] - ls) - (c == yy ? 1.f : 0.f));
+    dl[(size_t)row * ldo + c] = f2bf(v);
+  }
+}
+
+// ---------------------------------------------------------------- SGD (flat)
+// torch.optim.SGD semantics (first step: buf = d_p), plus grad_scale (1/world).
+__global__ __launch_bounds__(NT) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ buf, bf16_t* __restrict__ p16, int64_t n,
+                                                      float lr, float momentum, float dampening, float wd,
+                                                      int nesterov, int first, float grad_scale) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    float pi = p[i];
+    float d = g[i] * grad_scale;
+    if (wd != 0.f) d += wd * pi;
+    if (momentum != 0.f) {
+      float b = first ? d : momentum * buf[i] + (1.f - dampening) * d;
+      buf[i] = b;
+      d = nesterov ? d + momentum * b : b;
+    }
+    pi -= lr * d;
+    p[i] = pi;
+    if (p16) p16[i] = f2bf(pi);
+  }
+}
+
+__global__ __launch_bounds__(NT) void cast_bf16_kernel(const float* __restrict__ s, bf16_t* __restrict__ d, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) d[i] = f2bf(s[i]);
+}
+
+// ---------------------------------------------------------- input pipeline
+// uint8 NHWC [N][H][W][C] -> bf16 NHWC [N][H][W][Cout] (Cout >= C, zero fill),
+// random crop with zero padding `pad` (offsets in [0, 2*pad]) and hflip per
+// image from a counter-based hash of (seed, image) -> reproducible, no state.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+__global__ __launch_bounds__(NT) void augment_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                     int Nb, int H, int W, int C, int Cout, int pad, int flip,
+                                                     uint32_t seed, const float* __restrict__ mean,
+                                                     const float* __restrict__ stdinv) {
+  const int64_t total = (int64_t)Nb * H * W;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int w = (int)(t % W);
+    const int h = (int)((t / W) % H);
+    const int n = (int)(t / ((int64_t)W * H));
+    const uint32_t hv = hash32(seed * 0x9E3779B9u + (uint32_t)n);
+    int dy = 0, dx = 0, fl = 0;
+    if (pad > 0) { dy = (int)(hv % (2 * pad + 1)) - pad; dx = (int)((hv >> 8) % (2 * pad + 1)) - pad; }
+    if (flip) fl = (hv >> 20) & 1;
+    const int sh = h + dy;
+    const int sw0 = fl ? (W - 1 - w) : w;
+    const int sw = sw0 + dx;
+    const bool ok = (unsigned)sh < (unsigned)H && (unsigned)sw < (unsigned)W;
+    bf16_t* o = dst + (size_t)t * Cout;
+    for (int c = 0; c < Cout; ++c) {
+      float v = 0.f;
+      if (c < C && ok) v = ((float)src[(((size_t)n * H + sh) * W + sw) * C + c] * (1.f / 255.f) - mean[c]) * stdinv[c];
+      o[c] = f2bf(v);
+    }
+  }
+}
+
+// NHWC bf16 [N][H][W][C] -> col [N*P*Q][Kp], k = (r*S + s)*C + c, zero for k >= R*S*C
+__global__ __launch_bounds__(NT) void im2col_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ col, int Nb,
+                                                    int H, int W, int C, int R, int S, int stride, int pad, int P,
+                                                    int Q, int Kp) {
+  const int64_t total = (int64_t)Nb * P * Q * Kp;
+  const int K = R * S * C;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int k = (int)(t % Kp);
+    int64_t pix = t / Kp;
+    bf16_t v = 0;
+    if (k < K) {
+      const int c = k % C, rs = k / C, s = rs % S, r = rs / S;
+      const int q = (int)(pix % Q);
+      const int p = (int)((pix / Q) % P);
+      const int n = (int)(pix / ((int64_t)P * Q));
+      const int ih = p * stride - pad + r, iw = q * stride - pad + s;
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = x[(((size_t)n * H + ih) * W + iw) * C + c];
+    }
+    col[t] = v;
+  }
+}
+
+// elementwise bf16 add (residual gradients that autograd would otherwise sum)
+__global__ __launch_bounds__(NT) void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                      bf16_t* __restrict__ o, int64_t nvec) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    float fa[8], fb[8];
+    unpack8(((const uint4*)a)[v], fa);
+    unpack8(((const uint4*)b)[v], fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] += fb[j];
+    ((uint4*)o)[v] = pack8(fa);
+  }
+}
+
+// sum of squares / checksum of an fp32 buffer (replica-divergence detector)
+__global__ __launch_bounds__(NT) void checksum_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out) {
+  __shared__ double red[NT / 64];
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    s += (double)x[i] * (double)((i % 7) + 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+}  // namespace
+
+MI_API int mi_maxpool_fwd(const void* x, void* y, void* idx, int Nb, int H, int W, int C, int P, int Q, int k, int s,
+                          int pad, hipStream_t st) {
+  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
+  int64_t total = (int64_t)Nb * P * Q * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16_t*)x, (bf16_t*)y,
+                     (uint8_t*)idx, Nb, H, W, C, P, Q, k, s, pad);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_maxpool_bwd(const void* dy, const void* idx, void* dx, int Nb, int H, int W, int C, int P, int Q, int k,
+                          int s, int pad, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  int64_t total = (int64_t)Nb * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16_t*)dy,
+                     (const uint8_t*)idx, (bf16_t*)dx, Nb, H, W, C, P, Q, k, s, pad);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_gap_fwd(const void* x, void* y, int Nb, int HW, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(cdiv((int64_t)Nb * C / 8, NT)), dim3(NT), 0, st, (const bf16_t*)x,
+                     (bf16_t*)y, Nb, HW, C);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_gap_bwd(const void* dy, void* dx, int Nb, int HW, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  int64_t total = (int64_t)Nb * HW * (C / 8);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16_t*)dy, (bf16_t*)dx, Nb, HW, C);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_ce_fwd(const float* logits, const int64_t* y, float* lse, float* loss, int N, int ncls, int ld,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(N), dim3(NT), 0, st, logits, y, lse, loss, ncls, ld, 1.f / N);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_ce_bwd(const float* logits, const int64_t* y, const float* lse, const float* gout, void* dl, int N,
+                     int ncls, int ld, int ldo, hipStream_t st) {
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3(N), dim3(NT), 0, st, logits, y, lse, gout, (bf16_t*)dl, ncls, ld, ldo,
+                     1.f / N);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_sgd_flat(float* p, const float* g, float* buf, void* p16, int64_t n, float lr, float momentum,
+                       float dampening, float wd, int nesterov, int first, float grad_scale, hipStream_t st) {
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(ew_grid(n)), dim3(NT), 0, st, p, g, buf, (bf16_t*)p16, n, lr, momentum,
+                     dampening, wd, nesterov, first, grad_scale);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_cast_bf16(const float* s, void* d, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(ew_grid(n)), dim3(NT), 0, st, s, (bf16_t*)d, n);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_augment(const void* src, void* dst, int Nb, int H, int W, int C, int Cout, int pad, int flip,
+                      uint32_t seed, const float* mean, const float* stdinv, hipStream_t st) {
+  int64_t total = (int64_t)Nb * H * W;
+  hipLaunchKernelGGL(augment_kernel, dim3(ew_grid(total)), dim3(NT), 0, st, (const uint8_t*)src, (bf16_t*)dst, Nb, H,
+                     W, C, Cout, pad, flip, seed, mean, stdinv);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_im2col(const void* x, void* col, int Nb, int H, int W, int C, int R, int S, int stride, int pad, int P,
+                     int Q, int Kp, hipStream_t st) {
+  int64_t total = (int64_t)Nb * P * Q * Kp;
+  hipLaunchKernelGGL(im2col_kernel, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16_t*)x, (bf16_t*)col, Nb, H, W,
+                     C, R, S, stride, pad, P, Q, Kp);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_add_bf16(const void* a, const void* b, void* o, int64_t n, hipStream_t st) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(ew_grid(n / 8)), dim3(NT), 0, st, (const bf16_t*)a, (const bf16_t*)b,
+                     (bf16_t*)o, n / 8);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_checksum(const float* x, int64_t n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(checksum_kernel, dim3(std::min<int64_t>(1024, (n + NT - 1) / NT)), dim3(NT), 0, st, x, n, out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,314 @@
+// BatchNorm2d (train + eval) over NHWC bf16 activations with fused ReLU and
+// residual add, for gfx950.  Replaces cuDNN BN fwd/bwd + ATen ReLU / add
+// kernels on the reference's ResNet hot path.
+//
+// Forward (train):  stats partials -> finalize (mean/invstd, running stats,
+//                   num_batches_tracked, scale/shift) -> apply y = act(x*a+b (+res))
+// Backward:         partial sums of dz and dz*xhat (dz = dy * [y>0]) ->
+//                   finalize (dgamma/dbeta accumulated into the fp32 grad buffer,
+//                   per-channel affine dx = k0*dz + k1*x + k2) -> apply (+ dres = dz)
+// The ReLU mask is recovered from the saved output y, so no mask tensor exists.
+// All loads/stores are 16-byte vectors (8 bf16 per lane).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+struct SlabGeom {
+  int tpr;   // threads per row (each covers 8 channels)
+  int rp;    // rows processed in parallel per block
+  int cw;    // channel slab width
+};
+
+__host__ __device__ inline SlabGeom slab_geom(int C) {
+  SlabGeom g;
+  g.tpr = C / 8 < NT ? C / 8 : NT;
+  g.rp = NT / g.tpr;
+  g.cw = g.tpr * 8;
+  return g;
+}
+
+// Reduce the per-thread 8-channel partials over the rp row-groups and write
+// two rows (s0, s1) of the partial slab for this block.
+__device__ __forceinline__ void block_reduce_store(float* s0, float* s1, float* part, int C, int cbase,
+                                                   const SlabGeom& g) {
+  __shared__ float red[2][NT * 8];
+  const int tid = threadIdx.x;
+  const int c8 = tid % g.tpr, r0 = tid / g.tpr;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][r0 * g.cw + c8 * 8 + j] = s0[j];
+    red[1][r0 * g.cw + c8 * 8 + j] = s1[j];
+  }
+  __syncthreads();
+  // each of the first cw threads sums one channel over rp rows
+  for (int c = tid; c < g.cw; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < g.rp; ++r) { a += red[0][r * g.cw + c]; b += red[1][r * g.cw + c]; }
+    part[(size_t)(blockIdx.x * 2 + 0) * C + cbase + c] = a;
+    part[(size_t)(blockIdx.x * 2 + 1) * C + cbase + c] = b;
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                      int M, int C, int rows_per_block) {
+  const SlabGeom g = slab_geom(C);
+  const int tid = threadIdx.x;
+  const int c8 = tid % g.tpr, r0 = tid / g.tpr;
+  const int cbase = blockIdx.y * g.cw;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  float s[8] = {0}, q[8] = {0};
+  const bf16_t* base = x + cbase + c8 * 8;
+  for (int r = rb + r0; r < re; r += g.rp) {
+    uint4 v = *(const uint4*)(base + (size_t)r * C);
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+  }
+  block_reduce_store(s, q, part, C, cbase, g);
+}
+
+// training-mode finalize: one thread per channel
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C, float eps, float momentum,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                   float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) { s += part[(size_t)(2 * b) * C + c]; q += part[(size_t)(2 * b + 1) * C + c]; }
+  const double mean = s / M;
+  double var = q / M - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = gm * invstd;
+  shift[c] = bt - (float)mean * gm * invstd;
+  if (rmean) {
+    const double unbiased = M > 1 ? var * M / (M - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+  }
+}
+
+__global__ void bn_eval_coeffs_kernel(int C, float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                      const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                      float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rvar[c] + eps);
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = gm * invstd;
+  shift[c] = bt - rmean[c] * gm * invstd;
+}
+
+// y = act(x*scale + shift (+ res)); grid-stride over 8-element vectors
+__global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                      bf16_t* __restrict__ y, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, int64_t nvec, int C, int relu) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int c = (int)((v * 8) % C);
+    float f[8];
+    unpack8(((const uint4*)x)[v], f);
+    const float4 a0 = *(const float4*)(scale + c), a1 = *(const float4*)(scale + c + 4);
+    const float4 b0 = *(const float4*)(shift + c), b1 = *(const float4*)(shift + c + 4);
+    f[0] = f[0] * a0.x + b0.x; f[1] = f[1] * a0.y + b0.y; f[2] = f[2] * a0.z + b0.z; f[3] = f[3] * a0.w + b0.w;
+    f[4] = f[4] * a1.x + b1.x; f[5] = f[5] * a1.y + b1.y; f[6] = f[6] * a1.z + b1.z; f[7] = f[7] * a1.w + b1.w;
+    if (res) {
+      float r[8];
+      unpack8(((const uint4*)res)[v], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += r[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    ((uint4*)y)[v] = pack8(f);
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          const bf16_t* __restrict__ x, const float* __restrict__ mean,
+                                                          float* __restrict__ part, int M, int C, int rows_per_block,
+                                                          int relu) {
+  const SlabGeom g = slab_geom(C);
+  const int tid = threadIdx.x;
+  const int c8 = tid % g.tpr, r0 = tid / g.tpr;
+  const int cbase = blockIdx.y * g.cw;
+  const int cc = cbase + c8 * 8;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  float mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = mean[cc + j];
+  float s[8] = {0}, q[8] = {0};
+  for (int r = rb + r0; r < re; r += g.rp) {
+    const size_t off = (size_t)r * C + cc;
+    float d[8], xv[8];
+    unpack8(*(const uint4*)(dy + off), d);
+    unpack8(*(const uint4*)(x + off), xv);
+    if (relu) {
+      float yv[8];
+      unpack8(*(const uint4*)(y + off), yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] += d[j]; q[j] += d[j] * (xv[j] - mu[j]); }
+  }
+  block_reduce_store(s, q, part, C, cbase, g);
+}
+
+// -> dgamma/dbeta (+=) and coef[0..2][C] so that dx = coef0*dz + coef1*x + coef2
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) { s += part[(size_t)(2 * b) * C + c]; q += part[(size_t)(2 * b + 1) * C + c]; }
+  const float is = invstd[c];
+  const float sum_dz = (float)s;
+  const float sum_dz_xhat = (float)q * is;
+  if (dgamma) dgamma[c] += sum_dz_xhat;
+  if (dbeta) dbeta[c] += sum_dz;
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float k0 = gm * is;
+  const float mdz = sum_dz / M, mdzx = sum_dz_xhat / M;
+  // dx = k0*(dz - mdz - xhat*mdzx),  xhat = (x-mean)*is
+  const float k1 = -k0 * is * mdzx;
+  const float k2 = -k0 * mdz - k1 * mean[c];
+  coef[c] = k0;
+  coef[C + c] = k1;
+  coef[2 * C + c] = k2;
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                                          bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
+                                                          int64_t nvec, int C, int relu) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int c = (int)((v * 8) % C);
+    float d[8], xv[8];
+    unpack8(((const uint4*)dy)[v], d);
+    unpack8(((const uint4*)x)[v], xv);
+    if (relu) {
+      float yv[8];
+      unpack8(((const uint4*)y)[v], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+    if (dres) ((uint4*)dres)[v] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = coef[c + j] * d[j] + coef[C + c + j] * xv[j] + coef[2 * C + c + j];
+    ((uint4*)dx)[v] = pack8(o);
+  }
+}
+
+// eval-mode / frozen BN backward: dx = scale * dz
+__global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                         const float* __restrict__ scale, bf16_t* __restrict__ dx,
+                                                         bf16_t* __restrict__ dres, int64_t nvec, int C, int relu) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int c = (int)((v * 8) % C);
+    float d[8];
+    unpack8(((const uint4*)dy)[v], d);
+    if (relu) {
+      float yv[8];
+      unpack8(((const uint4*)y)[v], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+    if (dres) ((uint4*)dres)[v] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = scale[c + j] * d[j];
+    ((uint4*)dx)[v] = pack8(o);
+  }
+}
+
+inline int ew_grid(int64_t nvec) {
+  int64_t g = (nvec + NT - 1) / NT;
+  return (int)(g < 4096 ? g : 4096);
+}
+
+inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3& grid) {
+  SlabGeom g = slab_geom(C);
+  int ncs = C / g.cw;
+  // ~2048 blocks in total, each handling >= 4*rp rows
+  int target = std::max(1, 2048 / ncs);
+  rows_per_block = std::max(g.rp * 4, cdiv(M, target));
+  rows_per_block = cdiv(rows_per_block, g.rp) * g.rp;
+  nblk = cdiv(M, rows_per_block);
+  grid = dim3(nblk, ncs);
+}
+
+}  // namespace
+
+MI_API int mi_bn_partial_rows(int M, int C) {
+  int nblk, rpb; dim3 grid;
+  slab_launch_dims(M, C, nblk, rpb, grid);
+  return nblk;
+}
+
+// Training-mode forward.  part: fp32 workspace [mi_bn_partial_rows(M,C)][2][C].
+MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C, float eps, float momentum,
+                           const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
+                           float* save_mean, float* save_invstd, float* scale, float* shift, float* part,
+                           int relu, hipStream_t st) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  int nblk, rpb; dim3 grid;
+  slab_launch_dims(M, C, nblk, rpb, grid);
+  hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nblk, M, C, eps, momentum,
+                     gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
+  int64_t nvec = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
+                     (bf16_t*)y, scale, shift, nvec, C, relu);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_bn_fwd_eval(const void* x, const void* res, void* y, int M, int C, float eps, const float* gamma,
+                          const float* beta, const float* rmean, const float* rvar, float* scale, float* shift,
+                          int relu, hipStream_t st) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, C, eps, gamma, beta, rmean, rvar,
+                     scale, shift);
+  int64_t nvec = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
+                     (bf16_t*)y, scale, shift, nvec, C, relu);
+  return (int)hipGetLastError();
+}
+
+// Training-mode backward.  coef: fp32 [3][C] workspace; dres may be null.
+MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* dx, void* dres, int M, int C,
+                           const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
+                           float* dbeta, float* coef, float* part, int relu, hipStream_t st) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  int nblk, rpb; dim3 grid;
+  slab_launch_dims(M, C, nblk, rpb, grid);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                     (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nblk, M, C, gamma,
+                     save_mean, save_invstd, dgamma, dbeta, coef);
+  int64_t nvec = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)y, (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_bn_bwd_eval(const void* dy, const void* y, const float* scale, void* dx, void* dres, int M, int C,
+                          int relu, hipStream_t st) {
+  int64_t nvec = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_eval_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)y, scale, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
+  return (int)hipGetLastError();
+}

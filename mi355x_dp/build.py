@@ -1,0 +1,124 @@
+"""Build the in-tree native components for gfx950.
+
+    python -m mi355x_dp.build            # kernels + comm backend + launcher
+    python -m mi355x_dp.build kernels    # only libmi355x_kernels.so
+
+Artefacts land in ``mi355x_dp/_native`` (git-ignored, but shipped to the GPU box
+with the repo snapshot).  Every HIP source is compiled with
+``hipcc --offload-arch=gfx950``; no JIT cache under ~/.cache is used.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+NATIVE = os.path.join(ROOT, "mi355x_dp", "_native")
+BUILD = os.path.join(ROOT, "build")
+ARCH = os.environ.get("MI355X_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _run(cmd, cwd=None):
+    r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed: " + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def _digest(paths, extra=""):
+    h = hashlib.sha256(extra.encode())
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def build_kernels(force=False, verbose=True):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    out = os.path.join(NATIVE, "libmi355x_kernels.so")
+    stamp = out + ".sha256"
+    dig = _digest(srcs + hdrs, " ".join(HIP_FLAGS))
+    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == dig:
+        if verbose:
+            print(f"[build] {os.path.relpath(out, ROOT)} up to date")
+        return out
+    os.makedirs(os.path.join(BUILD, "kernels"), exist_ok=True)
+    os.makedirs(NATIVE, exist_ok=True)
+    objs = []
+
+    def one(src):
+        obj = os.path.join(BUILD, "kernels", os.path.basename(src) + ".o")
+        _run([HIPCC, *HIP_FLAGS, "-c", src, "-o", obj])
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(one, srcs))
+    tmp = out + ".tmp"
+    _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs])
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    if verbose:
+        print(f"[build] built {os.path.relpath(out, ROOT)} from {len(srcs)} HIP sources")
+    return out
+
+
+def build_launcher(force=False, verbose=True):
+    src = os.path.join(CSRC, "launch", "launcher.cpp")
+    if not os.path.exists(src):
+        return None
+    out = os.path.join(NATIVE, "mi355x_launch")
+    stamp = out + ".sha256"
+    dig = _digest([src])
+    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == dig:
+        return out
+    os.makedirs(NATIVE, exist_ok=True)
+    _run(["g++", "-O2", "-std=c++17", "-Wall", "-o", out + ".tmp", src])
+    os.replace(out + ".tmp", out)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    if verbose:
+        print(f"[build] built {os.path.relpath(out, ROOT)}")
+    return out
+
+
+def build_comm(force=False, verbose=True):
+    src_dir = os.path.join(CSRC, "comm")
+    srcs = sorted(glob.glob(os.path.join(src_dir, "*.cpp")) + glob.glob(os.path.join(src_dir, "*.hip")))
+    if not srcs:
+        return None
+    from mi355x_dp.parallel import _smddp_build
+    return _smddp_build.build(srcs, NATIVE, force=force, verbose=verbose)
+
+
+def build_all(force=False, verbose=True):
+    outs = [build_kernels(force, verbose), build_launcher(force, verbose)]
+    try:
+        outs.append(build_comm(force, verbose))
+    except ImportError:
+        pass
+    return [o for o in outs if o]
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    force = "--force" in sys.argv
+    if what == "kernels":
+        build_kernels(force)
+    elif what == "launcher":
+        build_launcher(force)
+    elif what == "comm":
+        build_comm(force)
+    else:
+        build_all(force)

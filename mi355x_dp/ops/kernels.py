@@ -1,0 +1,37 @@
+"""ctypes signatures of the C ABI exported by ``libmi355x_kernels.so``.
+
+One entry per ``MI_API`` function in ``csrc/kernels/*.hip``.
+"""
+from ._lib import signature, c_void_p as P, c_int as I, c_int64 as L, c_float as F
+import ctypes
+
+U32 = ctypes.c_uint32
+
+# gemm_conv.hip
+signature("mi_conv2d_fwd", P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_conv2d_dgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_conv2d_wgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_conv_wtrans", P, P, I, I, I, P)
+signature("mi_gemm_nt", P, P, P, P, I, I, I, I, I, I, I, I, P)
+signature("mi_gemm_tn", P, P, P, I, I, I, I, I, I, P)
+
+# norm_act.hip
+signature("mi_bn_partial_rows", I, I)
+signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, I, P)
+signature("mi_bn_fwd_eval", P, P, P, I, I, F, P, P, P, P, P, P, I, P)
+signature("mi_bn_bwd_train", P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)
+signature("mi_bn_bwd_eval", P, P, P, P, P, I, I, I, P)
+
+# misc.hip
+signature("mi_maxpool_fwd", P, P, P, I, I, I, I, I, I, I, I, I, P)
+signature("mi_maxpool_bwd", P, P, P, I, I, I, I, I, I, I, I, I, P)
+signature("mi_gap_fwd", P, P, I, I, I, P)
+signature("mi_gap_bwd", P, P, I, I, I, P)
+signature("mi_ce_fwd", P, P, P, P, I, I, I, P)
+signature("mi_ce_bwd", P, P, P, P, P, I, I, I, I, P)
+signature("mi_sgd_flat", P, P, P, P, L, F, F, F, F, I, I, F, P)
+signature("mi_cast_bf16", P, P, L, P)
+signature("mi_augment", P, P, I, I, I, I, I, I, I, U32, P, P, P)
+signature("mi_im2col", P, P, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_add_bf16", P, P, P, L, P)
+signature("mi_checksum", P, L, P, P)

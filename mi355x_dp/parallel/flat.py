@@ -1,0 +1,109 @@
+"""Flat parameter / gradient storage.
+
+All trainable parameters of a model are re-homed into ONE contiguous fp32
+master buffer (plus matching fp32 gradient buffer and a bf16 compute copy),
+laid out in reverse registration order (= approximate backward order), each
+tensor aligned to 64 elements.  4-D conv weights are stored ``[K][R][S][C]``
+(the ``channels_last`` strides of a ``[K, C, R, S]`` tensor) which is the
+layout the MFMA conv kernels consume, so the bf16 copy refreshed by the fused
+SGD kernel is directly the kernel operand.  Parameter objects are kept (their
+``.data`` is re-pointed), so optimizers/state_dict/named_parameters behave as
+before; ``state_dict`` hooks write NCHW-contiguous tensors.
+
+This replaces the reference's per-tensor DDP bucket copy-in/copy-out
+(SURVEY.md §2.5 K14, §3.2): buckets are slices of the gradient buffer, the
+backward kernels accumulate straight into them, and the all-reduce runs on
+the slice in place.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+
+ALIGN = 64  # elements (256 B for fp32)
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def _kernel_view(flat: torch.Tensor, off: int, shape) -> torch.Tensor:
+    n = 1
+    for s in shape:
+        n *= s
+    v = flat[off:off + n]
+    if len(shape) == 4:
+        K, C, R, S = shape
+        return v.view(K, R, S, C).permute(0, 3, 1, 2)
+    return v.view(shape)
+
+
+class FlatParams:
+    """Owns the flat fp32 params, fp32 grads and bf16 copy for a list of parameters."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], bf16_copy: bool = True):
+        params = [p for p in params if p.requires_grad]
+        if not params:
+            raise ValueError("no trainable parameters")
+        dev = params[0].device
+        self.device = dev
+        self.params: List[torch.nn.Parameter] = list(params)
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += _align(p.numel())
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.bf16 = torch.zeros(off, dtype=torch.bfloat16, device=dev) if bf16_copy else None
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                v = _kernel_view(self.data, o, tuple(p.shape))
+                v.copy_(p.data)
+                p.data = v
+                p.grad = _kernel_view(self.grad, o, tuple(p.shape))
+                p._mi_flat = True
+                if self.bf16 is not None:
+                    p._mi_bf16 = _kernel_view(self.bf16, o, tuple(p.shape))
+            if self.bf16 is not None:
+                from mi355x_dp.ops.functional import cast_bf16_
+                cast_bf16_(self.data, self.bf16)
+
+    def param_range(self, i: int):
+        p = self.params[i]
+        return self.offsets[i], self.offsets[i] + p.numel()
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def refresh_bf16(self):
+        if self.bf16 is not None:
+            from mi355x_dp.ops.functional import cast_bf16_
+            cast_bf16_(self.data, self.bf16)
+
+    def reattach_grads(self):
+        """Re-point .grad at the flat views (after user code set them to None)."""
+        for p, o in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr():
+                p.grad = _kernel_view(self.grad, o, tuple(p.shape))
+
+
+class FlatBuffers:
+    """Flat fp32 storage for floating-point module buffers (BN running stats) so the
+    per-forward ``broadcast_buffers`` of DDP is one collective."""
+
+    def __init__(self, buffers: Sequence[torch.Tensor]):
+        self.buffers = [b for b in buffers if b.is_floating_point()]
+        self.others = [b for b in buffers if not b.is_floating_point()]
+        n = sum(b.numel() for b in self.buffers)
+        dev = self.buffers[0].device if self.buffers else torch.device("cpu")
+        self.data = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for b in self.buffers:
+                v = self.data[off:off + b.numel()].view(b.shape)
+                v.copy_(b)
+                b.data = v
+                off += b.numel()

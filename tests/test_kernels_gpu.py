@@ -1,0 +1,226 @@
+"""Numerics of every native HIP kernel against a plain PyTorch fp32 reference of the
+same op (inputs rounded to bf16 first, so only kernel arithmetic is compared).
+Shapes cover every ResNet-18/50 conv geometry class."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from mi355x_dp.ops import _lib
+    _lib.load(True)  # fail loudly if the extension is missing
+    torch.manual_seed(0)
+
+
+def rel_err(a, b):
+    a = a.detach().float()
+    b = b.detach().float()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-6))
+
+
+CONV_SHAPES = [
+    # N, C, H, K, R, stride, pad
+    (4, 64, 56, 64, 1, 1, 0),
+    (4, 64, 56, 64, 3, 1, 1),
+    (4, 64, 56, 256, 1, 1, 0),
+    (4, 256, 56, 128, 1, 1, 0),
+    (4, 128, 56, 128, 3, 2, 1),
+    (4, 256, 56, 512, 1, 2, 0),
+    (2, 512, 14, 512, 3, 1, 1),
+    (3, 1024, 7, 2048, 1, 1, 0),
+    (2, 128, 9, 192, 3, 1, 1),   # odd spatial / non-power-of-2 Cout
+    (5, 64, 8, 128, 3, 2, 1),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_bwd(shape):
+    from mi355x_dp.ops import conv2d
+    N, C, H, K, R, s, p = shape
+    x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, R, device="cuda") * (2.0 / (C * R * R)) ** 0.5).to(BF).float()
+    w = w.contiguous(memory_format=CL).requires_grad_(True)
+    x.requires_grad_(True)
+    y = conv2d(x, w, None, s, p)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, p)
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < 1e-2
+    gy = torch.randn_like(yr).to(BF).float()
+    y.backward(gy.to(BF).contiguous(memory_format=CL))
+    yr.backward(gy)
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+
+
+def test_conv_stem_im2col():
+    from mi355x_dp.ops import conv2d
+    x = torch.randn(4, 3, 64, 64, device="cuda").to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(64, 3, 7, 7, device="cuda") * 0.1).to(BF).float().contiguous(memory_format=CL).requires_grad_()
+    y = conv2d(x, w, None, 2, 3)
+    wr = w.detach().clone().requires_grad_()
+    yr = F.conv2d(x.float(), wr, None, 2, 3)
+    assert rel_err(y, yr) < 1e-2
+    g = torch.randn_like(yr).to(BF).float()
+    y.backward(g.to(BF).contiguous(memory_format=CL))
+    yr.backward(g)
+    assert rel_err(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_batchnorm_act(relu, res, C):
+    from mi355x_dp.ops import batch_norm_act
+    N, H = 8, 7
+    x = (torch.randn(N, C, H, H, device="cuda") * 3 + 1).to(BF).contiguous(memory_format=CL).requires_grad_()
+    r = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL).requires_grad_() if res else None
+    gamma = torch.rand(C, device="cuda").add_(0.5).requires_grad_()
+    beta = torch.randn(C, device="cuda").requires_grad_()
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    y = batch_norm_act(x, gamma, beta, rm, rv, nbt, True, 0.1, 1e-5, relu=relu, residual=r)
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    gr, br = gamma.detach().clone().requires_grad_(), beta.detach().clone().requires_grad_()
+    rm2, rv2 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    yr = F.batch_norm(xr, rm2, rv2, gr, br, True, 0.1, 1e-5)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    assert rel_err(y, yr) < 1e-2
+    assert torch.allclose(rm, rm2, rtol=1e-3, atol=1e-3) and torch.allclose(rv, rv2, rtol=1e-3, atol=1e-3)
+    assert int(nbt) == 1
+    g = torch.randn_like(yr).to(BF).float()
+    y.backward(g.to(BF).contiguous(memory_format=CL))
+    yr.backward(g)
+    assert rel_err(x.grad, xr.grad) < 3e-2
+    assert rel_err(gamma.grad, gr.grad) < 1e-2
+    assert rel_err(beta.grad, br.grad) < 1e-2
+    if res:
+        assert rel_err(r.grad, rr.grad) < 1e-2
+    # eval path
+    y2 = batch_norm_act(x.detach(), gamma.detach(), beta.detach(), rm, rv, None, False, 0.1, 1e-5, relu=relu)
+    y2r = F.batch_norm(x.detach().float(), rm, rv, gamma.detach(), beta.detach(), False, 0.1, 1e-5)
+    if relu:
+        y2r = F.relu(y2r)
+    assert rel_err(y2, y2r) < 1e-2
+
+
+def test_maxpool_gap():
+    from mi355x_dp.ops import global_avg_pool, max_pool2d
+    x = torch.randn(4, 64, 56, 56, device="cuda").to(BF).contiguous(memory_format=CL).requires_grad_()
+    y = max_pool2d(x, 3, 2, 1)
+    xr = x.detach().float().requires_grad_()
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y.float(), yr)
+    g = torch.randn_like(yr).to(BF).float()
+    y.backward(g.to(BF).contiguous(memory_format=CL))
+    yr.backward(g)
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    z = torch.randn(4, 2048, 7, 7, device="cuda").to(BF).contiguous(memory_format=CL).requires_grad_()
+    p = global_avg_pool(z)
+    zr = z.detach().float().requires_grad_()
+    pr = zr.mean(dim=(2, 3))
+    assert rel_err(p, pr) < 1e-2
+    gg = torch.randn_like(pr)
+    p.backward(gg.to(BF))
+    pr.backward(gg)
+    assert rel_err(z.grad, zr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 2048, 1000), (37, 512, 10), (128, 768, 3072)])
+def test_linear(M, K, N):
+    from mi355x_dp.ops import linear
+    x = torch.randn(M, K, device="cuda").to(BF).requires_grad_()
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(BF).float().requires_grad_()
+    b = torch.randn(N, device="cuda").requires_grad_()
+    y = linear(x, w, b)
+    xr, wr, br = x.detach().float().requires_grad_(), w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = F.linear(xr, wr, br)
+    assert rel_err(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+    assert rel_err(b.grad, br.grad) < 1e-3
+
+
+def test_cross_entropy():
+    from mi355x_dp.ops import cross_entropy
+    lg = (torch.randn(64, 1000, device="cuda") * 3).requires_grad_()
+    y = torch.randint(0, 1000, (64,), device="cuda")
+    l = cross_entropy(lg, y)
+    lr = lg.detach().clone().requires_grad_()
+    l2 = F.cross_entropy(lr, y)
+    assert abs(float(l) - float(l2)) < 1e-4 * max(1.0, abs(float(l2)))
+    (l * 2).backward()
+    (l2 * 2).backward()
+    assert rel_err(lg.grad, lr.grad) < 1e-2
+
+
+def test_sgd_flat_matches_torch():
+    from mi355x_dp.ops import sgd_flat_
+    n = 100_003
+    p = torch.randn(n, device="cuda")
+    p16 = torch.empty(n, dtype=BF, device="cuda")
+    buf = torch.zeros(n, device="cuda")
+    ref = torch.nn.Parameter(p.clone())
+    opt = torch.optim.SGD([ref], lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for step in range(3):
+        g = torch.randn(n, device="cuda")
+        sgd_flat_(p, g * 2, buf, p16, 0.1, 0.9, 0.0, 1e-4, True, first_step=(step == 0), grad_scale=0.5)
+        ref.grad = g.clone()
+        opt.step()
+    assert torch.allclose(p, ref.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(p16.float(), p, rtol=1e-2, atol=1e-2)
+
+
+def test_augment_pipeline():
+    from mi355x_dp.ops import augment
+    u8 = torch.randint(0, 256, (8, 32, 32, 3), dtype=torch.uint8, device="cuda")
+    mean, std = (0.4914, 0.4822, 0.4465), (0.2023, 0.1994, 0.2010)
+    x = augment(u8, 3, mean, std, pad=0, flip=False, seed=3)
+    ref = (u8.float().div(255).permute(0, 3, 1, 2) - torch.tensor(mean, device="cuda").view(1, 3, 1, 1)) \
+        / torch.tensor(std, device="cuda").view(1, 3, 1, 1)
+    assert rel_err(x, ref) < 1e-2
+    xa = augment(u8, 3, mean, std, pad=4, flip=True, seed=3)
+    xb = augment(u8, 3, mean, std, pad=4, flip=True, seed=3)
+    assert torch.equal(xa, xb)  # deterministic per seed
+
+
+def test_resnet18_train_step_matches_fp32():
+    """One full fwd+bwd of ResNet-18 on the native path vs an fp32 PyTorch run of the same weights."""
+    from mi355x_dp.models import resnet18
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).cuda()
+    ref = resnet18(num_classes=10)
+    ref.load_state_dict(m.state_dict())
+    ref = ref.cuda()
+    x = torch.randn(8, 3, 64, 64, device="cuda")
+    y = torch.randint(0, 10, (8,), device="cuda")
+    out = m(x)
+    from mi355x_dp.ops import cross_entropy
+    loss = cross_entropy(out, y)
+    loss.backward()
+    # fp32 reference through stock torch ops (layers fall back to nn math on CPU)
+    ref_cpu = resnet18(num_classes=10)
+    ref_cpu.load_state_dict(m.state_dict())
+    out_r = ref_cpu(x.cpu())
+    loss_r = F.cross_entropy(out_r, y.cpu())
+    loss_r.backward()
+    assert abs(float(loss) - float(loss_r)) < 0.05 * max(1.0, abs(float(loss_r)))
+    g = m.fc.weight.grad.cpu()
+    gr = ref_cpu.fc.weight.grad
+    assert rel_err(g, gr) < 0.1
+    g1 = m.conv1.weight.grad.cpu()
+    g1r = ref_cpu.conv1.weight.grad
+    assert rel_err(g1, g1r) < 0.15
