@@ -11,6 +11,7 @@
 //                                        hflip + normalize -> bf16 NHWC, on the GPU
 //   stem im2col (C=3 input)           -> im2col_nhwc
 #include "common.h"
+#include <algorithm>
 
 namespace {
 constexpr int NT = 256;

@@ -10,6 +10,7 @@
 // The ReLU mask is recovered from the saved output y, so no mask tensor exists.
 // All loads/stores are 16-byte vectors (8 bf16 per lane).
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -70,17 +71,41 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const bf16_t* __restrict__
   block_reduce_store(s, q, part, C, cbase, g);
 }
 
-// training-mode finalize: one thread per channel
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C, float eps, float momentum,
+// Reduce the [nblk][2][C] partial slab for 64 consecutive channels per block:
+// 1024 threads = 64 channel lanes x 16 row groups, coalesced 256-B row reads,
+// fp64 accumulation, LDS tree over the 16 groups.  Result in (s, q) of tid<64.
+constexpr int FIN_T = 1024, FIN_G = FIN_T / 64;
+
+__device__ __forceinline__ bool slab_reduce64(const float* __restrict__ part, int nblk, int C, double& s, double& q) {
+  __shared__ double red[2][FIN_G][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int i = rg; i < nblk; i += FIN_G) {
+      a += part[(size_t)(2 * i) * C + c];
+      b += part[(size_t)(2 * i + 1) * C + c];
+    }
+  }
+  red[0][rg][cl] = a;
+  red[1][rg][cl] = b;
+  __syncthreads();
+  if (rg != 0) return false;
+  for (int g = 1; g < FIN_G; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
+  s = a; q = b;
+  return c < C;
+}
+
+// training-mode finalize
+__global__ __launch_bounds__(FIN_T) void bn_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C, float eps, float momentum,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                    float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) nbt[0] += 1;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) { s += part[(size_t)(2 * b) * C + c]; q += part[(size_t)(2 * b + 1) * C + c]; }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+  double s, q;
+  if (!slab_reduce64(part, nblk, C, s, q)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double mean = s / M;
   double var = q / M - mean * mean;
   if (var < 0) var = 0;
@@ -166,14 +191,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(const bf16_t* __restri
 }
 
 // -> dgamma/dbeta (+=) and coef[0..2][C] so that dx = coef0*dz + coef1*x + coef2
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C,
+__global__ __launch_bounds__(FIN_T) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) { s += part[(size_t)(2 * b) * C + c]; q += part[(size_t)(2 * b + 1) * C + c]; }
+  double s, q;
+  if (!slab_reduce64(part, nblk, C, s, q)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float is = invstd[c];
   const float sum_dz = (float)s;
   const float sum_dz_xhat = (float)q * is;
@@ -206,9 +230,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
       for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
     }
     if (dres) ((uint4*)dres)[v] = pack8(d);
-    float o[8];
+    float k0[8], k1[8], k2[8], o[8];
+    *(float4*)&k0[0] = *(const float4*)(coef + c); *(float4*)&k0[4] = *(const float4*)(coef + c + 4);
+    *(float4*)&k1[0] = *(const float4*)(coef + C + c); *(float4*)&k1[4] = *(const float4*)(coef + C + c + 4);
+    *(float4*)&k2[0] = *(const float4*)(coef + 2 * C + c); *(float4*)&k2[4] = *(const float4*)(coef + 2 * C + c + 4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = coef[c + j] * d[j] + coef[C + c + j] * xv[j] + coef[2 * C + c + j];
+    for (int j = 0; j < 8; ++j) o[j] = k0[j] * d[j] + k1[j] * xv[j] + k2[j];
     ((uint4*)dx)[v] = pack8(o);
   }
 }
@@ -228,9 +255,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const bf16_t* __restric
       for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
     }
     if (dres) ((uint4*)dres)[v] = pack8(d);
-    float o[8];
+    float o[8], sc[8];
+    *(float4*)&sc[0] = *(const float4*)(scale + c); *(float4*)&sc[4] = *(const float4*)(scale + c + 4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = scale[c + j] * d[j];
+    for (int j = 0; j < 8; ++j) o[j] = sc[j] * d[j];
     ((uint4*)dx)[v] = pack8(o);
   }
 }
@@ -244,7 +272,7 @@ inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3&
   SlabGeom g = slab_geom(C);
   int ncs = C / g.cw;
   // ~2048 blocks in total, each handling >= 4*rp rows
-  int target = std::max(1, 2048 / ncs);
+  int target = std::max(1, 1024 / ncs);
   rows_per_block = std::max(g.rp * 4, cdiv(M, target));
   rows_per_block = cdiv(rows_per_block, g.rp) * g.rp;
   nblk = cdiv(M, rows_per_block);
@@ -268,7 +296,7 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
   int nblk, rpb; dim3 grid;
   slab_launch_dims(M, C, nblk, rpb, grid);
   hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nblk, M, C, eps, momentum,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, part, nblk, M, C, eps, momentum,
                      gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
@@ -297,7 +325,7 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
   slab_launch_dims(M, C, nblk, rpb, grid);
   hipLaunchKernelGGL(bn_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
                      (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nblk, M, C, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, part, nblk, M, C, gamma,
                      save_mean, save_invstd, dgamma, dbeta, coef);
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,

@@ -161,7 +161,7 @@ def test_cross_entropy():
     l = cross_entropy(lg, y)
     lr = lg.detach().clone().requires_grad_()
     l2 = F.cross_entropy(lr, y)
-    assert abs(float(l) - float(l2)) < 1e-4 * max(1.0, abs(float(l2)))
+    assert abs(float(l.detach()) - float(l2)) < 1e-4 * max(1.0, abs(float(l2)))
     (l * 2).backward()
     (l2 * 2).backward()
     assert rel_err(lg.grad, lr.grad) < 1e-2
@@ -198,29 +198,29 @@ def test_augment_pipeline():
 
 
 def test_resnet18_train_step_matches_fp32():
-    """One full fwd+bwd of ResNet-18 on the native path vs an fp32 PyTorch run of the same weights."""
+    """One full fwd+bwd of ResNet-18 on the native bf16 path vs an fp32 PyTorch run of the same
+    weights.  At this tiny batch bf16 itself is lossy through 17 BN layers, so every gradient must be
+    within 1.5x (+0.02) of the error that STOCK PyTorch bf16 (MIOpen) makes on the same problem."""
     from mi355x_dp.models import resnet18
+    from mi355x_dp.models.stock import stock_resnet
+    from mi355x_dp.ops import cross_entropy
     torch.manual_seed(0)
     m = resnet18(num_classes=10).cuda()
-    ref = resnet18(num_classes=10)
-    ref.load_state_dict(m.state_dict())
-    ref = ref.cuda()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
     x = torch.randn(8, 3, 64, 64, device="cuda")
     y = torch.randint(0, 10, (8,), device="cuda")
-    out = m(x)
-    from mi355x_dp.ops import cross_entropy
-    loss = cross_entropy(out, y)
+    loss = cross_entropy(m(x), y)
     loss.backward()
-    # fp32 reference through stock torch ops (layers fall back to nn math on CPU)
-    ref_cpu = resnet18(num_classes=10)
-    ref_cpu.load_state_dict(m.state_dict())
-    out_r = ref_cpu(x.cpu())
-    loss_r = F.cross_entropy(out_r, y.cpu())
+    ref = stock_resnet("resnet18", 10).cuda()
+    ref.load_state_dict(sd)
+    loss_r = F.cross_entropy(ref(x), y)
     loss_r.backward()
-    assert abs(float(loss) - float(loss_r)) < 0.05 * max(1.0, abs(float(loss_r)))
-    g = m.fc.weight.grad.cpu()
-    gr = ref_cpu.fc.weight.grad
-    assert rel_err(g, gr) < 0.1
-    g1 = m.conv1.weight.grad.cpu()
-    g1r = ref_cpu.conv1.weight.grad
-    assert rel_err(g1, g1r) < 0.15
+    st = stock_resnet("resnet18", 10).cuda().to(BF).to(memory_format=CL)
+    st.load_state_dict(sd)
+    F.cross_entropy(st(x.to(BF).contiguous(memory_format=CL)).float(), y).backward()
+    assert abs(float(loss.detach()) - float(loss_r.detach())) < 0.05 * max(1.0, abs(float(loss_r.detach())))
+    pn, pr, ps = dict(m.named_parameters()), dict(ref.named_parameters()), dict(st.named_parameters())
+    for n in pr:
+        e_native = rel_err(pn[n].grad, pr[n].grad)
+        e_stock = rel_err(ps[n].grad, pr[n].grad)
+        assert e_native <= 1.5 * e_stock + 0.02, (n, e_native, e_stock)
