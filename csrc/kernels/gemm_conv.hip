@@ -49,8 +49,11 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 struct ConvGeom {
   int H, W, Cs;      // gathered tensor spatial dims / channels (NHWC)
   int P, Q;          // "row pixel" spatial dims: rows index (n, p, q)
-  int S, stride, pad;
+  int R, S, stride, pad;
   FastDiv fPQ, fQ, fS, fCpt;  // divisors: P*Q, Q, S, Cs/64 (channel chunks per tap)
+  // mode 3 (strided dgrad, one parity class per blockIdx.y): class row dims
+  int Pc[4], Qc[4];
+  FastDiv fPQc[4], fQc[4];
 };
 
 struct NTArgs {
@@ -58,11 +61,13 @@ struct NTArgs {
   const bf16_t* B;
   void* C;
   const float* bias;
+  float* stats;      // optional [tiles_m][2][N] per-channel (sum, sumsq) partials of the bf16 output
   int M, N, K;
   int lda, ldb, ldc;
   int mode;
   int out_f32;
   int accumulate;
+  int tiles_m;       // m-tiles per class (mode 3) / total (others)
   ConvGeom g;
 };
 
@@ -80,22 +85,42 @@ struct TNArgs {
 constexpr int BK = 64;
 
 // ----------------------------------------------------------------- NT kernel
+// modes: 0 plain GEMM, 1 conv fwd, 2 conv dgrad (stride-1 or masked), 3 conv dgrad
+// decomposed by output parity class (stride 2: only the taps that hit real dY pixels).
 template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * (BM + BN) * 8];
+  constexpr int SMEM_U4 = 2 * (BM + BN) * 8;
+  __shared__ __attribute__((aligned(16))) uint4 smem[SMEM_U4];
   uint4* As = smem;                 // [2][BM][8]
   uint4* Bs = smem + 2 * BM * 8;    // [2][BN][8]
 
   const int nbn = (a.N + BN - 1) / BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
+  const int tm = tile / nbn;
+  const int m0 = tm * BM, n0 = (tile % nbn) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int chk = tid & 7;
   const int rbase = tid >> 3;  // + 32*i
+
+  // ---- class geometry (mode 3)
+  int cls = 0, ph = 0, pw = 0, r0 = 0, s0 = 0, nr = a.g.R, ns = a.g.S, dh = 0, dw = 0;
+  int Mrows = a.M;
+  FastDiv fPQ = a.g.fPQ, fQ = a.g.fQ;
+  if (a.mode == 3) {
+    cls = blockIdx.y;
+    ph = cls / a.g.stride; pw = cls - ph * a.g.stride;
+    r0 = (ph + a.g.pad) % a.g.stride; s0 = (pw + a.g.pad) % a.g.stride;
+    nr = r0 < a.g.R ? (a.g.R - r0 + a.g.stride - 1) / a.g.stride : 0;
+    ns = s0 < a.g.S ? (a.g.S - s0 + a.g.stride - 1) / a.g.stride : 0;
+    dh = (ph + a.g.pad - r0) / a.g.stride; dw = (pw + a.g.pad - s0) / a.g.stride;
+    fPQ = a.g.fPQc[cls]; fQ = a.g.fQc[cls];
+    Mrows = (a.M / (a.g.P * a.g.Q)) * a.g.Pc[cls] * a.g.Qc[cls];
+  }
+  if (m0 >= Mrows) return;
 
   // ---- per-thread A row geometry (fixed over the K loop)
   int a_m[A_CH], a_img[A_CH], a_hb[A_CH], a_wb[A_CH];
@@ -104,43 +129,51 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
     int m = m0 + rbase + 32 * i;
     a_m[i] = m;
     if (a.mode != 0) {
-      uint32_t mm = m < a.M ? (uint32_t)m : 0u;
-      uint32_t img = fdiv(mm, a.g.fPQ);
-      uint32_t rem = mm - img * a.g.fPQ.d;
-      uint32_t p = fdiv(rem, a.g.fQ);
-      uint32_t q = rem - p * a.g.fQ.d;
+      uint32_t mm = m < Mrows ? (uint32_t)m : 0u;
+      uint32_t img = fdiv(mm, fPQ);
+      uint32_t rem = mm - img * fPQ.d;
+      uint32_t p = fdiv(rem, fQ);
+      uint32_t q = rem - p * fQ.d;
       a_img[i] = (int)img;
-      if (a.mode == 1) { a_hb[i] = (int)p * a.g.stride - a.g.pad; a_wb[i] = (int)q * a.g.stride - a.g.pad; }
-      else             { a_hb[i] = (int)p + a.g.pad;             a_wb[i] = (int)q + a.g.pad; }
+      if (a.mode == 1)      { a_hb[i] = (int)p * a.g.stride - a.g.pad; a_wb[i] = (int)q * a.g.stride - a.g.pad; }
+      else if (a.mode == 2) { a_hb[i] = (int)p + a.g.pad;             a_wb[i] = (int)q + a.g.pad; }
+      else                  { a_hb[i] = (int)p + dh;                  a_wb[i] = (int)q + dw; }
     } else {
       a_img[i] = 0; a_hb[i] = 0; a_wb[i] = 0;
     }
   }
 
-  const int nk = (a.K + BK - 1) / BK;
+  const int cpt = (int)a.g.fCpt.d;
+  const int nk = (a.mode == 3) ? nr * ns * cpt : (a.K + BK - 1) / BK;
   uint4 ra[A_CH], rb[B_CH];
 
   auto load_tiles = [&](int kt) {
-    int tap = 0, c = 0, r = 0, s = 0;
+    int c = 0, r = 0, s = 0, kB = kt * BK + chk * 8;
+    int tr = 0, ts = 0;
     if (a.mode != 0) {
-      tap = (int)fdiv((uint32_t)kt, a.g.fCpt);
-      c = (kt - tap * (int)a.g.fCpt.d) * 64 + chk * 8;
-      r = (int)fdiv((uint32_t)tap, a.g.fS);
-      s = tap - r * a.g.S;
+      const int tap = (int)fdiv((uint32_t)kt, a.g.fCpt);
+      c = (kt - tap * cpt) * 64 + chk * 8;
+      if (a.mode == 3) {
+        tr = tap / ns; ts = tap - tr * ns;
+        r = r0 + a.g.stride * tr; s = s0 + a.g.stride * ts;
+      } else {
+        r = (int)fdiv((uint32_t)tap, a.g.fS);
+        s = tap - r * a.g.S;
+      }
+      kB = (r * a.g.S + s) * a.g.Cs + c;
     }
-    const int k = kt * BK + chk * 8;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const bf16_t* src = nullptr;
       if (a.mode == 0) {
-        if (a_m[i] < a.M && k < a.K) src = a.A + (size_t)a_m[i] * a.lda + k;
+        if (a_m[i] < a.M && kB < a.K) src = a.A + (size_t)a_m[i] * a.lda + kB;
       } else if (a.mode == 1) {
         int ih = a_hb[i] + r, iw = a_wb[i] + s;
-        if (a_m[i] < a.M && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
+        if (a_m[i] < Mrows && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
           src = a.A + ((size_t)(a_img[i] * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c;
-      } else {
+      } else if (a.mode == 2) {
         int th = a_hb[i] - r, tw = a_wb[i] - s;
-        bool ok = a_m[i] < a.M && th >= 0 && tw >= 0;
+        bool ok = a_m[i] < Mrows && th >= 0 && tw >= 0;
         int ih = th, iw = tw;
         if (a.g.stride != 1) {
           ok = ok && (th % a.g.stride) == 0 && (tw % a.g.stride) == 0;
@@ -148,13 +181,17 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
         }
         if (ok && ih < a.g.H && iw < a.g.W)
           src = a.A + ((size_t)(a_img[i] * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c;
+      } else {
+        int ih = a_hb[i] - tr, iw = a_wb[i] - ts;
+        if (a_m[i] < Mrows && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
+          src = a.A + ((size_t)(a_img[i] * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c;
       }
       ra[i] = src ? *(const uint4*)src : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       int n = n0 + rbase + 32 * i;
-      rb[i] = (n < a.N && k < a.K) ? *(const uint4*)(a.B + (size_t)n * a.ldb + k) : make_uint4(0, 0, 0, 0);
+      rb[i] = (n < a.N && kB < a.K) ? *(const uint4*)(a.B + (size_t)n * a.ldb + kB) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_tiles = [&](int buf) {
@@ -176,11 +213,12 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_tiles(0);
-  store_tiles(0);
-  __syncthreads();
-
   const int fr = lane & 15, fq = lane >> 4;
+  if (nk > 0) {
+    load_tiles(0);
+    store_tiles(0);
+  }
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_tiles(kt + 1);
@@ -209,25 +247,86 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds D[n = 16j + 4fq + r][m = 16i + fr]
+  // output row offset (elements) of tile row m
+  auto row_off = [&](int m) -> size_t {
+    if (a.mode != 3) return (size_t)m * a.ldc;
+    uint32_t img = fdiv((uint32_t)m, fPQ);
+    uint32_t rem = (uint32_t)m - img * fPQ.d;
+    uint32_t i = fdiv(rem, fQ);
+    uint32_t j = rem - i * fQ.d;
+    const int h = (int)i * a.g.stride + ph, w = (int)j * a.g.stride + pw;
+    return ((size_t)((int)img * a.g.P + h) * a.g.Q + w) * a.ldc;
+  };
+
+  if (a.out_f32) {
+    // ---- direct epilogue (fp32 logits etc.): lane holds D[n = 16j + 4fq + r][m = 16i + fr]
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * WM + 16 * i + fr;
-    if (m >= a.M) continue;
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * WM + 16 * i + fr;
+      if (m >= Mrows) continue;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * WN + 16 * j + 4 * fq;
-      if (n >= a.N) continue;
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      if (a.bias) { v0 += a.bias[n]; v1 += a.bias[n + 1]; v2 += a.bias[n + 2]; v3 += a.bias[n + 3]; }
-      if (a.out_f32) {
-        float* dst = (float*)a.C + (size_t)m * a.ldc + n;
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WN + 16 * j + 4 * fq;
+        if (n >= a.N) continue;
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if (a.bias) { v0 += a.bias[n]; v1 += a.bias[n + 1]; v2 += a.bias[n + 2]; v3 += a.bias[n + 3]; }
+        float* dst = (float*)a.C + row_off(m) + n;
         if (a.accumulate) { float4 o = *(float4*)dst; v0 += o.x; v1 += o.y; v2 += o.z; v3 += o.w; }
         *(float4*)dst = make_float4(v0, v1, v2, v3);
-      } else {
-        bf16_t* dst = (bf16_t*)a.C + (size_t)m * a.ldc + n;
-        *(uint2*)dst = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
       }
+    }
+    return;
+  }
+
+  // ---- bf16 epilogue staged through LDS: full 16-byte row chunks to HBM (+ BN partial stats)
+  constexpr int CST = BN + 8;                    // padded row stride (elements): 16-B aligned rows
+  bf16_t* Ct = (bf16_t*)smem;                    // [BM][CST]
+  float* Sred = (float*)(smem) + (BM * CST) / 2; // [rows_par][2][BN] stats scratch
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int ml = wm * WM + 16 * i + fr;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nl = wn * WN + 16 * j + 4 * fq;
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if (a.bias && n0 + nl < a.N) {
+        v0 += a.bias[n0 + nl]; v1 += a.bias[n0 + nl + 1]; v2 += a.bias[n0 + nl + 2]; v3 += a.bias[n0 + nl + 3];
+      }
+      *(uint2*)&Ct[ml * CST + nl] = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;          // 16-B chunks per row
+  constexpr int RPP = 256 / CPR;       // rows per pass
+  const int cc = tid % CPR, rr = tid / CPR;
+  const int n = n0 + cc * 8;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int ml = rr; ml < BM; ml += RPP) {
+    const int m = m0 + ml;
+    if (m >= Mrows) break;
+    const uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
+    if (n < a.N) *(uint4*)((bf16_t*)a.C + row_off(m) + n) = v;
+    if (a.stats) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
+    }
+  }
+  if (a.stats) {
+    // reduce the RPP row groups of each column chunk through LDS (Sred is disjoint from Ct)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      Sred[(rr * 2 + 0) * BN + cc * 8 + q] = s1[q];
+      Sred[(rr * 2 + 1) * BN + cc * 8 + q] = s2[q];
+    }
+    __syncthreads();
+    const int prow = blockIdx.y * a.tiles_m + tm;
+    for (int c = tid; c < 2 * BN; c += 256) {
+      const int which = c / BN, col = c - which * BN;
+      float t = 0.f;
+      for (int g = 0; g < RPP; ++g) t += Sred[(g * 2 + which) * BN + col];
+      if (n0 + col < a.N) a.stats[((size_t)prow * 2 + which) * a.N + n0 + col] = t;
     }
   }
 }
@@ -402,9 +501,9 @@ __global__ void wtrans_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__
   }
 }
 
-ConvGeom make_geom(int H, int W, int Cs, int P, int Q, int S, int stride, int pad) {
-  ConvGeom g;
-  g.H = H; g.W = W; g.Cs = Cs; g.P = P; g.Q = Q; g.S = S; g.stride = stride; g.pad = pad;
+ConvGeom make_geom(int H, int W, int Cs, int P, int Q, int S, int stride, int pad, int R = 1) {
+  ConvGeom g{};
+  g.H = H; g.W = W; g.Cs = Cs; g.P = P; g.Q = Q; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
   g.fPQ = make_fastdiv((uint32_t)(P * Q));
   g.fQ = make_fastdiv((uint32_t)Q);
   g.fS = make_fastdiv((uint32_t)S);
@@ -413,17 +512,33 @@ ConvGeom make_geom(int H, int W, int Cs, int P, int Q, int S, int stride, int pa
 }
 
 template <int BM, int BN>
-hipError_t launch_nt(const NTArgs& a, hipStream_t st) {
-  int grid = cdiv(a.M, BM) * cdiv(a.N, BN);
-  hipLaunchKernelGGL((nt_kernel<BM, BN>), dim3(grid), dim3(256), 0, st, a);
+hipError_t launch_nt(NTArgs& a, hipStream_t st) {
+  int classes = 1, mrows = a.M;
+  if (a.mode == 3) {
+    classes = a.g.stride * a.g.stride;
+    mrows = 0;
+    const int nimg = a.M / (a.g.P * a.g.Q);
+    for (int c = 0; c < classes; ++c) mrows = std::max(mrows, nimg * a.g.Pc[c] * a.g.Qc[c]);
+  }
+  a.tiles_m = cdiv(mrows, BM);
+  int grid = a.tiles_m * cdiv(a.N, BN);
+  hipLaunchKernelGGL((nt_kernel<BM, BN>), dim3(grid, classes), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
+// tile choice shared with the host-side stats-slab sizing (mi_nt_tile_m)
+int nt_choice(int M, int N) {
+  if (N <= 64) return 1;                                         // 128x64
+  if ((int64_t)cdiv(M, 128) * cdiv(N, 128) < 512) return 2;     // 64x64 (fill 256 CUs)
+  return 0;                                                      // 128x128
+}
+
 hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
-  if (a.N <= 64) return launch_nt<128, 64>(a, st);
-  // small-M problems (late ResNet stages / fc): keep enough blocks to fill 256 CUs
-  if ((int64_t)cdiv(a.M, 128) * cdiv(a.N, 128) < 512) return launch_nt<64, 64>(a, st);
-  return launch_nt<128, 128>(a, st);
+  switch (nt_choice(a.M, a.N)) {
+    case 1: return launch_nt<128, 64>(a, st);
+    case 2: return launch_nt<64, 64>(a, st);
+    default: return launch_nt<128, 128>(a, st);
+  }
 }
 
 template <int BM, int BN>
@@ -452,15 +567,23 @@ hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
 
 // ============================================================== C ABI
 // Conv forward: x NHWC [Nb,H,W,C] bf16, w [K][R][S][C] bf16, y NHWC [Nb,P,Q,K].
-MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bias,
+// Rows of the per-channel statistics slab written by a conv/GEMM forward with M rows, N cols.
+MI_API int mi_nt_stat_rows(int M, int N) {
+  const int bm = nt_choice(M, N) == 2 ? 64 : 128;
+  return cdiv(M, bm);
+}
+
+// Conv forward: x NHWC [Nb,H,W,C] bf16, w [K][R][S][C] bf16, y NHWC [Nb,P,Q,K].
+// stats (optional, bf16 output only): fp32 [mi_nt_stat_rows(M,K)][2][K] partial (sum, sumsq).
+MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bias, float* stats,
                          int Nb, int H, int W, int C, int K, int R, int S,
                          int stride, int pad, int P, int Q, int out_f32, hipStream_t st) {
-  if (C % 64 != 0) return (int)hipErrorInvalidValue;
+  if (C % 64 != 0 || K % 8 != 0) return (int)hipErrorInvalidValue;
   NTArgs a{};
-  a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias;
+  a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias; a.stats = stats;
   a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
   a.lda = 0; a.ldb = a.K; a.ldc = K; a.mode = 1; a.out_f32 = out_f32; a.accumulate = 0;
-  a.g = make_geom(H, W, C, P, Q, S, stride, pad);
+  a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
   return (int)dispatch_nt(a, st);
 }
 
@@ -468,13 +591,24 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
 MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
-  if (K % 64 != 0) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || C % 8 != 0) return (int)hipErrorInvalidValue;
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
   a.lda = 0; a.ldb = a.K; a.ldc = C; a.mode = 2; a.out_f32 = 0; a.accumulate = 0;
   // gathered tensor = dy (spatial P,Q, channels K); rows = dx pixels (H, W)
-  a.g = make_geom(P, Q, K, H, W, S, stride, pad);
+  a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);
+  if (stride == 2) {
+    // parity-class decomposition: class (ph, pw) rows only visit taps r = ph+pad (mod 2)
+    a.mode = 3;
+    for (int c = 0; c < 4; ++c) {
+      const int ph = c / 2, pw = c % 2;
+      a.g.Pc[c] = (H - ph + 1) / 2;
+      a.g.Qc[c] = (W - pw + 1) / 2;
+      a.g.fPQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Pc[c] * a.g.Qc[c]));
+      a.g.fQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Qc[c]));
+    }
+  }
   return (int)dispatch_nt(a, st);
 }
 
@@ -487,7 +621,7 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
   a.M = K; a.N = R * S * C; a.K = Nb * P * Q;
   a.lda = K; a.ldb = 0; a.ldc = a.N; a.mode = 1;
-  a.g = make_geom(H, W, C, P, Q, S, stride, pad);
+  a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
   return (int)dispatch_tn(a, st);
 }
 
@@ -498,12 +632,12 @@ MI_API int mi_conv_wtrans(const void* w, void* wt, int K, int RS, int C, hipStre
 }
 
 // Plain GEMM, "NT": C[M][N] = A[M][K] * B[N][K]^T (+bias[N]); A, B bf16; C bf16 or fp32.
-MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias,
+MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias, float* stats,
                       int M, int N, int K, int lda, int ldb, int ldc,
                       int out_f32, int accumulate, hipStream_t st) {
-  if (K % 8 != 0 || N % 4 != 0) return (int)hipErrorInvalidValue;
+  if (K % 8 != 0 || N % 4 != 0 || (!out_f32 && N % 8 != 0)) return (int)hipErrorInvalidValue;
   NTArgs a{};
-  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.stats = out_f32 ? nullptr : stats;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.mode = 0; a.out_f32 = out_f32; a.accumulate = accumulate;
   a.g = make_geom(1, 1, 64, 1, 1, 1, 1, 0);

@@ -287,15 +287,20 @@ MI_API int mi_bn_partial_rows(int M, int C) {
   return nblk;
 }
 
-// Training-mode forward.  part: fp32 workspace [mi_bn_partial_rows(M,C)][2][C].
+// Training-mode forward.  part: fp32 workspace [mi_bn_partial_rows(M,C)][2][C], or -- when
+// pre_rows > 0 -- a [pre_rows][2][C] slab of (sum, sumsq) already written by the conv epilogue.
 MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C, float eps, float momentum,
                            const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                            float* save_mean, float* save_invstd, float* scale, float* shift, float* part,
-                           int relu, hipStream_t st) {
+                           int pre_rows, int relu, hipStream_t st) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
   int nblk, rpb; dim3 grid;
   slab_launch_dims(M, C, nblk, rpb, grid);
-  hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
+  if (pre_rows > 0) {
+    nblk = pre_rows;  // partials already produced by the producing conv's epilogue
+  } else {
+    hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
+  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, part, nblk, M, C, eps, momentum,
                      gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
   int64_t nvec = (int64_t)M * C / 8;

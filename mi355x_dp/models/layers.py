@@ -36,7 +36,7 @@ class Conv2d(nn.Conv2d):
 class BatchNorm2d(nn.BatchNorm2d):
     """BatchNorm2d with optional fused residual add and ReLU: ``act(bn(x) + residual)``."""
 
-    def forward(self, x, relu: bool = False, residual=None):
+    def forward(self, x, relu: bool = False, residual=None, stats=None):
         if self.momentum is None:
             eaf = 0.0
         else:
@@ -54,7 +54,7 @@ class BatchNorm2d(nn.BatchNorm2d):
                                  self.running_mean if self.track_running_stats else None,
                                  self.running_var if self.track_running_stats else None,
                                  self.num_batches_tracked if (self.training and self.track_running_stats) else None,
-                                 use_batch, eaf, self.eps, relu, residual)
+                                 use_batch, eaf, self.eps, relu, residual, stats if use_batch else None)
 
 
 class Linear(nn.Linear):
@@ -86,6 +86,17 @@ class GlobalAvgPool2d(nn.AdaptiveAvgPool2d):
 
 class ReLU(nn.ReLU):
     pass
+
+
+def conv_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = False, residual=None):
+    """act(bn(conv(x)) + residual).  On the native training path the conv epilogue also emits the
+    BN batch-statistics partials, so BN never re-reads the conv output to compute them."""
+    if (x.is_cuda and bn.training and isinstance(conv, Conv2d) and isinstance(bn, BatchNorm2d)
+            and conv.bias is None and conv.groups == 1):
+        y, st = Fm.conv2d_with_stats(x, conv.weight, _pair_square(conv.stride, "stride"),
+                                     _pair_square(conv.padding, "padding"))
+        return bn(y, relu=relu, residual=residual, stats=st)
+    return bn(conv(x), relu=relu, residual=residual)
 
 
 def to_device_input(x: torch.Tensor) -> torch.Tensor:

@@ -16,7 +16,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from .layers import BatchNorm2d, Conv2d, GlobalAvgPool2d, Linear, MaxPool2d, ReLU, to_device_input
+from .layers import BatchNorm2d, Conv2d, GlobalAvgPool2d, Linear, MaxPool2d, ReLU, conv_bn, to_device_input
 
 
 def conv3x3(in_planes, out_planes, stride=1):
@@ -42,10 +42,10 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         identity = x
-        out = self.bn1(self.conv1(x), relu=True)
+        out = conv_bn(self.conv1, self.bn1, x, relu=True)
         if self.downsample is not None:
-            identity = self.downsample[1](self.downsample[0](x))
-        return self.bn2(self.conv2(out), relu=True, residual=identity)
+            identity = conv_bn(self.downsample[0], self.downsample[1], x)
+        return conv_bn(self.conv2, self.bn2, out, relu=True, residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -66,11 +66,11 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x
-        out = self.bn1(self.conv1(x), relu=True)
-        out = self.bn2(self.conv2(out), relu=True)
+        out = conv_bn(self.conv1, self.bn1, x, relu=True)
+        out = conv_bn(self.conv2, self.bn2, out, relu=True)
         if self.downsample is not None:
-            identity = self.downsample[1](self.downsample[0](x))
-        return self.bn3(self.conv3(out), relu=True, residual=identity)
+            identity = conv_bn(self.downsample[0], self.downsample[1], x)
+        return conv_bn(self.conv3, self.bn3, out, relu=True, residual=identity)
 
 
 class ResNet(nn.Module):
@@ -117,7 +117,7 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         x = to_device_input(x)
-        x = self.bn1(self.conv1(x), relu=True)
+        x = conv_bn(self.conv1, self.bn1, x, relu=True)
         x = self.maxpool(x)
         x = self.layer1(x)
         x = self.layer2(x)

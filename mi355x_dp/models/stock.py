@@ -32,4 +32,5 @@ def stock_resnet(name: str, num_classes: int = 1000):
     R.Conv2d, R.BatchNorm2d, R.Linear, R.MaxPool2d, R.GlobalAvgPool2d = (
         nn.Conv2d, StockBN, nn.Linear, nn.MaxPool2d, StockGAP)
     R.to_device_input = lambda x: x
+    R.conv_bn = lambda conv, bn, x, relu=False, residual=None: bn(conv(x), relu=relu, residual=residual)
     return getattr(R, name)(num_classes=num_classes)

@@ -78,7 +78,7 @@ def _conv_out(h, r, stride, pad):
 # ======================================================================= conv
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding):
+    def forward(ctx, x, weight, bias, stride, padding, stats):
         N, C, H, W = x.shape
         K, _, R, S = weight.shape
         P, Q = _conv_out(H, R, stride, padding), _conv_out(W, S, stride, padding)
@@ -88,8 +88,8 @@ class _Conv2d(torch.autograd.Function):
         y = torch.empty((N, K, P, Q), dtype=BF16, device=x.device, memory_format=CL)
         col = None
         if C % 64 == 0:
-            _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), N, H, W, C, K, R, S, stride, padding,
-                      P, Q, 0, st)
+            _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), ptr(stats), N, H, W, C, K, R, S,
+                      stride, padding, P, Q, 0, st)
         else:
             # small-C stem: explicit im2col (k = (r*S+s)*C + c) + MFMA GEMM
             Kr = R * S * C
@@ -98,7 +98,8 @@ class _Conv2d(torch.autograd.Function):
             _lib.call("mi_im2col", ptr(x), ptr(col), N, H, W, C, R, S, stride, padding, P, Q, Kp, st)
             wp = torch.zeros((K, Kp), dtype=BF16, device=x.device)
             wp[:, :Kr].copy_(w16.permute(0, 2, 3, 1).reshape(K, Kr))
-            _lib.call("mi_gemm_nt", ptr(col), ptr(wp), ptr(y), ptr(None), N * P * Q, K, Kp, Kp, Kp, K, 0, 0, st)
+            _lib.call("mi_gemm_nt", ptr(col), ptr(wp), ptr(y), ptr(None), ptr(stats), N * P * Q, K, Kp, Kp, Kp, K,
+                      0, 0, st)
         if bias is not None:
             y = y + bias.to(BF16).view(1, K, 1, 1)
         ctx.geom = (N, C, H, W, K, R, S, stride, padding, P, Q)
@@ -138,19 +139,33 @@ class _Conv2d(torch.autograd.Function):
             gb = _grad_buffer(bias)
             gb.add_(dy.float().sum(dim=(0, 2, 3)))
             db = _finish_grad(bias, gb)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0):
     if not x.is_cuda:
         return F.conv2d(x, weight, bias, stride, padding)
-    return _Conv2d.apply(x, weight, bias, stride, padding)
+    return _Conv2d.apply(x, weight, bias, stride, padding, None)
+
+
+def conv2d_with_stats(x, weight, stride=1, padding=0):
+    """Conv (no bias) whose epilogue also writes per-channel (sum, sumsq) partials of its bf16
+    output -> (y, (slab, rows)); feeds ``batch_norm_act(..., stats=...)`` so BN skips its own
+    statistics pass over y (one full read of the activation saved per BN layer)."""
+    N, C, H, W = x.shape
+    K, _, R, S = weight.shape
+    P, Q = _conv_out(H, R, stride, padding), _conv_out(W, S, stride, padding)
+    rows = _lib.load().mi_nt_stat_rows(N * P * Q, K)
+    slab = torch.empty((rows, 2, K), dtype=torch.float32, device=x.device)
+    y = _Conv2d.apply(x, weight, None, stride, padding, slab)
+    return y, (slab, rows)
 
 
 # ================================================================ batch norm
 class _BatchNormAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training, momentum, eps, relu,
+                stats):
         N, C, H, W = x.shape
         M = N * H * W
         x = _nhwc(x)
@@ -162,13 +177,16 @@ class _BatchNormAct(torch.autograd.Function):
         scale = torch.empty(C, **f32)
         shift = torch.empty(C, **f32)
         if training:
-            nblk = _lib.load().mi_bn_partial_rows(M, C)
-            part = torch.empty((nblk, 2, C), **f32)
+            if stats is not None:
+                part, pre_rows = stats
+            else:
+                part = torch.empty((_lib.load().mi_bn_partial_rows(M, C), 2, C), **f32)
+                pre_rows = 0
             mean = torch.empty(C, **f32)
             invstd = torch.empty(C, **f32)
             _lib.call("mi_bn_fwd_train", ptr(x), ptr(res), ptr(y), M, C, float(eps), float(momentum),
                       ptr(weight), ptr(bias), ptr(running_mean), ptr(running_var), ptr(nbt), ptr(mean),
-                      ptr(invstd), ptr(scale), ptr(shift), ptr(part), int(relu), st)
+                      ptr(invstd), ptr(scale), ptr(shift), ptr(part), int(pre_rows), int(relu), st)
         else:
             mean = invstd = None
             _lib.call("mi_bn_fwd_eval", ptr(x), ptr(res), ptr(y), M, C, float(eps), ptr(weight), ptr(bias),
@@ -204,11 +222,11 @@ class _BatchNormAct(torch.autograd.Function):
                 db = _finish_grad(bias, gb)
         else:
             _lib.call("mi_bn_bwd_eval", ptr(dy), ptr(y), ptr(scale), ptr(dx), ptr(dres), M, C, int(ctx.relu), st)
-        return dx, dw, db, dres, None, None, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked, training, momentum, eps,
-                   relu=False, residual=None):
+                   relu=False, residual=None, stats=None):
     """y = act(BN(x) + residual).  ``momentum=None`` (cumulative average) is resolved by the caller."""
     if not x.is_cuda:
         y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
@@ -221,7 +239,7 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_track
         raise ValueError("eval-mode batch_norm without running statistics")
     return _BatchNormAct.apply(x, weight, bias, residual, running_mean, running_var,
                                num_batches_tracked if training else None, bool(training), float(momentum),
-                               float(eps), bool(relu))
+                               float(eps), bool(relu), stats if training else None)
 
 
 # ==================================================================== pooling
@@ -306,7 +324,8 @@ class _Linear(torch.autograd.Function):
                 bp = torch.zeros(Np, dtype=torch.float32, device=x.device)
                 bp[:N].copy_(bias)
         y = torch.empty((M, Np), dtype=torch.float32, device=x.device)
-        _lib.call("mi_gemm_nt", ptr(x2), ptr(w16), ptr(y), ptr(bp), M, Np, Kd, Kd, Kd, Np, 1, 0, stream_of(x))
+        _lib.call("mi_gemm_nt", ptr(x2), ptr(w16), ptr(y), ptr(bp), ptr(None), M, Np, Kd, Kd, Kd, Np, 1, 0,
+                  stream_of(x))
         if Np != N:
             y = y[:, :N].contiguous()
         ctx.save_for_backward(x2, weight, w16)
@@ -335,7 +354,7 @@ class _Linear(torch.autograd.Function):
             # dX[M][Kd] = dY[M][Np] * W[Np][Kd]  ->  NT with B = W^T [Kd][Np]
             wt = w16.t().contiguous()
             dxf = torch.empty((M, Kd), dtype=BF16, device=dy.device)
-            _lib.call("mi_gemm_nt", ptr(dy2), ptr(wt), ptr(dxf), ptr(None), M, Kd, Np, Np, Np, Kd, 0, 0, st)
+            _lib.call("mi_gemm_nt", ptr(dy2), ptr(wt), ptr(dxf), ptr(None), ptr(None), M, Kd, Np, Np, Np, Kd, 0, 0, st)
             dx = dxf.reshape(ctx.in_shape).to(ctx.in_dtype)
         if ctx.needs_input_grad[1]:
             g = _grad_buffer(weight)

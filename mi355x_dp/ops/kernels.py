@@ -8,16 +8,17 @@ import ctypes
 U32 = ctypes.c_uint32
 
 # gemm_conv.hip
-signature("mi_conv2d_fwd", P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_conv2d_fwd", P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_nt_stat_rows", I, I)
 signature("mi_conv2d_dgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_wgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv_wtrans", P, P, I, I, I, P)
-signature("mi_gemm_nt", P, P, P, P, I, I, I, I, I, I, I, I, P)
+signature("mi_gemm_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, P)
 signature("mi_gemm_tn", P, P, P, I, I, I, I, I, I, P)
 
 # norm_act.hip
 signature("mi_bn_partial_rows", I, I)
-signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, I, P)
+signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_bn_fwd_eval", P, P, P, I, I, F, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_train", P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_eval", P, P, P, P, P, I, I, I, P)

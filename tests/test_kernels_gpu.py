@@ -224,3 +224,19 @@ def test_resnet18_train_step_matches_fp32():
         e_native = rel_err(pn[n].grad, pr[n].grad)
         e_stock = rel_err(ps[n].grad, pr[n].grad)
         assert e_native <= 1.5 * e_stock + 0.02, (n, e_native, e_stock)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 56, 256, 1, 1, 0), (4, 128, 28, 128, 3, 2, 1), (3, 3, 32, 64, 7, 2, 3)])
+def test_conv_bn_fused_stats(shape):
+    """conv epilogue statistics + BN (fused path) == conv then BN with its own stats pass."""
+    from mi355x_dp.models.layers import BatchNorm2d, Conv2d, conv_bn
+    N, C, H, K, R, s, p = shape
+    torch.manual_seed(1)
+    conv = Conv2d(C, K, R, s, p, bias=False).cuda()
+    bn1, bn2 = BatchNorm2d(K).cuda(), BatchNorm2d(K).cuda()
+    x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    y_fused = conv_bn(conv, bn1, x, relu=True)
+    y_ref = bn2(conv(x), relu=True)
+    assert rel_err(y_fused, y_ref) < 1e-2
+    assert torch.allclose(bn1.running_mean, bn2.running_mean, rtol=1e-3, atol=1e-4)
+    assert torch.allclose(bn1.running_var, bn2.running_var, rtol=1e-3, atol=1e-4)
