@@ -96,6 +96,30 @@ __device__ __forceinline__ bool slab_reduce64(const float* __restrict__ part, in
   return c < C;
 }
 
+// Stage-1 of a tall slab: block (cg, split) reduces rows [split*rows_per, ...) of 64 channels
+// into out[split][2][C] (fp32, deterministic; no atomics).  Stage 2 is the finalize kernel.
+__global__ __launch_bounds__(FIN_T) void slab_split_kernel(const float* __restrict__ part, int nblk, int C,
+                                                           int rows_per, float* __restrict__ out) {
+  __shared__ double red[2][FIN_G][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int b0 = blockIdx.y * rows_per, b1 = min(nblk, b0 + rows_per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int i = b0 + rg; i < b1; i += FIN_G) {
+      a += part[(size_t)(2 * i) * C + c];
+      b += part[(size_t)(2 * i + 1) * C + c];
+    }
+  }
+  red[0][rg][cl] = a;
+  red[1][rg][cl] = b;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  for (int g = 1; g < FIN_G; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
+  out[(size_t)(2 * blockIdx.y) * C + c] = (float)a;
+  out[(size_t)(2 * blockIdx.y + 1) * C + c] = (float)b;
+}
+
 // training-mode finalize
 __global__ __launch_bounds__(FIN_T) void bn_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C, float eps, float momentum,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -279,7 +303,23 @@ inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3&
   grid = dim3(nblk, ncs);
 }
 
+// Tall slabs (e.g. one row per conv M-tile) are first reduced by a (C/64) x S grid into S rows
+// written just past the slab (callers allocate SLAB_EXTRA_ROWS spare rows), then finalized.
+constexpr int SLAB_EXTRA_ROWS = 64;
+inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const float*& fin) {
+  fin = part;
+  if (nblk <= 256) return nblk;
+  const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, 128));
+  const int rows_per = cdiv(nblk, S);
+  float* out = part + (size_t)nblk * 2 * C;
+  hipLaunchKernelGGL(slab_split_kernel, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, C, rows_per, out);
+  fin = out;
+  return S;
+}
+
 }  // namespace
+
+MI_API int mi_bn_slab_extra_rows() { return SLAB_EXTRA_ROWS; }
 
 MI_API int mi_bn_partial_rows(int M, int C) {
   int nblk, rpb; dim3 grid;
@@ -301,7 +341,9 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
   } else {
     hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, part, nblk, M, C, eps, momentum,
+  const float* fin = part;
+  nblk = tall_slab_split(part, nblk, C, st, fin);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, eps, momentum,
                      gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
@@ -330,7 +372,9 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
   slab_launch_dims(M, C, nblk, rpb, grid);
   hipLaunchKernelGGL(bn_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
                      (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, part, nblk, M, C, gamma,
+  const float* fin = part;
+  nblk = tall_slab_split(part, nblk, C, st, fin);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
                      save_mean, save_invstd, dgamma, dbeta, coef);
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,

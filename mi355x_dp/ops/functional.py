@@ -155,8 +155,9 @@ def conv2d_with_stats(x, weight, stride=1, padding=0):
     N, C, H, W = x.shape
     K, _, R, S = weight.shape
     P, Q = _conv_out(H, R, stride, padding), _conv_out(W, S, stride, padding)
-    rows = _lib.load().mi_nt_stat_rows(N * P * Q, K)
-    slab = torch.empty((rows, 2, K), dtype=torch.float32, device=x.device)
+    lib = _lib.load()
+    rows = lib.mi_nt_stat_rows(N * P * Q, K)
+    slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=torch.float32, device=x.device)
     y = _Conv2d.apply(x, weight, None, stride, padding, slab)
     return y, (slab, rows)
 
@@ -180,7 +181,8 @@ class _BatchNormAct(torch.autograd.Function):
             if stats is not None:
                 part, pre_rows = stats
             else:
-                part = torch.empty((_lib.load().mi_bn_partial_rows(M, C), 2, C), **f32)
+                lib = _lib.load()
+                part = torch.empty((lib.mi_bn_partial_rows(M, C) + lib.mi_bn_slab_extra_rows(), 2, C), **f32)
                 pre_rows = 0
             mean = torch.empty(C, **f32)
             invstd = torch.empty(C, **f32)
@@ -211,7 +213,8 @@ class _BatchNormAct(torch.autograd.Function):
         if ctx.training:
             gw = _grad_buffer(weight) if (weight is not None and ctx.needs_input_grad[1]) else None
             gb = _grad_buffer(bias) if (bias is not None and ctx.needs_input_grad[2]) else None
-            nblk = _lib.load().mi_bn_partial_rows(M, C)
+            lib = _lib.load()
+            nblk = lib.mi_bn_partial_rows(M, C) + lib.mi_bn_slab_extra_rows()
             part = torch.empty((nblk, 2, C), dtype=torch.float32, device=dev)
             coef = torch.empty((3, C), dtype=torch.float32, device=dev)
             _lib.call("mi_bn_bwd_train", ptr(dy), ptr(y), ptr(x), ptr(dx), ptr(dres), M, C, ptr(weight), ptr(mean),

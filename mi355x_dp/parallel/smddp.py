@@ -1,0 +1,79 @@
+"""The ``smddp`` process-group backend (SMDDP-equivalent, reference gpu.py:16-23,
+SURVEY.md §2.2 C25 / §5.8).
+
+``import smdistributed.dataparallel.torch.torch_smddp`` (our compat shim) calls
+``register()``, after which the reference's ``dist.init_process_group(backend='smddp')``
+works unmodified.  The creator:
+
+  1. binds the rank to its GPU *before* anything else (``LOCAL_RANK``): the
+     reference moves the model to "cuda" and wraps DDP before calling
+     ``set_device`` (gpu.py:145-153), which only works because SMDDP binds the
+     device at init;
+  2. returns the native C++ backend (``csrc/comm/smddp_backend.cpp``: RCCL
+     communicator on its own high-priority HIP stream, event-ordered with the
+     caller's stream, plus xGMI-aware bucket chunking) when it is built, else
+     torch's RCCL ``ProcessGroupNCCL``;
+  3. on a host with no GPU (CPU tests, gloo plumbing) returns a gloo backend
+     bound to the loopback interface so the same user code runs.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+BACKEND_NAME = "smddp"
+_registered = False
+
+
+def _gpu_count() -> int:
+    try:
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+def bind_local_device():
+    n = _gpu_count()
+    if n <= 0:
+        return None
+    local_rank = int(os.environ.get("LOCAL_RANK", os.environ.get("OMPI_COMM_WORLD_LOCAL_RANK", "0")))
+    dev = local_rank % n
+    torch.cuda.set_device(dev)
+    return dev
+
+
+def _gloo(store, rank, world_size, timeout):
+    opts = dist.ProcessGroupGloo._Options()
+    opts._timeout = timeout
+    host = os.environ.get("MI355X_DP_GLOO_HOST", "127.0.0.1")
+    opts._devices = [dist.ProcessGroupGloo.create_device(hostname=host)]
+    return dist.ProcessGroupGloo(store, rank, world_size, opts)
+
+
+def create_backend(store, rank, world_size, timeout):
+    dev = bind_local_device()
+    if dev is None:
+        return _gloo(store, rank, world_size, timeout)
+    if os.environ.get("MI355X_DP_SMDDP_IMPL", "native") == "native":
+        try:
+            from . import _smddp_native
+            mod = _smddp_native.load()
+            if mod is not None:
+                secs = timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout)
+                return mod.create_backend(store, rank, world_size, dev, secs)
+        except ImportError:
+            pass
+    return dist.ProcessGroupNCCL(store, rank, world_size, timeout)
+
+
+def register():
+    """Idempotently register the ``smddp`` backend name with torch.distributed."""
+    global _registered
+    if _registered or BACKEND_NAME in dist.Backend.backend_list:
+        _registered = True
+        return
+    dist.Backend.register_backend(BACKEND_NAME, create_backend, extended_api=False, devices=["cpu", "cuda"])
+    _registered = True
