@@ -1,0 +1,366 @@
+// smddp: native c10d::Backend for MI355X (RCCL over xGMI).  Registered in Python as the
+// process-group backend name "smddp" (mi355x_dp/parallel/smddp.py), so the reference's
+// `dist.init_process_group(backend='smddp')` (cifar10-distributed-smddp-gpu.py:23) and
+// stock torch DDP run on it unmodified.  SURVEY.md §2.2 C25, §2.3 N3/N4, §5.8.
+//
+// Design:
+//   * one RCCL communicator per backend, bootstrapped through the c10d Store
+//     (rank 0 publishes the ncclUniqueId);
+//   * every collective runs on a dedicated HIGH-PRIORITY HIP stream taken from torch's
+//     stream pool: it first waits (hipStreamWaitEvent) on an event recorded on the
+//     caller's current stream, so it sees all producing kernels, and the caller never
+//     blocks -- backward keeps issuing kernels while buckets reduce over xGMI;
+//   * tensors touched by the comm stream are recordStream()'d with torch's caching
+//     allocator so their memory is not recycled early;
+//   * Work::wait() makes the caller's stream wait on the completion event (no host
+//     block); getFuture() returns a device-aware ivalue::Future completed under the
+//     comm-stream guard, which is what DDP comm hooks and torch.distributed use;
+//   * a watchdog thread aborts the communicator and the process if a collective does
+//     not complete within the timeout (the launcher then tears down every rank --
+//     SURVEY.md §5.3 failure detection);
+//   * allreduce AVG maps to ncclAvg; large all-reduces can be split into link-sized
+//     chunks queued back to back (MI355X_DP_SMDDP_CHUNK_MB) so a long bucket does not
+//     hold the comm stream in one monolithic kernel.
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/Backend.hpp>
+#include <torch/csrc/distributed/c10d/Store.hpp>
+#include <torch/csrc/distributed/c10d/Types.hpp>
+#include <torch/csrc/distributed/c10d/Work.hpp>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
+#include <ATen/core/ivalue.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <pybind11/chrono.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+namespace smddp {
+
+using c10::hip::HIPStreamMasqueradingAsCUDA;
+
+#define HIPCHECK(x)                                                                       \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    TORCH_CHECK(e_ == hipSuccess, "smddp: HIP error ", hipGetErrorString(e_), " at ", #x); \
+  } while (0)
+#define NCCLCHECK(x)                                                                          \
+  do {                                                                                        \
+    ncclResult_t r_ = (x);                                                                    \
+    TORCH_CHECK(r_ == ncclSuccess, "smddp: RCCL error ", ncclGetErrorString(r_), " at ", #x); \
+  } while (0)
+
+static ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kChar: return ncclInt8;
+    case at::kByte: return ncclUint8;
+    case at::kBool: return ncclUint8;
+    default: TORCH_CHECK(false, "smddp: unsupported dtype ", t);
+  }
+}
+
+static ncclRedOp_t to_nccl(const c10d::ReduceOp& op) {
+  switch (op) {
+    case c10d::ReduceOp::SUM: return ncclSum;
+    case c10d::ReduceOp::PRODUCT: return ncclProd;
+    case c10d::ReduceOp::MIN: return ncclMin;
+    case c10d::ReduceOp::MAX: return ncclMax;
+    case c10d::ReduceOp::AVG: return ncclAvg;
+    default: TORCH_CHECK(false, "smddp: unsupported reduce op");
+  }
+}
+
+class SmddpWork : public c10d::Work {
+ public:
+  SmddpWork(int rank, c10d::OpType op, int device, HIPStreamMasqueradingAsCUDA comm, std::vector<at::Tensor> outputs,
+            bool blocking)
+      : c10d::Work(rank, op), device_(device), comm_(comm), outputs_(std::move(outputs)), blocking_(blocking) {
+    HIPCHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    HIPCHECK(hipEventRecord(done_, comm_.stream()));
+    start_ = std::chrono::steady_clock::now();
+    std::vector<c10::Device> devs{c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device)};
+    future_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()), devs);
+    c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_);
+    future_->markCompleted(c10::IValue(outputs_));
+  }
+  ~SmddpWork() override { hipEventDestroy(done_); }
+
+  bool isCompleted() override { return hipEventQuery(done_) == hipSuccess; }
+  bool isSuccess() const override { return true; }
+
+  bool wait(std::chrono::milliseconds timeout) override {
+    auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_);
+    HIPCHECK(hipStreamWaitEvent(cur.stream(), done_, 0));
+    if (blocking_) HIPCHECK(hipEventSynchronize(done_));
+    return true;
+  }
+  void synchronize() override { wait(kNoTimeout); }
+  c10::intrusive_ptr<c10::ivalue::Future> getFuture() override { return future_; }
+  std::vector<at::Tensor> result() override { return outputs_; }
+
+  std::chrono::steady_clock::time_point start_;
+  hipEvent_t done_;
+
+ private:
+  int device_;
+  HIPStreamMasqueradingAsCUDA comm_;
+  std::vector<at::Tensor> outputs_;
+  bool blocking_;
+  c10::intrusive_ptr<c10::ivalue::Future> future_;
+};
+
+class SmddpBackend : public c10d::Backend {
+ public:
+  SmddpBackend(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, int device, double timeout_s)
+      : c10d::Backend(rank, size), store_(store), device_(device),
+        comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(true, (c10::DeviceIndex)device)),
+        timeout_(std::chrono::milliseconds((int64_t)(timeout_s * 1000))) {
+    HIPCHECK(hipSetDevice(device));
+    ncclUniqueId uid;
+    const std::string key = "smddp/uid";
+    if (rank == 0) {
+      NCCLCHECK(ncclGetUniqueId(&uid));
+      std::vector<uint8_t> v((uint8_t*)&uid, (uint8_t*)&uid + sizeof(uid));
+      store_->set(key, v);
+    } else {
+      auto v = store_->get(key);
+      TORCH_CHECK(v.size() == sizeof(uid), "smddp: bad unique id from store");
+      memcpy(&uid, v.data(), sizeof(uid));
+    }
+    NCCLCHECK(ncclCommInitRank(&comm_, size, uid, rank));
+    HIPCHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    if (const char* c = std::getenv("MI355X_DP_SMDDP_CHUNK_MB")) chunk_bytes_ = (size_t)(atof(c) * (1 << 20));
+    watchdog_ = std::thread([this] { watchdog_loop(); });
+  }
+
+  ~SmddpBackend() override {
+    stop_ = true;
+    if (watchdog_.joinable()) watchdog_.join();
+    hipEventDestroy(ready_);
+    if (comm_) ncclCommDestroy(comm_);
+  }
+
+  const std::string getBackendName() const override { return "smddp"; }
+
+  // ---------------------------------------------------------------- helpers
+  template <typename Fn>
+  c10::intrusive_ptr<c10d::Work> run(c10d::OpType op, std::vector<at::Tensor> touched, std::vector<at::Tensor> outputs,
+                                     Fn&& fn, bool blocking = false) {
+    for (auto& t : touched) TORCH_CHECK(t.is_cuda(), "smddp: tensors must live on the GPU (SMDDP is GPU-only)");
+    c10::hip::HIPGuardMasqueradingAsCUDA dg((c10::DeviceIndex)device_);
+    auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_);
+    HIPCHECK(hipEventRecord(ready_, cur.stream()));
+    HIPCHECK(hipStreamWaitEvent(comm_stream_.stream(), ready_, 0));
+    for (auto& t : touched)
+      c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(),
+                                                                                       comm_stream_);
+    fn(comm_stream_.stream());
+    auto w = c10::make_intrusive<SmddpWork>(rank_, op, device_, comm_stream_, std::move(outputs), blocking);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      pending_.push_back(w);
+    }
+    return w;
+  }
+
+  void allreduce_chunked(at::Tensor& t, ncclRedOp_t op, hipStream_t s) {
+    const size_t esz = t.element_size();
+    const size_t n = t.numel();
+    const size_t chunk = chunk_bytes_ ? std::max<size_t>(1, chunk_bytes_ / esz) : n;
+    char* p = (char*)t.data_ptr();
+    for (size_t off = 0; off < n; off += chunk) {
+      size_t cnt = std::min(chunk, n - off);
+      NCCLCHECK(ncclAllReduce(p + off * esz, p + off * esz, cnt, to_nccl(t.scalar_type()), op, comm_, s));
+    }
+  }
+
+  // ------------------------------------------------------------ collectives
+  c10::intrusive_ptr<c10d::Work> allreduce(std::vector<at::Tensor>& tensors,
+                                           const c10d::AllreduceOptions& opts) override {
+    auto op = to_nccl(opts.reduceOp);
+    return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) {
+      NCCLCHECK(ncclGroupStart());
+      for (auto& t : tensors) {
+        TORCH_CHECK(t.is_contiguous(), "smddp allreduce: tensor must be contiguous");
+        allreduce_chunked(t, op, s);
+      }
+      NCCLCHECK(ncclGroupEnd());
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> allreduce_coalesced(std::vector<at::Tensor>& tensors,
+                                                     const c10d::AllreduceCoalescedOptions& opts) override {
+    c10d::AllreduceOptions o;
+    o.reduceOp = opts.reduceOp;
+    return allreduce(tensors, o);
+  }
+
+  c10::intrusive_ptr<c10d::Work> broadcast(std::vector<at::Tensor>& tensors,
+                                           const c10d::BroadcastOptions& opts) override {
+    return run(c10d::OpType::BROADCAST, tensors, tensors, [&](hipStream_t s) {
+      NCCLCHECK(ncclGroupStart());
+      for (auto& t : tensors)
+        NCCLCHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
+                                (int)opts.rootRank, comm_, s));
+      NCCLCHECK(ncclGroupEnd());
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> reduce(std::vector<at::Tensor>& tensors, const c10d::ReduceOptions& opts) override {
+    return run(c10d::OpType::REDUCE, tensors, tensors, [&](hipStream_t s) {
+      for (auto& t : tensors)
+        NCCLCHECK(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
+                             to_nccl(opts.reduceOp), (int)opts.rootRank, comm_, s));
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> _allgather_base(at::Tensor& out, at::Tensor& in,
+                                                 const c10d::AllgatherOptions&) override {
+    TORCH_CHECK(out.numel() == in.numel() * size_, "smddp _allgather_base: size mismatch");
+    return run(c10d::OpType::_ALLGATHER_BASE, {out, in}, {out}, [&](hipStream_t s) {
+      NCCLCHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, s));
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> allgather(std::vector<std::vector<at::Tensor>>& outputs,
+                                           std::vector<at::Tensor>& inputs,
+                                           const c10d::AllgatherOptions&) override {
+    TORCH_CHECK(inputs.size() == 1 && outputs.size() == 1, "smddp allgather: one tensor per rank");
+    auto in = inputs[0].contiguous();
+    auto flat = at::empty({(int64_t)size_ * in.numel()}, in.options());
+    std::vector<at::Tensor> touched{in, flat};
+    for (auto& o : outputs[0]) touched.push_back(o);
+    return run(c10d::OpType::ALLGATHER, touched, outputs[0], [&](hipStream_t s) {
+      NCCLCHECK(ncclAllGather(in.data_ptr(), flat.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, s));
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
+      for (int r = 0; r < size_; ++r) outputs[0][r].copy_(flat.narrow(0, r * in.numel(), in.numel()).view_as(in), true);
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> _reduce_scatter_base(at::Tensor& out, at::Tensor& in,
+                                                      const c10d::ReduceScatterOptions& opts) override {
+    TORCH_CHECK(in.numel() == out.numel() * size_, "smddp _reduce_scatter_base: size mismatch");
+    return run(c10d::OpType::_REDUCE_SCATTER_BASE, {out, in}, {out}, [&](hipStream_t s) {
+      NCCLCHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()),
+                                  to_nccl(opts.reduceOp), comm_, s));
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> reduce_scatter(std::vector<at::Tensor>& outputs,
+                                                std::vector<std::vector<at::Tensor>>& inputs,
+                                                const c10d::ReduceScatterOptions& opts) override {
+    TORCH_CHECK(outputs.size() == 1 && inputs.size() == 1, "smddp reduce_scatter: one output tensor");
+    auto out = outputs[0];
+    auto flat = at::cat(inputs[0]).contiguous();
+    return run(c10d::OpType::REDUCE_SCATTER, {out, flat}, outputs, [&](hipStream_t s) {
+      NCCLCHECK(ncclReduceScatter(flat.data_ptr(), out.data_ptr(), out.numel(), to_nccl(out.scalar_type()),
+                                  to_nccl(opts.reduceOp), comm_, s));
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> alltoall_base(at::Tensor& out, at::Tensor& in, std::vector<int64_t>& out_splits,
+                                               std::vector<int64_t>& in_splits,
+                                               const c10d::AllToAllOptions&) override {
+    TORCH_CHECK(out_splits.empty() && in_splits.empty(), "smddp alltoall_base: equal splits only");
+    const int64_t n = in.numel() / size_;
+    const size_t esz = in.element_size();
+    return run(c10d::OpType::ALLTOALL_BASE, {out, in}, {out}, [&](hipStream_t s) {
+      NCCLCHECK(ncclGroupStart());
+      for (int r = 0; r < size_; ++r) {
+        NCCLCHECK(ncclSend((char*)in.data_ptr() + r * n * esz, n, to_nccl(in.scalar_type()), r, comm_, s));
+        NCCLCHECK(ncclRecv((char*)out.data_ptr() + r * n * esz, n, to_nccl(out.scalar_type()), r, comm_, s));
+      }
+      NCCLCHECK(ncclGroupEnd());
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> send(std::vector<at::Tensor>& tensors, int dst, int) override {
+    return run(c10d::OpType::SEND, tensors, tensors, [&](hipStream_t s) {
+      for (auto& t : tensors) NCCLCHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), dst, comm_, s));
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> recv(std::vector<at::Tensor>& tensors, int src, int) override {
+    return run(c10d::OpType::RECV, tensors, tensors, [&](hipStream_t s) {
+      for (auto& t : tensors) NCCLCHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), src, comm_, s));
+    });
+  }
+
+  c10::intrusive_ptr<c10d::Work> barrier(const c10d::BarrierOptions&) override {
+    auto t = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(c10::Device(c10::DeviceType::CUDA,
+                                                                                      (c10::DeviceIndex)device_)));
+    return run(c10d::OpType::BARRIER, {t}, {t}, [&](hipStream_t s) {
+      NCCLCHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), 1, ncclFloat32, ncclSum, comm_, s));
+    }, /*blocking=*/true);
+  }
+
+  void setTimeout(std::chrono::milliseconds t) override { timeout_ = t; }
+
+ private:
+  void watchdog_loop() {
+    while (!stop_) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      std::lock_guard<std::mutex> lk(mu_);
+      while (!pending_.empty()) {
+        auto& w = pending_.front();
+        if (hipEventQuery(w->done_) == hipSuccess) {
+          pending_.pop_front();
+          continue;
+        }
+        if (std::chrono::steady_clock::now() - w->start_ > timeout_) {
+          fprintf(stderr, "smddp watchdog: rank %d collective did not complete within %lld ms; aborting\n", rank_,
+                  (long long)timeout_.count());
+          fflush(stderr);
+          ncclCommAbort(comm_);
+          comm_ = nullptr;
+          std::abort();
+        }
+        break;
+      }
+    }
+  }
+
+  c10::intrusive_ptr<c10d::Store> store_;
+  int device_;
+  HIPStreamMasqueradingAsCUDA comm_stream_;
+  std::chrono::milliseconds timeout_;
+  ncclComm_t comm_ = nullptr;
+  hipEvent_t ready_;
+  size_t chunk_bytes_ = 0;
+  std::mutex mu_;
+  std::deque<c10::intrusive_ptr<SmddpWork>> pending_;
+  std::atomic<bool> stop_{false};
+  std::thread watchdog_;
+};
+
+c10::intrusive_ptr<c10d::Backend> create_backend(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size,
+                                                 int device, double timeout_s) {
+  return c10::make_intrusive<SmddpBackend>(store, rank, size, device, timeout_s);
+}
+
+int rccl_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+}  // namespace smddp
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "smddp: native RCCL c10d backend for MI355X";
+  m.def("create_backend", &smddp::create_backend, "create the smddp backend", pybind11::arg("store"),
+        pybind11::arg("rank"), pybind11::arg("size"), pybind11::arg("device"), pybind11::arg("timeout_s"));
+  m.def("rccl_version", &smddp::rccl_version);
+}

@@ -73,7 +73,9 @@ class DataParallel(nn.Module):
 
         params = [p for p in module.parameters() if p.requires_grad]
         params = list(reversed(params))  # approximate backward order
-        self.flat = FlatParams(params, bf16_copy=bf16_copy)
+        from mi355x_dp.models.layers import Conv2d as _NativeConv
+        kernel_ids = {id(m.weight) for m in module.modules() if isinstance(m, _NativeConv)}
+        self.flat = FlatParams(params, bf16_copy=bf16_copy, kernel_layout_ids=kernel_ids)
         self.buffers = FlatBuffers(list(module.buffers()))
 
         sizes = [p.numel() * 4 for p in self.flat.params]

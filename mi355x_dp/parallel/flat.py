@@ -28,12 +28,12 @@ def _align(n: int) -> int:
     return (n + ALIGN - 1) // ALIGN * ALIGN
 
 
-def _kernel_view(flat: torch.Tensor, off: int, shape) -> torch.Tensor:
+def _kernel_view(flat: torch.Tensor, off: int, shape, kernel_layout: bool = True) -> torch.Tensor:
     n = 1
     for s in shape:
         n *= s
     v = flat[off:off + n]
-    if len(shape) == 4:
+    if len(shape) == 4 and kernel_layout:
         K, C, R, S = shape
         return v.view(K, R, S, C).permute(0, 3, 1, 2)
     return v.view(shape)
@@ -42,13 +42,17 @@ def _kernel_view(flat: torch.Tensor, off: int, shape) -> torch.Tensor:
 class FlatParams:
     """Owns the flat fp32 params, fp32 grads and bf16 copy for a list of parameters."""
 
-    def __init__(self, params: Sequence[torch.nn.Parameter], bf16_copy: bool = True):
+    def __init__(self, params: Sequence[torch.nn.Parameter], bf16_copy: bool = True, kernel_layout_ids=None):
+        """``kernel_layout_ids``: ids of 4-D params consumed by the native conv kernels; they are
+        stored [K][R][S][C].  Every other parameter keeps PyTorch's default contiguous layout (a
+        stock nn.Conv2d would otherwise start producing channels_last outputs).  ``None`` = all."""
         params = [p for p in params if p.requires_grad]
         if not params:
             raise ValueError("no trainable parameters")
         dev = params[0].device
         self.device = dev
         self.params: List[torch.nn.Parameter] = list(params)
+        self.kernel_layout = [kernel_layout_ids is None or id(p) in kernel_layout_ids for p in self.params]
         self.offsets = []
         off = 0
         for p in self.params:
@@ -59,14 +63,14 @@ class FlatParams:
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
         self.bf16 = torch.zeros(off, dtype=torch.bfloat16, device=dev) if bf16_copy else None
         with torch.no_grad():
-            for p, o in zip(self.params, self.offsets):
-                v = _kernel_view(self.data, o, tuple(p.shape))
+            for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
+                v = _kernel_view(self.data, o, tuple(p.shape), kl)
                 v.copy_(p.data)
                 p.data = v
-                p.grad = _kernel_view(self.grad, o, tuple(p.shape))
+                p.grad = _kernel_view(self.grad, o, tuple(p.shape), kl)
                 p._mi_flat = True
                 if self.bf16 is not None:
-                    p._mi_bf16 = _kernel_view(self.bf16, o, tuple(p.shape))
+                    p._mi_bf16 = _kernel_view(self.bf16, o, tuple(p.shape), kl)
             if self.bf16 is not None:
                 from mi355x_dp.ops.functional import cast_bf16_
                 cast_bf16_(self.data, self.bf16)
@@ -85,9 +89,9 @@ class FlatParams:
 
     def reattach_grads(self):
         """Re-point .grad at the flat views (after user code set them to None)."""
-        for p, o in zip(self.params, self.offsets):
+        for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr():
-                p.grad = _kernel_view(self.grad, o, tuple(p.shape))
+                p.grad = _kernel_view(self.grad, o, tuple(p.shape), kl)
 
 
 class FlatBuffers:

@@ -1,0 +1,82 @@
+"""GPU integration: smoke entry point, smddp native backend (world 1), the reference GPU
+script run UNMODIFIED through the local estimator, checkpoint layout of its model.pth."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_CODE = "/root/reference/notebooks/code"
+
+
+def test_graft_smoke():
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    g.smoke()
+
+
+def test_smddp_backend_world1(tmp_path):
+    script = tmp_path / "s.py"
+    script.write_text(
+        "import os, torch, torch.distributed as dist\n"
+        "import smdistributed.dataparallel.torch.torch_smddp\n"
+        "dist.init_process_group(backend='smddp')\n"
+        "pg = dist.distributed_c10d._get_default_group()\n"
+        "t = torch.full((1000,), 3.0, device='cuda')\n"
+        "w = dist.all_reduce(t, async_op=True); w.wait()\n"
+        "assert torch.allclose(t, torch.full_like(t, 3.0))\n"
+        "o = [torch.empty(10, device='cuda')]; dist.all_gather(o, torch.arange(10., device='cuda'))\n"
+        "assert torch.equal(o[0], torch.arange(10., device='cuda'))\n"
+        "dist.broadcast(t, 0); dist.barrier()\n"
+        "b = pg._get_backend(torch.device('cuda'))\n"
+        "print('BACKEND', type(b).__name__, b.name() if hasattr(b,'name') else '')\n"
+        "m = torch.nn.parallel.DistributedDataParallel(torch.nn.Linear(8, 4).cuda())\n"
+        "m(torch.randn(2, 8, device='cuda')).sum().backward()\n"
+        "print('OK')\n")
+    from mi355x_dp.launch import launch
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "1", str(script)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CODE), reason="reference checkout not mounted")
+def test_reference_gpu_script_unmodified(tmp_path):
+    """notebook-2 flow: PyTorch(distribution=smddp).fit() runs cifar10-distributed-smddp-gpu.py as-is."""
+    code = (
+        "import sys, os\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.append({os.path.join(ROOT, 'compat')!r})\n"
+        "from mi355x_dp.data.cifar import write_synthetic_cifar10\n"
+        "write_synthetic_cifar10('data', n_train=2048, n_test=512)\n"
+        "from sagemaker.pytorch import PyTorch\n"
+        "est = PyTorch(entry_point='cifar10-distributed-smddp-gpu.py', source_dir=%r, role='r',\n"
+        "              instance_count=1, instance_type='ml.p4d.24xlarge', framework_version='1.11.0', py_version='py38',\n"
+        "              hyperparameters={'epochs': 2, 'lr': 0.01, 'momentum': 0.9, 'batch-size': 256,\n"
+        "                               'model-type': 'resnet18', 'backend': 'smddp'},\n"
+        "              distribution={'smdistributed': {'dataparallel': {'enabled': True}}},\n"
+        "              output_path=os.path.abspath('out'))\n"
+        "est.fit({'train': os.path.abspath('data')}, job_name='gpu-job')\n"
+        "print('MODEL_DATA', est.model_data)\n" % REF_CODE)
+    env = {**os.environ, "MI355X_DP_S3_ROOT": str(tmp_path / "s3"), "MI355X_DP_JOBS_ROOT": str(tmp_path / "jobs"),
+           "MI355X_DP_NPROC": "1"}
+    r = subprocess.run([sys.executable, "-c", code], cwd=tmp_path, capture_output=True, text=True, timeout=900,
+                       env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "Initialized the distributed environment: 'smddp' backend on 1 nodes." in out
+    assert "Test set: Average loss:" in out
+    assert "Training seconds:" in out
+    import tarfile
+    tar = [l.split()[1] for l in r.stdout.splitlines() if l.startswith("MODEL_DATA")][0]
+    with tarfile.open(tar) as tf:
+        tf.extract("model.pth", path=tmp_path)
+    sd = torch.load(tmp_path / "model.pth", map_location="cpu", weights_only=True)
+    keys = list(sd.keys())
+    assert keys[0] == "module.conv1.weight" and "module.fc.weight" in sd
+    assert sd["module.fc.weight"].shape == (1000, 512)
+    assert all(v.is_contiguous() for v in sd.values())
+    assert sum(v.numel() for k, v in sd.items() if "running" not in k and "num_batches" not in k) == 11689512

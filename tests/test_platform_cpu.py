@@ -1,0 +1,136 @@
+"""CPU tests of the platform layer: SM_* contract, native launcher, local estimator running the
+reference CPU script unmodified (gloo, world 2), model artifact + serving."""
+import io
+import json
+import os
+import subprocess
+import sys
+import tarfile
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_CODE = "/root/reference/notebooks/code"
+
+
+def test_hyperparameters_and_env_contract():
+    from mi355x_dp.sagemaker_local.env import env_vars, hyperparameters_to_args, training_env
+    hps = {"epochs": 15, "lr": 0.01, "momentum": 0.9, "batch-size": 256, "model-type": "resnet18", "backend": "smddp"}
+    # SM_USER_ARGS in the captured log (nb2): sorted --key value pairs
+    assert hyperparameters_to_args(hps) == ["--backend", "smddp", "--batch-size", "256", "--epochs", "15", "--lr",
+                                            "0.01", "--model-type", "resnet18", "--momentum", "0.9"]
+    t = training_env("job", "cifar10-distributed-smddp-gpu.py", hps, {"train": "/opt/ml/input/data/train"},
+                     "/opt/ml/model", "/opt/ml/output", "/opt/ml/input", ["algo-1"], "algo-1", 8, 96,
+                     "ml.p4d.24xlarge", "s3://x/source", {"smdistributed": {"dataparallel": {"enabled": True}}})
+    e = env_vars(t)
+    assert e["SM_HOSTS"] == '["algo-1"]'
+    assert e["SM_CURRENT_HOST"] == "algo-1"
+    assert e["SM_MODEL_DIR"] == "/opt/ml/model"
+    assert e["SM_CHANNEL_TRAIN"] == "/opt/ml/input/data/train"
+    assert e["SM_NUM_GPUS"] == "8" and e["SM_NUM_CPUS"] == "96"
+    assert e["SM_HP_BATCH-SIZE"] == "256" and e["SM_HP_BACKEND"] == "smddp"
+    assert e["SM_MODULE_NAME"] == "cifar10-distributed-smddp-gpu"
+    assert json.loads(e["SM_TRAINING_ENV"])["additional_framework_parameters"][
+        "sagemaker_distributed_dataparallel_enabled"] is True
+    assert json.loads(e["SM_USER_ARGS"])[:2] == ["--backend", "smddp"]
+
+
+def _launcher():
+    from mi355x_dp.launch import ensure_launcher
+    return ensure_launcher()
+
+
+def test_native_launcher_env_and_tags():
+    exe = _launcher()
+    r = subprocess.run([exe, "--nproc", "3", "--tag-output", "--rank-env", "SM_CURRENT_HOST=algo-", "--",
+                        sys.executable, "-c",
+                        "import os;print(os.environ['RANK'],os.environ['LOCAL_RANK'],os.environ['WORLD_SIZE'],"
+                        "os.environ['SM_CURRENT_HOST'],os.environ['MASTER_ADDR'])"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    lines = sorted(r.stdout.strip().splitlines())
+    assert lines == [f"[1,mpirank:{i},algo-1]<stdout>:{i} {i} 3 algo-{i + 1} 127.0.0.1" for i in range(3)]
+
+
+def test_native_launcher_abort_all_on_failure():
+    exe = _launcher()
+    code = "import os,sys,time\nr=int(os.environ['RANK'])\nif r==1: sys.exit(7)\ntime.sleep(60)\n"
+    r = subprocess.run([exe, "--nproc", "3", "--grace", "2", "--", sys.executable, "-c", code],
+                       capture_output=True, text=True, timeout=40)
+    assert r.returncode == 7
+    assert "rank 1 exited with status 7; aborting all ranks" in r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CODE), reason="reference checkout not mounted")
+def test_notebook1_flow_cpu_gloo_world2(tmp_path):
+    """Notebook-1 path end to end: upload_data -> PyTorch(instance_count=2, gloo).fit() running the
+    UNMODIFIED cifar10-distributed-native-cpu.py -> model.tar.gz -> PyTorchModel(inference.py).deploy()
+    -> predictor.predict(4 images) (in-process and over HTTP)."""
+    code = f"""
+import os, sys, json
+sys.path.insert(0, {ROOT!r}); sys.path.append({os.path.join(ROOT, 'compat')!r})
+from mi355x_dp.data.cifar import write_synthetic_cifar10
+write_synthetic_cifar10('cifar10-dataset', n_train=512, n_test=128)
+import sagemaker, torch
+from sagemaker.pytorch import PyTorch, PyTorchModel
+sess = sagemaker.Session(); role = sagemaker.get_execution_role()
+uri = sess.upload_data(path='cifar10-dataset', key_prefix='datasets/cifar10-dataset')
+est = PyTorch(entry_point='cifar10-distributed-native-cpu.py', source_dir={REF_CODE!r},
+              output_path=f"s3://{{sess.default_bucket()}}/jobs/", role=role, instance_count=2,
+              instance_type='ml.c5.2xlarge', framework_version='1.8.0', py_version='py3',
+              hyperparameters={{'epochs': 1, 'lr': 0.01, 'momentum': 0.9, 'batch-size': 64,
+                               'model-type': 'custom', 'backend': 'gloo'}})
+est.fit({{'train': uri}}, job_name='nb1', wait=True)
+m = PyTorchModel(model_data=est.model_data, source_dir={REF_CODE!r}, entry_point='inference.py', role=role,
+                 framework_version='1.6.0', py_version='py3')
+p = m.deploy(initial_instance_count=1, instance_type='ml.c5.xlarge')
+out = p.predict(torch.randn(4, 3, 32, 32))
+ph = m.deploy(initial_instance_count=1, instance_type='ml.c5.xlarge', http=True)
+out2 = ph.predict(torch.randn(4, 3, 32, 32)); ph.delete_endpoint()
+print('SHAPES', out.shape, out2.shape)
+print('MODEL_DATA', est.model_data)
+"""
+    env = {**os.environ, "MI355X_DP_S3_ROOT": str(tmp_path / "s3"), "MI355X_DP_JOBS_ROOT": str(tmp_path / "jobs")}
+    r = subprocess.run([sys.executable, "-c", code], cwd=tmp_path, capture_output=True, text=True, timeout=600,
+                       env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "Initialized the distributed environment: 'gloo' backend on 2 nodes." in out
+    assert "[1,mpirank:1,algo-1]<stdout>:" in out
+    assert "Training seconds:" in out and "Completed - Training job completed" in out
+    assert "SHAPES (4, 10) (4, 10)" in out
+    from mi355x_dp.sagemaker_local.session import s3_to_local
+    os.environ["MI355X_DP_S3_ROOT"] = str(tmp_path / "s3")
+    tar = s3_to_local([l.split()[1] for l in r.stdout.splitlines() if l.startswith("MODEL_DATA")][0])
+    with tarfile.open(tar) as tf:
+        tf.extract("model.pth", path=tmp_path)
+    sd = torch.load(tmp_path / "model.pth", weights_only=True)
+    # CPU script saves model.module.state_dict(): bare Net keys (cpu.py:199) -> loadable by inference.py
+    assert list(sd.keys()) == ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "fc1.weight", "fc1.bias",
+                               "fc2.weight", "fc2.bias", "fc3.weight", "fc3.bias"]
+    assert sum(v.numel() for v in sd.values()) == 62006
+
+
+def test_serving_default_handlers():
+    from mi355x_dp.serve import NPY, default_input_fn, default_output_fn
+    x = np.random.randn(2, 3).astype(np.float32)
+    buf = io.BytesIO()
+    np.save(buf, x)
+    t = default_input_fn(buf.getvalue(), NPY)
+    assert torch.allclose(t, torch.from_numpy(x))
+    back = np.load(io.BytesIO(default_output_fn(t * 2, NPY)))
+    assert np.allclose(back, 2 * x)
+
+
+def test_model_archive_path_traversal_refused(tmp_path):
+    from mi355x_dp.serve import extract_model
+    evil = tmp_path / "m.tar.gz"
+    with tarfile.open(evil, "w:gz") as tf:
+        data = b"x"
+        ti = tarfile.TarInfo("../escape.txt")
+        ti.size = 1
+        tf.addfile(ti, io.BytesIO(data))
+    with pytest.raises(ValueError):
+        extract_model(str(evil))
