@@ -20,6 +20,7 @@
 //    (huge) N*P*Q reduction with fp32 atomics into the fp32 gradient buffer.
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -68,6 +69,7 @@ struct NTArgs {
   int out_f32;
   int accumulate;
   int tiles_m;       // m-tiles per class (mode 3) / total (others)
+  int a_bytes, b_bytes;  // buffer-resource ranges (GLDS path): A / B extents in bytes
   ConvGeom g;
 };
 
@@ -79,6 +81,7 @@ struct TNArgs {
   int lda, ldb, ldc;
   int mode;
   int k_per_split;
+  int a_bytes, b_bytes;
   ConvGeom g;
 };
 
@@ -87,15 +90,27 @@ constexpr int BK = 64;
 // ----------------------------------------------------------------- NT kernel
 // modes: 0 plain GEMM, 1 conv fwd, 2 conv dgrad (stride-1 or masked), 3 conv dgrad
 // decomposed by output parity class (stride 2: only the taps that hit real dY pixels).
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
+template <int BM, int BN, int STAGES>
+constexpr int nt_smem_u4() {
+  // max(staging ring, epilogue C tile [BM][BN+8] bf16 + stats scratch [RPP][2][BN] fp32)
+  constexpr int stage = STAGES * (BM + BN) * 8;
+  constexpr int epi = (BM * (BN + 8) * 2 + (256 / (BN / 8)) * 2 * BN * 4) / 16;
+  return stage > epi ? stage : epi;
+}
+
+// STAGES = 1: one LDS buffer, load -> barrier -> MFMA -> barrier per k-step, 3 blocks per CU (the other
+//             blocks' MFMAs hide each block's load latency);
+// STAGES = 2: double buffer, next k-step's loads in flight during this one's MFMAs, 2 blocks per CU.
+// Both stage with buffer_load ... lds (16 B per lane, zero-fill by range check) and track the
+// (tap, channel-chunk) position incrementally in scalar registers.
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
-  constexpr int SMEM_U4 = 2 * (BM + BN) * 8;
-  __shared__ __attribute__((aligned(16))) uint4 smem[SMEM_U4];
-  uint4* As = smem;                 // [2][BM][8]
-  uint4* Bs = smem + 2 * BM * 8;    // [2][BN][8]
+  __shared__ __attribute__((aligned(16))) uint4 smem[nt_smem_u4<BM, BN, STAGES>()];
+  uint4* As = smem;                      // [STAGES][BM][8]
+  uint4* Bs = smem + STAGES * BM * 8;    // [STAGES][BN][8]
 
   const int nbn = (a.N + BN - 1) / BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -122,88 +137,91 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
   }
   if (m0 >= Mrows) return;
 
-  // ---- per-thread A row geometry (fixed over the K loop)
-  int a_m[A_CH], a_img[A_CH], a_hb[A_CH], a_wb[A_CH];
+  // glds writes lane-linear pieces (LDS row rbase+32i, physical chunk chk): the XOR swizzle is on
+  // the SOURCE, this lane fetches logical chunk lc of its rows (row & 7 == rbase & 7 for all i).
+  const int lc = chk ^ (rbase & 7);
+  const int W = a.g.W, H = a.g.H, Cs = a.g.Cs;
+
+  // ---- per-thread A rows: gather-space pixel (hb, wb) and its element offset (may be negative)
+  int a_hb[A_CH], a_wb[A_CH], a_base[A_CH];
+  bool a_ok[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
-    int m = m0 + rbase + 32 * i;
-    a_m[i] = m;
+    const int m = m0 + rbase + 32 * i;
+    a_ok[i] = m < Mrows;
     if (a.mode != 0) {
-      uint32_t mm = m < Mrows ? (uint32_t)m : 0u;
-      uint32_t img = fdiv(mm, fPQ);
-      uint32_t rem = mm - img * fPQ.d;
-      uint32_t p = fdiv(rem, fQ);
-      uint32_t q = rem - p * fQ.d;
-      a_img[i] = (int)img;
+      const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
+      const uint32_t img = fdiv(mm, fPQ);
+      const uint32_t rem = mm - img * fPQ.d;
+      const uint32_t p = fdiv(rem, fQ);
+      const uint32_t q = rem - p * fQ.d;
       if (a.mode == 1)      { a_hb[i] = (int)p * a.g.stride - a.g.pad; a_wb[i] = (int)q * a.g.stride - a.g.pad; }
       else if (a.mode == 2) { a_hb[i] = (int)p + a.g.pad;             a_wb[i] = (int)q + a.g.pad; }
       else                  { a_hb[i] = (int)p + dh;                  a_wb[i] = (int)q + dw; }
+      a_base[i] = (((int)img * H + a_hb[i]) * W + a_wb[i]) * Cs + lc * 8;
     } else {
-      a_img[i] = 0; a_hb[i] = 0; a_wb[i] = 0;
+      a_hb[i] = 0; a_wb[i] = 0;
+      a_base[i] = m * a.lda + lc * 8;
     }
   }
+  int b_base[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const int n = n0 + rbase + 32 * i;
+    b_base[i] = n < a.N ? n * a.ldb + lc * 8 : -1;
+  }
 
-  const int cpt = (int)a.g.fCpt.d;
-  const int nk = (a.mode == 3) ? nr * ns * cpt : (a.K + BK - 1) / BK;
-  uint4 ra[A_CH], rb[B_CH];
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0xFFFFFFF0u;
 
-  auto load_tiles = [&](int kt) {
-    int c = 0, r = 0, s = 0, kB = kt * BK + chk * 8;
-    int tr = 0, ts = 0;
-    if (a.mode != 0) {
-      const int tap = (int)fdiv((uint32_t)kt, a.g.fCpt);
-      c = (kt - tap * cpt) * 64 + chk * 8;
-      if (a.mode == 3) {
-        tr = tap / ns; ts = tap - tr * ns;
-        r = r0 + a.g.stride * tr; s = s0 + a.g.stride * ts;
-      } else {
-        r = (int)fdiv((uint32_t)tap, a.g.fS);
-        s = tap - r * a.g.S;
-      }
-      kB = (r * a.g.S + s) * a.g.Cs + c;
+  const int nS = (a.mode == 3) ? ns : a.g.S;
+  const int nk = (a.mode == 3) ? nr * ns * (int)a.g.fCpt.d : (a.K + BK - 1) / BK;
+  // wave-uniform k position: gather-space tap (kr, ks) and channel-chunk base kc
+  int kr = 0, ks = 0, kc = 0;
+
+  auto issue_loads = [&](int kt, int buf) {
+    int r, s, koffA, kB;
+    if (a.mode == 0) {
+      r = 0; s = 0;
+      koffA = kt * BK;
+      kB = kt * BK;
+    } else {
+      r = (a.mode == 3) ? r0 + a.g.stride * kr : kr;
+      s = (a.mode == 3) ? s0 + a.g.stride * ks : ks;
+      const int sgn_tap = (a.mode == 1) ? ((kr * W + ks) * Cs) : -((kr * W + ks) * Cs);
+      koffA = sgn_tap + kc;
+      kB = (r * a.g.S + s) * Cs + kc;
     }
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const bf16_t* src = nullptr;
+      bool ok = a_ok[i];
       if (a.mode == 0) {
-        if (a_m[i] < a.M && kB < a.K) src = a.A + (size_t)a_m[i] * a.lda + kB;
-      } else if (a.mode == 1) {
-        int ih = a_hb[i] + r, iw = a_wb[i] + s;
-        if (a_m[i] < Mrows && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
-          src = a.A + ((size_t)(a_img[i] * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c;
-      } else if (a.mode == 2) {
-        int th = a_hb[i] - r, tw = a_wb[i] - s;
-        bool ok = a_m[i] < Mrows && th >= 0 && tw >= 0;
-        int ih = th, iw = tw;
-        if (a.g.stride != 1) {
-          ok = ok && (th % a.g.stride) == 0 && (tw % a.g.stride) == 0;
-          ih = th / a.g.stride; iw = tw / a.g.stride;
-        }
-        if (ok && ih < a.g.H && iw < a.g.W)
-          src = a.A + ((size_t)(a_img[i] * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c;
+        ok = ok && kt * BK + lc * 8 < a.K;
       } else {
-        int ih = a_hb[i] - tr, iw = a_wb[i] - ts;
-        if (a_m[i] < Mrows && (unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
-          src = a.A + ((size_t)(a_img[i] * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c;
+        const int ih = (a.mode == 1) ? a_hb[i] + kr : a_hb[i] - kr;
+        const int iw = (a.mode == 1) ? a_wb[i] + ks : a_wb[i] - ks;
+        ok = ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       }
-      ra[i] = src ? *(const uint4*)src : make_uint4(0, 0, 0, 0);
+      const uint32_t vo = ok ? (uint32_t)(a_base[i] + koffA) * 2u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &As[(buf * BM + 32 * i + 8 * wid) * 8]), 16, vo,
+                                               0, 0, 0);
     }
+    const bool kok = (a.mode != 0) || (kt * BK + lc * 8 < a.K);
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      int n = n0 + rbase + 32 * i;
-      rb[i] = (n < a.N && kB < a.K) ? *(const uint4*)(a.B + (size_t)n * a.ldb + kB) : make_uint4(0, 0, 0, 0);
+      const bool ok = b_base[i] >= 0 && kok;
+      const uint32_t vo = ok ? (uint32_t)(b_base[i] + kB) * 2u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, LDS_PTR(void, &Bs[(buf * BN + 32 * i + 8 * wid) * 8]), 16, vo,
+                                               0, 0, 0);
     }
-  };
-  auto store_tiles = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      int row = rbase + 32 * i;
-      As[(buf * BM + row) * 8 + (chk ^ (row & 7))] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      int row = rbase + 32 * i;
-      Bs[(buf * BN + row) * 8 + (chk ^ (row & 7))] = rb[i];
+    // advance the k position
+    if (a.mode != 0) {
+      kc += 64;
+      if (kc >= Cs) {
+        kc = 0;
+        if (++ks >= nS) { ks = 0; ++kr; }
+      }
     }
   };
 
@@ -214,28 +232,19 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  if (nk > 0) {
-    load_tiles(0);
-    store_tiles(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles(kt + 1);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[MI], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        int row = wm * WM + 16 * i + fr;
-        uint4 v = As[(cur * BM + row) * 8 + ((kk * 4 + fq) ^ (row & 7))];
-        af[i] = __builtin_bit_cast(bf16x8, v);
+        const int row = wm * WM + 16 * i + fr;
+        af[i] = __builtin_bit_cast(bf16x8, As[(cur * BM + row) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        int row = wn * WN + 16 * j + fr;
-        uint4 v = Bs[(cur * BN + row) * 8 + ((kk * 4 + fq) ^ (row & 7))];
-        bfr[j] = __builtin_bit_cast(bf16x8, v);
+        const int row = wn * WN + 16 * j + fr;
+        bfr[j] = __builtin_bit_cast(bf16x8, Bs[(cur * BN + row) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -243,8 +252,27 @@ __global__ __launch_bounds__(256, 2) void nt_kernel(NTArgs a) {
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
+  };
+
+  if constexpr (STAGES == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      issue_loads(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      compute(0);
+      __syncthreads();
+    }
+  } else {
+    if (nk > 0) issue_loads(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) issue_loads(kt + 1, cur ^ 1);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // output row offset (elements) of tile row m
@@ -339,21 +367,21 @@ __device__ __forceinline__ int tr_swz(int k) {
   return (4 * (k & 3) + 16 * ((k >> 3) & 1)) & (UNITS - 1);
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void tn_kernel(TNArgs a) {
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int AU = BM / 4, BU = BN / 4;            // 8-byte units per LDS row
   constexpr int ACPR = BM / 8, BCPR = BN / 8;        // 16-byte chunks per row
   constexpr int A_CH = BK * ACPR / 256, B_CH = BK * BCPR / 256;
   constexpr int A_RSTEP = 256 / ACPR, B_RSTEP = 256 / BCPR;
-  __shared__ __attribute__((aligned(16))) uint2 smem[2 * BK * (AU + BU)];
-  uint2* As = smem;                   // [2][BK][AU]
-  uint2* Bs = smem + 2 * BK * AU;     // [2][BK][BU]
+  constexpr int A_RPI = 64 / ACPR, B_RPI = 64 / BCPR;  // LDS rows per wave-instruction
+  __shared__ __attribute__((aligned(16))) uint2 smem[STAGES * BK * (AU + BU)];
+  uint2* As = smem;                        // [STAGES][BK][AU]
+  uint2* Bs = smem + STAGES * BK * AU;     // [STAGES][BK][BU]
 
   const int nbn = (a.N + BN - 1) / BN;
-  const int ntiles = gridDim.x;
-  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
   const int kbeg = blockIdx.y * a.k_per_split;
   const int kend = min(a.K, kbeg + a.k_per_split);
@@ -363,58 +391,71 @@ __global__ __launch_bounds__(256, 2) void tn_kernel(TNArgs a) {
   const int wm = wid >> 1, wn = wid & 1;
   const int a_cc = tid % ACPR, a_r = tid / ACPR;
   const int b_cc = tid % BCPR, b_r = tid / BCPR;
+  // lane-linear LDS image, tr-read swizzle u' = u ^ sw(k) applied on the SOURCE side
+  const int a_lc = a_cc ^ (tr_swz<AU>(a_r) >> 1);
+  const int b_lc = b_cc ^ (tr_swz<BU>(b_r) >> 1);
 
   // conv-mode B column geometry: the block's n range sits inside one (r,s) tap
   int tap_r = 0, tap_s = 0, c0 = 0;
   if (a.mode == 1) {
-    int tap = n0 / a.g.Cs;
+    const int tap = n0 / a.g.Cs;
     c0 = n0 - tap * a.g.Cs;
     tap_r = tap / a.g.S;
     tap_s = tap - tap_r * a.g.S;
   }
+  const int H = a.g.H, W = a.g.W, P = a.g.P, Q = a.g.Q, Cs = a.g.Cs;
+  const int st = a.g.stride, pad = a.g.pad;
 
-  uint4 ra[A_CH], rb[B_CH];
-  auto load_tiles = [&](int k0) {
+  // ---- per-thread B rows (mode 1): output pixel (img, p, q) of reduction row k, advanced by BK
+  int b_img[B_CH], b_p[B_CH], b_q[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const uint32_t k = (uint32_t)min(kbeg + b_r + B_RSTEP * i, a.K - 1);
+    if (a.mode == 1) {
+      const uint32_t img = fdiv(k, a.g.fPQ);
+      const uint32_t rem = k - img * a.g.fPQ.d;
+      const uint32_t p = fdiv(rem, a.g.fQ);
+      b_img[i] = (int)img; b_p[i] = (int)p; b_q[i] = (int)(rem - p * a.g.fQ.d);
+    } else {
+      b_img[i] = b_p[i] = b_q[i] = 0;
+    }
+  }
+  // per-step carry deltas for +BK pixels
+  const int dq = BK % Q, dp = (BK / Q) % P, dimg = BK / (P * Q);
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0xFFFFFFF0u;
+  const int a_m = m0 + a_lc * 8;
+  const int b_n = n0 + b_lc * 8;
+
+  auto issue_loads = [&](int k0, int buf) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      int k = k0 + a_r + A_RSTEP * i;
-      int m = m0 + a_cc * 8;
-      ra[i] = (k < kend && m < a.M) ? *(const uint4*)(a.A + (size_t)k * a.lda + m) : make_uint4(0, 0, 0, 0);
+      const int k = k0 + a_r + A_RSTEP * i;
+      const bool ok = k < kend && a_m < a.M;
+      const uint32_t vo = ok ? (uint32_t)(k * a.lda + a_m) * 2u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsA, LDS_PTR(void, &As[(buf * BK + A_RSTEP * i + wid * A_RPI) * AU]), 16, vo, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      int k = k0 + b_r + B_RSTEP * i;
-      const bf16_t* src = nullptr;
-      if (k < kend) {
-        if (a.mode == 0) {
-          int n = n0 + b_cc * 8;
-          if (n < a.N) src = a.B + (size_t)k * a.ldb + n;
-        } else {
-          uint32_t img = fdiv((uint32_t)k, a.g.fPQ);
-          uint32_t rem = (uint32_t)k - img * a.g.fPQ.d;
-          uint32_t p = fdiv(rem, a.g.fQ);
-          uint32_t q = rem - p * a.g.fQ.d;
-          int ih = (int)p * a.g.stride - a.g.pad + tap_r;
-          int iw = (int)q * a.g.stride - a.g.pad + tap_s;
-          if ((unsigned)ih < (unsigned)a.g.H && (unsigned)iw < (unsigned)a.g.W)
-            src = a.B + ((size_t)((int)img * a.g.H + ih) * a.g.W + iw) * a.g.Cs + c0 + b_cc * 8;
-        }
+      const int k = k0 + b_r + B_RSTEP * i;
+      uint32_t vo = OOB;
+      if (a.mode == 0) {
+        if (k < kend && b_n < a.N) vo = (uint32_t)(k * a.ldb + b_n) * 2u;
+      } else {
+        const int ih = b_p[i] * st - pad + tap_r, iw = b_q[i] * st - pad + tap_s;
+        if (k < kend && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          vo = (uint32_t)((((b_img[i] * H + ih) * W + iw) * Cs) + c0 + b_lc * 8) * 2u;
+        // advance this row by BK output pixels
+        int q = b_q[i] + dq, p = b_p[i] + dp, img = b_img[i] + dimg;
+        if (q >= Q) { q -= Q; ++p; }
+        if (p >= P) { p -= P; ++img; }
+        b_q[i] = q; b_p[i] = p; b_img[i] = img;
       }
-      rb[i] = src ? *(const uint4*)src : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store_tiles = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      int k = a_r + A_RSTEP * i;
-      int u = (2 * a_cc) ^ tr_swz<AU>(k);
-      *(uint4*)&As[(buf * BK + k) * AU + u] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      int k = b_r + B_RSTEP * i;
-      int u = (2 * b_cc) ^ tr_swz<BU>(k);
-      *(uint4*)&Bs[(buf * BK + k) * BU + u] = rb[i];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsB, LDS_PTR(void, &Bs[(buf * BK + B_RSTEP * i + wid * B_RPI) * BU]), 16, vo, 0, 0, 0);
     }
   };
 
@@ -425,13 +466,7 @@ __global__ __launch_bounds__(256, 2) void tn_kernel(TNArgs a) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  load_tiles(kbeg);
-  store_tiles(0);
-  __syncthreads();
-  const int nk = (kend - kbeg + BK - 1) / BK;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[MI], bfr[NJ];
@@ -439,7 +474,7 @@ __global__ __launch_bounds__(256, 2) void tn_kernel(TNArgs a) {
       const int k2 = k1 + 4;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        int u = (wm * WM + 16 * i) / 4 + p4;
+        const int u = (wm * WM + 16 * i) / 4 + p4;
         short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, &As[(cur * BK + k1) * AU + (u ^ tr_swz<AU>(k1))]));
         short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, &As[(cur * BK + k2) * AU + (u ^ tr_swz<AU>(k2))]));
         short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -447,7 +482,7 @@ __global__ __launch_bounds__(256, 2) void tn_kernel(TNArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        int u = (wn * WN + 16 * j) / 4 + p4;
+        const int u = (wn * WN + 16 * j) / 4 + p4;
         short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, &Bs[(cur * BK + k1) * BU + (u ^ tr_swz<BU>(k1))]));
         short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, &Bs[(cur * BK + k2) * BU + (u ^ tr_swz<BU>(k2))]));
         short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -459,8 +494,28 @@ __global__ __launch_bounds__(256, 2) void tn_kernel(TNArgs a) {
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
+  };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if constexpr (STAGES == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      issue_loads(kbeg + kt * BK, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      compute(0);
+      __syncthreads();
+    }
+  } else {
+    issue_loads(kbeg, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) issue_loads(kbeg + (kt + 1) * BK, cur ^ 1);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // epilogue: lane holds D[m = 16i + 4g + r][n = 16j + li]; fp32 atomics (split-K)
@@ -501,6 +556,12 @@ __global__ void wtrans_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__
   }
 }
 
+// byte extent for a buffer resource; 0 (= use the register-staged path) beyond 2 GiB
+static int rsrc_bytes(int64_t elems) {
+  const int64_t b = elems * 2;
+  return b > 0x7FFFFFF0LL ? 0 : (int)b;
+}
+
 ConvGeom make_geom(int H, int W, int Cs, int P, int Q, int S, int stride, int pad, int R = 1) {
   ConvGeom g{};
   g.H = H; g.W = W; g.Cs = Cs; g.P = P; g.Q = Q; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
@@ -509,6 +570,23 @@ ConvGeom make_geom(int H, int W, int Cs, int P, int Q, int S, int stride, int pa
   g.fS = make_fastdiv((uint32_t)S);
   g.fCpt = make_fastdiv((uint32_t)(Cs >= 64 ? Cs / 64 : 1));
   return g;
+}
+
+static int g_nt_glds = -1;  // TN: 0 = register staging, else direct-to-LDS; NT: number of LDS stages (1|2)
+static int g_nt_stages = -1;
+static bool glds_on() {
+  if (g_nt_glds < 0) {
+    const char* e = std::getenv("MI355X_DP_GLDS");
+    g_nt_glds = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_nt_glds != 0;
+}
+static int nt_stages() {
+  if (g_nt_stages < 0) {
+    const char* e = std::getenv("MI355X_DP_NT_STAGES");
+    g_nt_stages = (e && e[0] == '2') ? 2 : 1;
+  }
+  return g_nt_stages;
 }
 
 template <int BM, int BN>
@@ -522,7 +600,11 @@ hipError_t launch_nt(NTArgs& a, hipStream_t st) {
   }
   a.tiles_m = cdiv(mrows, BM);
   int grid = a.tiles_m * cdiv(a.N, BN);
-  hipLaunchKernelGGL((nt_kernel<BM, BN>), dim3(grid, classes), dim3(256), 0, st, a);
+  if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
+  if (nt_stages() == 2)
+    hipLaunchKernelGGL((nt_kernel<BM, BN, 2>), dim3(grid, classes), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((nt_kernel<BM, BN, 1>), dim3(grid, classes), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -549,7 +631,11 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   int steps_per = cdiv(ksteps, splits);
   a.k_per_split = steps_per * BK;
   splits = cdiv(a.K, a.k_per_split);
-  hipLaunchKernelGGL((tn_kernel<BM, BN>), dim3(tiles, splits), dim3(256), 0, st, a);
+  if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
+  if (glds_on())
+    hipLaunchKernelGGL((tn_kernel<BM, BN, 1>), dim3(tiles, splits), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((tn_kernel<BM, BN, 2>), dim3(tiles, splits), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -567,6 +653,18 @@ hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
 
 // ============================================================== C ABI
 // Conv forward: x NHWC [Nb,H,W,C] bf16, w [K][R][S][C] bf16, y NHWC [Nb,P,Q,K].
+// Select direct-to-LDS (buffer_load ... lds) staging (1) or register staging (0) for all GEMM kernels.
+MI_API int mi_set_glds(int on) {
+  g_nt_glds = on ? 1 : 0;
+  return 0;
+}
+
+// NT (fwd/dgrad/GEMM) kernels: 1 = single LDS stage at 3 blocks/CU, 2 = double-buffered at 2 blocks/CU.
+MI_API int mi_set_nt_stages(int stages) {
+  g_nt_stages = stages == 2 ? 2 : 1;
+  return 0;
+}
+
 // Rows of the per-channel statistics slab written by a conv/GEMM forward with M rows, N cols.
 MI_API int mi_nt_stat_rows(int M, int N) {
   const int bm = nt_choice(M, N) == 2 ? 64 : 128;
@@ -583,6 +681,8 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
   a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias; a.stats = stats;
   a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
   a.lda = 0; a.ldb = a.K; a.ldc = K; a.mode = 1; a.out_f32 = out_f32; a.accumulate = 0;
+  a.a_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
+  a.b_bytes = rsrc_bytes((int64_t)K * a.K);
   a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
   return (int)dispatch_nt(a, st);
 }
@@ -591,11 +691,13 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
 MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
-  if (K % 64 != 0 || C % 8 != 0) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || C % 8 != 0 || stride > 2) return (int)hipErrorInvalidValue;
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
   a.lda = 0; a.ldb = a.K; a.ldc = C; a.mode = 2; a.out_f32 = 0; a.accumulate = 0;
+  a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
+  a.b_bytes = rsrc_bytes((int64_t)C * a.K);
   // gathered tensor = dy (spatial P,Q, channels K); rows = dx pixels (H, W)
   a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);
   if (stride == 2) {
@@ -621,6 +723,8 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
   a.M = K; a.N = R * S * C; a.K = Nb * P * Q;
   a.lda = K; a.ldb = 0; a.ldc = a.N; a.mode = 1;
+  a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
+  a.b_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
   a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
   return (int)dispatch_tn(a, st);
 }
@@ -640,6 +744,8 @@ MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias, 
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.stats = out_f32 ? nullptr : stats;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.mode = 0; a.out_f32 = out_f32; a.accumulate = accumulate;
+  a.a_bytes = rsrc_bytes((int64_t)M * lda);
+  a.b_bytes = rsrc_bytes((int64_t)N * ldb);
   a.g = make_geom(1, 1, 64, 1, 1, 1, 1, 0);
   return (int)dispatch_nt(a, st);
 }
@@ -651,6 +757,8 @@ MI_API int mi_gemm_tn(const void* A, const void* B, float* C, int M, int N, int 
   TNArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.mode = 0;
+  a.a_bytes = rsrc_bytes((int64_t)K * lda);
+  a.b_bytes = rsrc_bytes((int64_t)K * ldb);
   a.g = make_geom(1, 1, 64, 1, 1, 1, 1, 0);
   return (int)dispatch_tn(a, st);
 }

@@ -55,10 +55,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--no-stock", action="store_true")
+    ap.add_argument("--stages", type=int, default=1, help="NT kernel LDS stages (1 or 2)")
     a = ap.parse_args()
     from mi355x_dp.ops import _lib
     from mi355x_dp.ops import kernels  # noqa: F401
     from mi355x_dp.ops._lib import ptr, stream_of
+    _lib.load().mi_set_glds(1); _lib.load().mi_set_nt_stages(a.stages)
 
     tot = {"fwd": [0, 0], "dgrad": [0, 0], "wgrad": [0, 0]}
     print("| N C H K R s | count | fwd TF (ms) | dgrad TF (ms) | wgrad TF (ms) | stock fwd/dgrad/wgrad TF |")
