@@ -80,7 +80,7 @@ def main():
     labels = torch.randint(0, args.num_classes, (B,), dtype=torch.int64, device=dev, generator=g)
 
     def step(i):
-        x = augment(images, 3, IMAGENET_MEAN, IMAGENET_STD, pad=0, flip=True, seed=i)
+        x = augment(images, 8, IMAGENET_MEAN, IMAGENET_STD, pad=0, flip=True, seed=i)  # 3 ch + 5 zero pad
         engine.zero_grad()
         out = engine(x)
         loss = cross_entropy(out, labels)

@@ -155,10 +155,11 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
       const uint32_t rem = mm - img * fPQ.d;
       const uint32_t p = fdiv(rem, fQ);
       const uint32_t q = rem - p * fQ.d;
-      if (a.mode == 1)      { a_hb[i] = (int)p * a.g.stride - a.g.pad; a_wb[i] = (int)q * a.g.stride - a.g.pad; }
-      else if (a.mode == 2) { a_hb[i] = (int)p + a.g.pad;             a_wb[i] = (int)q + a.g.pad; }
-      else                  { a_hb[i] = (int)p + dh;                  a_wb[i] = (int)q + dw; }
-      a_base[i] = (((int)img * H + a_hb[i]) * W + a_wb[i]) * Cs + lc * 8;
+      if (a.mode == 1 || a.mode == 4) { a_hb[i] = (int)p * a.g.stride - a.g.pad; a_wb[i] = (int)q * a.g.stride - a.g.pad; }
+      else if (a.mode == 2)           { a_hb[i] = (int)p + a.g.pad;             a_wb[i] = (int)q + a.g.pad; }
+      else                            { a_hb[i] = (int)p + dh;                  a_wb[i] = (int)q + dw; }
+      // mode 4 (Cs == 8): the lane's 16-B chunk is one whole tap (8 channels), not a channel slice
+      a_base[i] = (((int)img * H + a_hb[i]) * W + a_wb[i]) * Cs + (a.mode == 4 ? 0 : lc * 8);
     } else {
       a_hb[i] = 0; a_wb[i] = 0;
       a_base[i] = m * a.lda + lc * 8;
@@ -179,12 +180,15 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
   const int nk = (a.mode == 3) ? nr * ns * (int)a.g.fCpt.d : (a.K + BK - 1) / BK;
   // wave-uniform k position: gather-space tap (kr, ks) and channel-chunk base kc
   int kr = 0, ks = 0, kc = 0;
+  // mode 4: per-LANE tap t = 8*kt + lc -> (tr4, ts4), advanced by 8 taps per k-step
+  int tr4 = lc / a.g.S, ts4 = lc - (lc / a.g.S) * a.g.S;
+  const int dts4 = 8 % a.g.S, dtr4 = 8 / a.g.S, ntaps = a.g.R * a.g.S;
 
   auto issue_loads = [&](int kt, int buf) {
     int r, s, koffA, kB;
-    if (a.mode == 0) {
+    if (a.mode == 0 || a.mode == 4) {
       r = 0; s = 0;
-      koffA = kt * BK;
+      koffA = (a.mode == 0) ? kt * BK : (tr4 * W + ts4) * Cs;
       kB = kt * BK;
     } else {
       r = (a.mode == 3) ? r0 + a.g.stride * kr : kr;
@@ -198,6 +202,9 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
       bool ok = a_ok[i];
       if (a.mode == 0) {
         ok = ok && kt * BK + lc * 8 < a.K;
+      } else if (a.mode == 4) {
+        const int ih = a_hb[i] + tr4, iw = a_wb[i] + ts4;
+        ok = ok && (kt * 8 + lc) < ntaps && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       } else {
         const int ih = (a.mode == 1) ? a_hb[i] + kr : a_hb[i] - kr;
         const int iw = (a.mode == 1) ? a_wb[i] + ks : a_wb[i] - ks;
@@ -207,7 +214,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &As[(buf * BM + 32 * i + 8 * wid) * 8]), 16, vo,
                                                0, 0, 0);
     }
-    const bool kok = (a.mode != 0) || (kt * BK + lc * 8 < a.K);
+    const bool kok = (a.mode != 0 && a.mode != 4) || (kt * BK + lc * 8 < a.K);
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const bool ok = b_base[i] >= 0 && kok;
@@ -216,7 +223,10 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
                                                0, 0, 0);
     }
     // advance the k position
-    if (a.mode != 0) {
+    if (a.mode == 4) {
+      ts4 += dts4; tr4 += dtr4;
+      if (ts4 >= a.g.S) { ts4 -= a.g.S; ++tr4; }
+    } else if (a.mode != 0) {
       kc += 64;
       if (kc >= Cs) {
         kc = 0;
@@ -395,11 +405,12 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
   const int a_lc = a_cc ^ (tr_swz<AU>(a_r) >> 1);
   const int b_lc = b_cc ^ (tr_swz<BU>(b_r) >> 1);
 
-  // conv-mode B column geometry: the block's n range sits inside one (r,s) tap
+  // conv-mode B column geometry: this thread's 8 columns n0 + 8*b_lc .. +7 = (tap, channel c0..c0+7)
   int tap_r = 0, tap_s = 0, c0 = 0;
   if (a.mode == 1) {
-    const int tap = n0 / a.g.Cs;
-    c0 = n0 - tap * a.g.Cs;
+    const int ncol = n0 + b_lc * 8;
+    const int tap = ncol / a.g.Cs;
+    c0 = ncol - tap * a.g.Cs;
     tap_r = tap / a.g.S;
     tap_s = tap - tap_r * a.g.S;
   }
@@ -447,7 +458,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
       } else {
         const int ih = b_p[i] * st - pad + tap_r, iw = b_q[i] * st - pad + tap_s;
         if (k < kend && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          vo = (uint32_t)((((b_img[i] * H + ih) * W + iw) * Cs) + c0 + b_lc * 8) * 2u;
+          vo = (b_n < a.N) ? (uint32_t)((((b_img[i] * H + ih) * W + iw) * Cs) + c0) * 2u : OOB;
         // advance this row by BK output pixels
         int q = b_q[i] + dq, p = b_p[i] + dp, img = b_img[i] + dimg;
         if (q >= Q) { q -= Q; ++p; }
@@ -641,7 +652,7 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
 
 hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
   const int target = 1024;
-  bool n64 = (a.N <= 64) || (a.mode == 1 && (a.g.Cs % 128) != 0);
+  bool n64 = a.N <= 64;
   bool m64 = a.M <= 64;
   if (m64 && n64) return launch_tn<64, 64>(a, st, target);
   if (m64) return launch_tn<64, 128>(a, st, target);
@@ -676,11 +687,11 @@ MI_API int mi_nt_stat_rows(int M, int N) {
 MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bias, float* stats,
                          int Nb, int H, int W, int C, int K, int R, int S,
                          int stride, int pad, int P, int Q, int out_f32, hipStream_t st) {
-  if (C % 64 != 0 || K % 8 != 0) return (int)hipErrorInvalidValue;
+  if ((C % 64 != 0 && C != 8) || K % 8 != 0) return (int)hipErrorInvalidValue;
   NTArgs a{};
   a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias; a.stats = stats;
   a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
-  a.lda = 0; a.ldb = a.K; a.ldc = K; a.mode = 1; a.out_f32 = out_f32; a.accumulate = 0;
+  a.lda = 0; a.ldb = a.K; a.ldc = K; a.mode = (C == 8) ? 4 : 1; a.out_f32 = out_f32; a.accumulate = 0;
   a.a_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
   a.b_bytes = rsrc_bytes((int64_t)K * a.K);
   a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
@@ -718,7 +729,7 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
 MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
-  if (C % 64 != 0 || K % 8 != 0) return (int)hipErrorInvalidValue;
+  if (C % 8 != 0 || K % 8 != 0) return (int)hipErrorInvalidValue;
   TNArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
   a.M = K; a.N = R * S * C; a.K = Nb * P * Q;

@@ -100,7 +100,10 @@ def conv_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = F
 
 
 def to_device_input(x: torch.Tensor) -> torch.Tensor:
-    """Model-entry conversion for the native path: bf16, NHWC storage."""
+    """Model-entry conversion for the native path: bf16, NHWC storage; images with <= 8 channels are
+    zero-padded to 8 (one 16-byte chunk per pixel, the stem conv's gather unit)."""
     if x.is_cuda:
+        if x.dim() == 4 and x.shape[1] < 8:
+            return Fm.pad_channels8(x)
         return x.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
     return x

@@ -1,0 +1,141 @@
+"""ViT-B/16 with torchvision-identical module / parameter names (BASELINE.json config 5:
+"ViT-B/16 bf16 DDP ... pure-GEMM MFMA path, same DDP engine"; SURVEY.md §2.5 note).
+
+    conv_proj, class_token, encoder.pos_embedding,
+    encoder.layers.encoder_layer_{i}.{ln_1, self_attention.{in_proj_weight, in_proj_bias,
+    out_proj.weight, out_proj.bias}, ln_2, mlp.{0,3}.{weight,bias}}, encoder.ln, heads.head
+
+(86,567,656 parameters for B/16 @ 224, 1000 classes.)  On the GPU every GEMM -- patch
+embedding (as a stride-16 implicit-GEMM conv, small-channel mode), the fused QKV
+projection, attention output projection, both MLP projections and the head -- runs on
+the MFMA kernels in bf16 with fp32 master weights in the flat DP engine.  Attention
+(softmax(QK^T)V) uses torch's fused ``scaled_dot_product_attention``; LayerNorm and
+GELU are PyTorch ops for now.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mi355x_dp.ops import functional as Fm
+from .layers import Conv2d, Linear
+
+
+class MultiheadSelfAttention(nn.Module):
+    """Parameter layout of nn.MultiheadAttention(embed_dim, num_heads, batch_first=True)."""
+
+    def __init__(self, dim, heads, dropout=0.0):
+        super().__init__()
+        self.embed_dim, self.num_heads, self.dropout = dim, heads, dropout
+        self.head_dim = dim // heads
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * dim, dim))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * dim))
+        self.out_proj = nn.Linear(dim, dim)  # NonDynamicallyQuantizableLinear in torch; same params
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.out_proj.bias)
+
+    def forward(self, x):
+        B, T, D = x.shape
+        if x.is_cuda:
+            qkv = Fm.linear(x, self.in_proj_weight, self.in_proj_bias, out_bf16=True)
+        else:
+            qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
+        q, k, v = qkv.view(B, T, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).unbind(0)
+        o = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
+        o = o.transpose(1, 2).reshape(B, T, D)
+        if x.is_cuda:
+            return Fm.linear(o, self.out_proj.weight, self.out_proj.bias, out_bf16=True)
+        return self.out_proj(o)
+
+
+class MLPBlock(nn.Sequential):
+    def __init__(self, dim, mlp_dim, dropout=0.0):
+        super().__init__(nn.Linear(dim, mlp_dim), nn.GELU(), nn.Dropout(dropout), nn.Linear(mlp_dim, dim),
+                         nn.Dropout(dropout))
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                nn.init.normal_(m.bias, std=1e-6)
+
+    def forward(self, x):
+        if not x.is_cuda:
+            return super().forward(x)
+        h = Fm.linear(x, self[0].weight, self[0].bias, out_bf16=True)
+        h = self[2](F.gelu(h))
+        return self[4](Fm.linear(h, self[3].weight, self[3].bias, out_bf16=True))
+
+
+class EncoderBlock(nn.Module):
+    def __init__(self, heads, dim, mlp_dim, dropout=0.0, attention_dropout=0.0):
+        super().__init__()
+        self.num_heads = heads
+        self.ln_1 = nn.LayerNorm(dim, eps=1e-6)
+        self.self_attention = MultiheadSelfAttention(dim, heads, attention_dropout)
+        self.dropout = nn.Dropout(dropout)
+        self.ln_2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = MLPBlock(dim, mlp_dim, dropout)
+
+    def forward(self, x):
+        y = self.dropout(self.self_attention(self.ln_1(x))) + x
+        return self.mlp(self.ln_2(y)) + y
+
+
+class Encoder(nn.Module):
+    def __init__(self, seq_length, num_layers, heads, dim, mlp_dim, dropout=0.0, attention_dropout=0.0):
+        super().__init__()
+        self.pos_embedding = nn.Parameter(torch.empty(1, seq_length, dim).normal_(std=0.02))
+        self.dropout = nn.Dropout(dropout)
+        self.layers = nn.Sequential(OrderedDict(
+            (f"encoder_layer_{i}", EncoderBlock(heads, dim, mlp_dim, dropout, attention_dropout))
+            for i in range(num_layers)))
+        self.ln = nn.LayerNorm(dim, eps=1e-6)
+
+    def forward(self, x):
+        x = x + self.pos_embedding.to(x.dtype)
+        return self.ln(self.layers(self.dropout(x)))
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, image_size=224, patch_size=16, num_layers=12, num_heads=12, hidden_dim=768, mlp_dim=3072,
+                 dropout=0.0, attention_dropout=0.0, num_classes=1000):
+        super().__init__()
+        self.image_size, self.patch_size, self.hidden_dim = image_size, patch_size, hidden_dim
+        self.num_classes = num_classes
+        self.conv_proj = Conv2d(3, hidden_dim, kernel_size=patch_size, stride=patch_size)
+        seq = (image_size // patch_size) ** 2 + 1
+        self.class_token = nn.Parameter(torch.zeros(1, 1, hidden_dim))
+        self.encoder = Encoder(seq, num_layers, num_heads, hidden_dim, mlp_dim, dropout, attention_dropout)
+        self.seq_length = seq
+        self.heads = nn.Sequential(OrderedDict(head=Linear(hidden_dim, num_classes)))
+        fan_in = 3 * patch_size * patch_size
+        nn.init.trunc_normal_(self.conv_proj.weight, std=math.sqrt(1 / fan_in))
+        nn.init.zeros_(self.conv_proj.bias)
+        nn.init.zeros_(self.heads.head.weight)
+        nn.init.zeros_(self.heads.head.bias)
+
+    def _process_input(self, x):
+        n = x.shape[0]
+        x = self.conv_proj(x)                 # [N, D, h, w]  (channels_last on the GPU path)
+        x = x.permute(0, 2, 3, 1).reshape(n, -1, self.hidden_dim)  # NHWC storage: a free view
+        return x
+
+    def forward(self, x):
+        if x.is_cuda:
+            if x.shape[1] < 8:
+                x = Fm.pad_channels8(x)
+            else:
+                x = x.to(torch.bfloat16, memory_format=torch.channels_last)
+        x = self._process_input(x)
+        n = x.shape[0]
+        x = torch.cat([self.class_token.expand(n, -1, -1).to(x.dtype), x], dim=1)
+        x = self.encoder(x)
+        return self.heads(x[:, 0])
+
+
+def vit_b_16(num_classes=1000, image_size=224, **kw):
+    return VisionTransformer(image_size=image_size, patch_size=16, num_layers=12, num_heads=12, hidden_dim=768,
+                             mlp_dim=3072, num_classes=num_classes, **kw)

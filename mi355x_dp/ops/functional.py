@@ -76,22 +76,50 @@ def _conv_out(h, r, stride, pad):
 
 
 # ======================================================================= conv
+def pad_channels8(x: torch.Tensor) -> torch.Tensor:
+    """[N, C<=8, H, W] -> bf16 channels_last [N, 8, H, W] (zero channels appended): one 16-byte
+    chunk per pixel, the layout the small-channel (stem) conv mode of the MFMA kernel gathers."""
+    N, C, H, W = x.shape
+    out = torch.zeros((N, 8, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    out[:, :C].copy_(x)
+    return out
+
+
 class _Conv2d(torch.autograd.Function):
+    """Implicit-GEMM convolution.  Paths (chosen by channel count, all MFMA):
+      direct : C % 64 == 0                      (every ResNet conv but the stem)
+      c8     : C <= 8, input padded to 8 channels (the 7x7 stem: one 16-B chunk = one tap)
+      col    : other C (explicit im2col + GEMM)"""
+
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, stats):
         N, C, H, W = x.shape
-        K, _, R, S = weight.shape
+        K, Cw, R, S = weight.shape
         P, Q = _conv_out(H, R, stride, padding), _conv_out(W, S, stride, padding)
-        x = _nhwc(x)
         w16 = weight_bf16(weight)
+        if C <= 8 and C % 64 != 0:
+            if C != 8:
+                x = pad_channels8(x)
+                C = 8
+            mode = "c8"
+        elif C % 64 == 0:
+            mode = "direct"
+        else:
+            mode = "col"
+        x = _nhwc(x)
         st = stream_of(x)
         y = torch.empty((N, K, P, Q), dtype=BF16, device=x.device, memory_format=CL)
-        col = None
-        if C % 64 == 0:
+        saved = x
+        if mode == "direct":
             _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), ptr(stats), N, H, W, C, K, R, S,
                       stride, padding, P, Q, 0, st)
+        elif mode == "c8":
+            wp = torch.zeros((K, R, S, 8), dtype=BF16, device=x.device)
+            wp[..., :Cw].copy_(w16.permute(0, 2, 3, 1))
+            _lib.call("mi_conv2d_fwd", ptr(x), ptr(wp), ptr(y), ptr(None), ptr(stats), N, H, W, 8, K, R, S,
+                      stride, padding, P, Q, 0, st)
         else:
-            # small-C stem: explicit im2col (k = (r*S+s)*C + c) + MFMA GEMM
+            # explicit im2col (k = (r*S+s)*C + c) + MFMA GEMM
             Kr = R * S * C
             Kp = (Kr + 7) // 8 * 8
             col = torch.empty((N * P * Q, Kp), dtype=BF16, device=x.device)
@@ -100,33 +128,39 @@ class _Conv2d(torch.autograd.Function):
             wp[:, :Kr].copy_(w16.permute(0, 2, 3, 1).reshape(K, Kr))
             _lib.call("mi_gemm_nt", ptr(col), ptr(wp), ptr(y), ptr(None), ptr(stats), N * P * Q, K, Kp, Kp, Kp, K,
                       0, 0, st)
+            saved = col
         if bias is not None:
             y = y + bias.to(BF16).view(1, K, 1, 1)
-        ctx.geom = (N, C, H, W, K, R, S, stride, padding, P, Q)
+        ctx.geom = (N, C, H, W, K, Cw, R, S, stride, padding, P, Q)
         ctx.has_bias = bias is not None
         ctx.bias_param = bias
-        ctx.save_for_backward(x if col is None else col, weight, w16)
-        ctx.col_mode = col is not None
+        ctx.mode = mode
+        ctx.save_for_backward(saved, weight, w16)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        N, C, H, W, K, R, S, stride, padding, P, Q = ctx.geom
+        N, C, H, W, K, Cw, R, S, stride, padding, P, Q = ctx.geom
         xs, weight, w16 = ctx.saved_tensors
         dy = _nhwc(dy)
         st = stream_of(dy)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            if ctx.col_mode:
-                raise NotImplementedError("input gradient of a small-C (im2col) convolution")
+            if ctx.mode != "direct":
+                raise NotImplementedError("input gradient of a small-channel (stem) convolution")
             wt = torch.empty((C, R, S, K), dtype=BF16, device=dy.device)
             _lib.call("mi_conv_wtrans", ptr(w16), ptr(wt), K, R * S, C, st)
             dx = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
             _lib.call("mi_conv2d_dgrad", ptr(dy), ptr(wt), ptr(dx), N, H, W, C, K, R, S, stride, padding, P, Q, st)
         if ctx.needs_input_grad[1]:
             g = _grad_buffer(weight)
-            if not ctx.col_mode:
+            if ctx.mode == "direct":
                 _lib.call("mi_conv2d_wgrad", ptr(xs), ptr(dy), ptr(g), N, H, W, C, K, R, S, stride, padding, P, Q, st)
+            elif ctx.mode == "c8":
+                gp = torch.zeros((K, R, S, 8), dtype=torch.float32, device=dy.device)
+                _lib.call("mi_conv2d_wgrad", ptr(xs), ptr(dy), ptr(gp), N, H, W, 8, K, R, S, stride, padding, P, Q,
+                          st)
+                g.add_(gp[..., :Cw].permute(0, 3, 1, 2))
             else:
                 Kr = R * S * C
                 Kp = xs.shape[1]
@@ -307,7 +341,7 @@ class _Linear(torch.autograd.Function):
     of 8 (e.g. a 10-class head) are zero-padded to the 16-byte vector granule."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, out_bf16=False):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.dtype != BF16:
             x2 = x2.to(BF16)
@@ -326,9 +360,9 @@ class _Linear(torch.autograd.Function):
             if bias is not None:
                 bp = torch.zeros(Np, dtype=torch.float32, device=x.device)
                 bp[:N].copy_(bias)
-        y = torch.empty((M, Np), dtype=torch.float32, device=x.device)
-        _lib.call("mi_gemm_nt", ptr(x2), ptr(w16), ptr(y), ptr(bp), ptr(None), M, Np, Kd, Kd, Kd, Np, 1, 0,
-                  stream_of(x))
+        y = torch.empty((M, Np), dtype=BF16 if out_bf16 else torch.float32, device=x.device)
+        _lib.call("mi_gemm_nt", ptr(x2), ptr(w16), ptr(y), ptr(bp), ptr(None), M, Np, Kd, Kd, Kd, Np,
+                  0 if out_bf16 else 1, 0, stream_of(x))
         if Np != N:
             y = y[:, :N].contiguous()
         ctx.save_for_backward(x2, weight, w16)
@@ -373,13 +407,15 @@ class _Linear(torch.autograd.Function):
             gb = _grad_buffer(bias)
             gb.add_(dy.reshape(M, N).float().sum(0))
             db = _finish_grad(bias, gb)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x, weight, bias=None):
+def linear(x, weight, bias=None, out_bf16=False):
+    """MFMA GEMM linear layer; ``out_bf16`` keeps activations bf16 (transformer internals),
+    otherwise fp32 output (classifier heads / logits)."""
     if not x.is_cuda:
         return F.linear(x, weight, bias)
-    return _Linear.apply(x, weight, bias)
+    return _Linear.apply(x, weight, bias, bool(out_bf16))
 
 
 # ============================================================= cross entropy

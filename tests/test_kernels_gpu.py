@@ -240,3 +240,19 @@ def test_conv_bn_fused_stats(shape):
     assert rel_err(y_fused, y_ref) < 1e-2
     assert torch.allclose(bn1.running_mean, bn2.running_mean, rtol=1e-3, atol=1e-4)
     assert torch.allclose(bn1.running_var, bn2.running_var, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("C,R,s,p", [(16, 3, 1, 1), (3, 7, 2, 3), (8, 3, 2, 1)])
+def test_conv_small_channel_paths(C, R, s, p):
+    """c8 (stem) and im2col fallbacks: forward + weight gradient vs fp32 reference."""
+    from mi355x_dp.ops import conv2d
+    x = torch.randn(3, C, 30, 30, device="cuda").to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(32, C, R, R, device="cuda") * 0.1).to(BF).float().contiguous(memory_format=CL).requires_grad_()
+    y = conv2d(x, w, None, s, p)
+    wr = w.detach().clone().requires_grad_()
+    yr = F.conv2d(x.float(), wr, None, s, p)
+    assert rel_err(y, yr) < 1e-2
+    g = torch.randn_like(yr).to(BF).float()
+    y.backward(g.to(BF).contiguous(memory_format=CL))
+    yr.backward(g)
+    assert rel_err(w.grad, wr.grad) < 2e-2
