@@ -103,7 +103,7 @@ constexpr int nt_smem_u4() {
 // STAGES = 2: double buffer, next k-step's loads in flight during this one's MFMAs, 2 blocks per CU.
 // Both stage with buffer_load ... lds (16 B per lane, zero-fill by range check) and track the
 // (tap, channel-chunk) position incrementally in scalar registers.
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, bool SMALLC>
 __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
       else if (a.mode == 2)           { a_hb[i] = (int)p + a.g.pad;             a_wb[i] = (int)q + a.g.pad; }
       else                            { a_hb[i] = (int)p + dh;                  a_wb[i] = (int)q + dw; }
       // mode 4 (Cs == 8): the lane's 16-B chunk is one whole tap (8 channels), not a channel slice
-      a_base[i] = (((int)img * H + a_hb[i]) * W + a_wb[i]) * Cs + (a.mode == 4 ? 0 : lc * 8);
+      a_base[i] = (((int)img * H + a_hb[i]) * W + a_wb[i]) * Cs + (SMALLC ? 0 : lc * 8);
     } else {
       a_hb[i] = 0; a_wb[i] = 0;
       a_base[i] = m * a.lda + lc * 8;
@@ -180,15 +180,18 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
   const int nk = (a.mode == 3) ? nr * ns * (int)a.g.fCpt.d : (a.K + BK - 1) / BK;
   // wave-uniform k position: gather-space tap (kr, ks) and channel-chunk base kc
   int kr = 0, ks = 0, kc = 0;
-  // mode 4: per-LANE tap t = 8*kt + lc -> (tr4, ts4), advanced by 8 taps per k-step
-  int tr4 = lc / a.g.S, ts4 = lc - (lc / a.g.S) * a.g.S;
-  const int dts4 = 8 % a.g.S, dtr4 = 8 / a.g.S, ntaps = a.g.R * a.g.S;
+  // mode 4 (SMALLC): per-LANE tap t = 8*kt + lc -> (tr4, ts4), advanced by 8 taps per k-step
+  int tr4 = 0, ts4 = 0, dts4 = 0, dtr4 = 0, ntaps = 0;
+  if constexpr (SMALLC) {
+    tr4 = lc / a.g.S; ts4 = lc - tr4 * a.g.S;
+    dts4 = 8 % a.g.S; dtr4 = 8 / a.g.S; ntaps = a.g.R * a.g.S;
+  }
 
   auto issue_loads = [&](int kt, int buf) {
     int r, s, koffA, kB;
-    if (a.mode == 0 || a.mode == 4) {
+    if (SMALLC || a.mode == 0) {
       r = 0; s = 0;
-      koffA = (a.mode == 0) ? kt * BK : (tr4 * W + ts4) * Cs;
+      koffA = SMALLC ? (tr4 * W + ts4) * Cs : kt * BK;
       kB = kt * BK;
     } else {
       r = (a.mode == 3) ? r0 + a.g.stride * kr : kr;
@@ -200,11 +203,11 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       bool ok = a_ok[i];
-      if (a.mode == 0) {
-        ok = ok && kt * BK + lc * 8 < a.K;
-      } else if (a.mode == 4) {
+      if constexpr (SMALLC) {
         const int ih = a_hb[i] + tr4, iw = a_wb[i] + ts4;
         ok = ok && (kt * 8 + lc) < ntaps && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      } else if (a.mode == 0) {
+        ok = ok && kt * BK + lc * 8 < a.K;
       } else {
         const int ih = (a.mode == 1) ? a_hb[i] + kr : a_hb[i] - kr;
         const int iw = (a.mode == 1) ? a_wb[i] + ks : a_wb[i] - ks;
@@ -214,7 +217,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &As[(buf * BM + 32 * i + 8 * wid) * 8]), 16, vo,
                                                0, 0, 0);
     }
-    const bool kok = (a.mode != 0 && a.mode != 4) || (kt * BK + lc * 8 < a.K);
+    const bool kok = (!SMALLC && a.mode != 0) || (kt * BK + lc * 8 < a.K);
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const bool ok = b_base[i] >= 0 && kok;
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
                                                0, 0, 0);
     }
     // advance the k position
-    if (a.mode == 4) {
+    if constexpr (SMALLC) {
       ts4 += dts4; tr4 += dtr4;
       if (ts4 >= a.g.S) { ts4 -= a.g.S; ++tr4; }
     } else if (a.mode != 0) {
@@ -612,10 +615,12 @@ hipError_t launch_nt(NTArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(mrows, BM);
   int grid = a.tiles_m * cdiv(a.N, BN);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
-  if (nt_stages() == 2)
-    hipLaunchKernelGGL((nt_kernel<BM, BN, 2>), dim3(grid, classes), dim3(256), 0, st, a);
+  if (a.mode == 4)
+    hipLaunchKernelGGL((nt_kernel<BM, BN, 1, true>), dim3(grid, classes), dim3(256), 0, st, a);
+  else if (nt_stages() == 2)
+    hipLaunchKernelGGL((nt_kernel<BM, BN, 2, false>), dim3(grid, classes), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((nt_kernel<BM, BN, 1>), dim3(grid, classes), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false>), dim3(grid, classes), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

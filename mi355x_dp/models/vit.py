@@ -25,6 +25,15 @@ from mi355x_dp.ops import functional as Fm
 from .layers import Conv2d, Linear
 
 
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm whose fp32 (master) affine params follow a bf16 activation's dtype."""
+
+    def forward(self, x):
+        w = self.weight.to(x.dtype) if self.weight is not None else None
+        b = self.bias.to(x.dtype) if self.bias is not None else None
+        return F.layer_norm(x, self.normalized_shape, w, b, self.eps)
+
+
 class MultiheadSelfAttention(nn.Module):
     """Parameter layout of nn.MultiheadAttention(embed_dim, num_heads, batch_first=True)."""
 
@@ -73,10 +82,10 @@ class EncoderBlock(nn.Module):
     def __init__(self, heads, dim, mlp_dim, dropout=0.0, attention_dropout=0.0):
         super().__init__()
         self.num_heads = heads
-        self.ln_1 = nn.LayerNorm(dim, eps=1e-6)
+        self.ln_1 = LayerNorm(dim, eps=1e-6)
         self.self_attention = MultiheadSelfAttention(dim, heads, attention_dropout)
         self.dropout = nn.Dropout(dropout)
-        self.ln_2 = nn.LayerNorm(dim, eps=1e-6)
+        self.ln_2 = LayerNorm(dim, eps=1e-6)
         self.mlp = MLPBlock(dim, mlp_dim, dropout)
 
     def forward(self, x):
@@ -92,7 +101,7 @@ class Encoder(nn.Module):
         self.layers = nn.Sequential(OrderedDict(
             (f"encoder_layer_{i}", EncoderBlock(heads, dim, mlp_dim, dropout, attention_dropout))
             for i in range(num_layers)))
-        self.ln = nn.LayerNorm(dim, eps=1e-6)
+        self.ln = LayerNorm(dim, eps=1e-6)
 
     def forward(self, x):
         x = x + self.pos_embedding.to(x.dtype)

@@ -80,7 +80,8 @@ def pad_channels8(x: torch.Tensor) -> torch.Tensor:
     """[N, C<=8, H, W] -> bf16 channels_last [N, 8, H, W] (zero channels appended): one 16-byte
     chunk per pixel, the layout the small-channel (stem) conv mode of the MFMA kernel gathers."""
     N, C, H, W = x.shape
-    out = torch.zeros((N, 8, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    out = torch.empty((N, 8, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    out[:, C:].zero_()
     out[:, :C].copy_(x)
     return out
 
