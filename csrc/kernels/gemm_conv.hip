@@ -70,6 +70,9 @@ struct NTArgs {
   int accumulate;
   int tiles_m;       // m-tiles per class (mode 3) / total (others)
   int a_bytes, b_bytes;  // buffer-resource ranges (GLDS path): A / B extents in bytes
+  bf16_t* aux;       // bf16 epilogue operand, same layout as C (see epi)
+  int epi;           // bf16 epilogue op: 0 none, 1 GELU (aux <- pre-activation, C <- gelu),
+                     // 2 GELU backward (C <- acc * gelu'(aux)), 3 residual (C <- acc + aux)
   ConvGeom g;
 };
 
@@ -86,6 +89,34 @@ struct TNArgs {
 };
 
 constexpr int BK = 64;
+
+// erf-form GELU (nn.GELU default) and its derivative
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678f)) + x * 0.39894228f * __expf(-0.5f * x * x);
+}
+
+// elementwise op on one 16-byte chunk (8 bf16) of the bf16 epilogue; aux has C's layout
+__device__ __forceinline__ uint4 epilogue_op(int epi, uint4 v, bf16_t* aux) {
+  float f[8];
+  unpack8(v, f);
+  if (epi == 1) {
+    *(uint4*)aux = v;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = gelu_f(f[q]);
+  } else {
+    float g[8];
+    unpack8(*(const uint4*)aux, g);
+    if (epi == 2) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] *= gelu_grad_f(g[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] += g[q];
+    }
+  }
+  return pack8(f);
+}
 
 // ----------------------------------------------------------------- NT kernel
 // modes: 0 plain GEMM, 1 conv fwd, 2 conv dgrad (stride-1 or masked), 3 conv dgrad
@@ -346,7 +377,12 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     const int m = m0 + ml;
     if (m >= Mrows) break;
     const uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
-    if (n < a.N) *(uint4*)((bf16_t*)a.C + row_off(m) + n) = v;
+    if (n < a.N) {
+      const size_t off = row_off(m) + n;
+      uint4 o = v;
+      if (a.epi) o = epilogue_op(a.epi, v, a.aux + off);
+      *(uint4*)((bf16_t*)a.C + off) = o;
+    }
     if (a.stats) {
       float f[8];
       unpack8(v, f);
@@ -760,6 +796,21 @@ MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias, 
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.stats = out_f32 ? nullptr : stats;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.mode = 0; a.out_f32 = out_f32; a.accumulate = accumulate;
+  a.a_bytes = rsrc_bytes((int64_t)M * lda);
+  a.b_bytes = rsrc_bytes((int64_t)N * ldb);
+  a.g = make_geom(1, 1, 64, 1, 1, 1, 1, 0);
+  return (int)dispatch_nt(a, st);
+}
+
+// NT GEMM with a bf16 elementwise epilogue (NTArgs::epi): transformer MLP / residual fusion.
+MI_API int mi_gemm_nt_epi(const void* A, const void* B, void* C, const float* bias, void* aux, int epi,
+                          int M, int N, int K, int lda, int ldb, int ldc, hipStream_t st) {
+  if (K % 8 != 0 || N % 8 != 0 || ldc % 8 != 0 || epi < 0 || epi > 3 || (epi && !aux))
+    return (int)hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.stats = nullptr;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.mode = 0; a.out_f32 = 0; a.accumulate = 0; a.aux = (bf16_t*)aux; a.epi = epi;
   a.a_bytes = rsrc_bytes((int64_t)M * lda);
   a.b_bytes = rsrc_bytes((int64_t)N * ldb);
   a.g = make_geom(1, 1, 64, 1, 1, 1, 1, 0);

@@ -1,0 +1,214 @@
+// Transformer (ViT-B/16) support kernels for gfx950: LayerNorm forward / backward with the
+// residual-gradient add fused, and the bias-gradient column reduction.  All bf16 activations,
+// fp32 statistics / parameters / gradients.  The GEMMs themselves (QKV, projections, MLP with
+// fused GELU and residual epilogues) are the MFMA kernels of gemm_conv.hip.
+#include "common.h"
+
+namespace {
+
+constexpr int LN_MAXV = 8;  // 4-element (8-byte) vectors per lane: D <= 64 * 4 * 8 = 2048
+
+__device__ __forceinline__ void load4(const bf16_t* p, float* f) {
+  const uint2 v = *(const uint2*)p;
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+__device__ __forceinline__ void store4(bf16_t* p, const float* f) {
+  *(uint2*)p = make_uint2(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]));
+}
+
+// One wave per row; lane owns 4-element vectors v = lane + 64 i (coalesced 512-B wave accesses).
+// y = (x - mean) * rstd * w + b; the row stays in registers between the two reduction passes.
+template <int LN_V>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, bf16_t* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = D >> 2;
+  const bf16_t* xr = x + (size_t)row * D;
+  float v[LN_V][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_V; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      load4(xr + 4 * c, v[i]);
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_V; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+  bf16_t* yr = y + (size_t)row * D;
+#pragma unroll
+  for (int i = 0; i < LN_V; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      const float4 wv = *(const float4*)(w + 4 * c);
+      const float4 bv = *(const float4*)(b + 4 * c);
+      float o[4] = {(v[i][0] - mean) * rstd * wv.x + bv.x, (v[i][1] - mean) * rstd * wv.y + bv.y,
+                    (v[i][2] - mean) * rstd * wv.z + bv.z, (v[i][3] - mean) * rstd * wv.w + bv.w};
+      store4(yr + 4 * c, o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// dx = dres + rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
+// dw += sum_rows dy * xhat, db += sum_rows dy: per-lane register partials over the rows this
+// wave visits (grid-stride), reduced across the block's 4 waves in LDS, one atomic per column.
+template <int LN_V>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in,
+                                                     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                     float* __restrict__ dw, float* __restrict__ db, int M, int D) {
+  extern __shared__ float red[];  // [4][D]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nv = D >> 2;
+  float pw[LN_V][4], pb[LN_V][4];
+#pragma unroll
+  for (int i = 0; i < LN_V; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { pw[i][e] = 0.f; pb[i][e] = 0.f; }
+
+  for (int row = blockIdx.x * 4 + wv; row < M; row += gridDim.x * 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    const bf16_t* dyr = dy + (size_t)row * D;
+    const bf16_t* xr = x + (size_t)row * D;
+    float xh[LN_V][4], g[LN_V][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_V; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nv) {
+        float d[4];
+        load4(dyr + 4 * c, d);
+        load4(xr + 4 * c, xh[i]);
+        const float4 wq = *(const float4*)(w + 4 * c);
+        const float wa[4] = {wq.x, wq.y, wq.z, wq.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[i][e] = (xh[i][e] - mean) * rstd;
+          g[i][e] = d[e] * wa[e];
+          s1 += g[i][e];
+          s2 += g[i][e] * xh[i][e];
+          pw[i][e] += d[e] * xh[i][e];
+          pb[i][e] += d[e];
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+    bf16_t* dxr = dx + (size_t)row * D;
+#pragma unroll
+    for (int i = 0; i < LN_V; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nv) {
+        float o[4], r[4] = {0.f, 0.f, 0.f, 0.f};
+        if (dres) load4(dres + (size_t)row * D + 4 * c, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = r[e] + rstd * (g[i][e] - m1 - xh[i][e] * m2);
+        store4(dxr + 4 * c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < LN_V; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nv) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[wv * D + 4 * c + e] = pass ? pb[i][e] : pw[i][e];
+      }
+    }
+    __syncthreads();
+    float* dst = pass ? db : dw;
+    for (int col = threadIdx.x; col < D; col += 256)
+      atomicAdd(dst + col, red[col] + red[D + col] + red[2 * D + col] + red[3 * D + col]);
+  }
+}
+
+// out[n] += sum_m X[m][n] (bf16 X, row stride ld): lane owns an 8-column chunk, the block's 4
+// waves split the rows of a row slab, LDS reduction, one fp32 atomic per column per block.
+__global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ X, float* __restrict__ out,
+                                                     int M, int N, int ld, int rows_per_block) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = (blockIdx.x * 64 + lane) * 8;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (n < N) {
+    for (int m = r0 + wv; m < r1; m += 4) {
+      float f[8];
+      unpack8(*(const uint4*)(X + (size_t)m * ld + n), f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += f[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[wv][lane * 8 + q] = acc[q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int col = blockIdx.x * 512 + c;
+    if (col < N) atomicAdd(out + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  }
+}
+
+}  // namespace
+
+MI_API int mi_layernorm_fwd(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                            int M, int D, float eps, hipStream_t st) {
+  if (D % 4 != 0 || D > 64 * 4 * LN_MAXV || M <= 0) return (int)hipErrorInvalidValue;
+#define MI_LN_FWD(V)                                                                                    \
+  case V:                                                                                               \
+    hipLaunchKernelGGL(ln_fwd_kernel<V>, dim3(cdiv(M, 4)), dim3(256), 0, st, (const bf16_t*)x, w, b,     \
+                       (bf16_t*)y, mean, rstd, M, D, eps);                                              \
+    break;
+  switch (cdiv(D, 256)) {
+    MI_LN_FWD(1) MI_LN_FWD(2) MI_LN_FWD(3) MI_LN_FWD(4) MI_LN_FWD(5) MI_LN_FWD(6) MI_LN_FWD(7) MI_LN_FWD(8)
+  }
+#undef MI_LN_FWD
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                            const void* dres, void* dx, float* dw, float* db, int M, int D, hipStream_t st) {
+  if (D % 4 != 0 || D > 64 * 4 * LN_MAXV || M <= 0) return (int)hipErrorInvalidValue;
+  const int blocks = min(cdiv(M, 4), 1024);
+  const size_t lds = (size_t)4 * D * sizeof(float);
+#define MI_LN_BWD(V)                                                                                    \
+  case V:                                                                                               \
+    hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(blocks), dim3(256), lds, st, (const bf16_t*)dy,            \
+                       (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, dw, db, M, D);  \
+    break;
+  switch (cdiv(D, 256)) {
+    MI_LN_BWD(1) MI_LN_BWD(2) MI_LN_BWD(3) MI_LN_BWD(4) MI_LN_BWD(5) MI_LN_BWD(6) MI_LN_BWD(7) MI_LN_BWD(8)
+  }
+#undef MI_LN_BWD
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_colsum_bf16(const void* X, float* out, int M, int N, int ld, hipStream_t st) {
+  if (N % 8 != 0 || ld % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
+  const int bx = cdiv(N, 512);
+  int by = max(1, min(cdiv(M, 64), 2048 / bx));
+  const int rpb = cdiv(M, by);
+  by = cdiv(M, rpb);
+  hipLaunchKernelGGL(colsum_kernel, dim3(bx, by), dim3(256), 0, st, (const bf16_t*)X, out, M, N, ld, rpb);
+  return (int)hipGetLastError();
+}

@@ -8,9 +8,10 @@
 (86,567,656 parameters for B/16 @ 224, 1000 classes.)  On the GPU every GEMM -- patch
 embedding (as a stride-16 implicit-GEMM conv, small-channel mode), the fused QKV
 projection, attention output projection, both MLP projections and the head -- runs on
-the MFMA kernels in bf16 with fp32 master weights in the flat DP engine.  Attention
-(softmax(QK^T)V) uses torch's fused ``scaled_dot_product_attention``; LayerNorm and
-GELU are PyTorch ops for now.
+the MFMA kernels in bf16 with fp32 master weights in the flat DP engine.  On the GPU each
+encoder block is one fused autograd node (``mi355x_dp.ops.transformer.encoder_layer``):
+native LayerNorm kernels, GELU and residual adds in the GEMM epilogues, bias gradients as
+bf16 column sums.
 """
 from __future__ import annotations
 
@@ -22,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mi355x_dp.ops import functional as Fm
+from mi355x_dp.ops import transformer as Tm
 from .layers import Conv2d, Linear
 
 
@@ -29,6 +31,8 @@ class LayerNorm(nn.LayerNorm):
     """nn.LayerNorm whose fp32 (master) affine params follow a bf16 activation's dtype."""
 
     def forward(self, x):
+        if x.is_cuda and self.elementwise_affine and self.weight.dtype == torch.float32:
+            return Tm.layer_norm(x, self.weight, self.bias, self.eps)
         w = self.weight.to(x.dtype) if self.weight is not None else None
         b = self.bias.to(x.dtype) if self.bias is not None else None
         return F.layer_norm(x, self.normalized_shape, w, b, self.eps)
@@ -88,7 +92,14 @@ class EncoderBlock(nn.Module):
         self.ln_2 = LayerNorm(dim, eps=1e-6)
         self.mlp = MLPBlock(dim, mlp_dim, dropout)
 
+    def fused_params(self):
+        return [self.get_parameter(n) for n in Tm.PARAM_ORDER]
+
     def forward(self, x):
+        fusable = (self.self_attention.dropout == 0.0 and self.dropout.p == 0.0 and self.mlp[2].p == 0.0) \
+            or not self.training
+        if x.is_cuda and fusable and self.ln_1.weight.dtype == torch.float32:
+            return Tm.encoder_layer(x, self.num_heads, self.ln_1.eps, self.fused_params())
         y = self.dropout(self.self_attention(self.ln_1(x))) + x
         return self.mlp(self.ln_2(y)) + y
 

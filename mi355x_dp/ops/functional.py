@@ -172,7 +172,10 @@ class _Conv2d(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             bias = ctx.bias_param
             gb = _grad_buffer(bias)
-            gb.add_(dy.float().sum(dim=(0, 2, 3)))
+            if K % 8 == 0:  # dy is NHWC storage: a [N*P*Q][K] row-major matrix
+                _lib.call("mi_colsum_bf16", ptr(dy), ptr(gb), N * P * Q, K, K, st)
+            else:
+                gb.add_(dy.float().sum(dim=(0, 2, 3)))
             db = _finish_grad(bias, gb)
         return dx, dw, db, None, None, None
 
@@ -406,7 +409,10 @@ class _Linear(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             bias = ctx.bias_param
             gb = _grad_buffer(bias)
-            gb.add_(dy.reshape(M, N).float().sum(0))
+            if dy2.dtype == BF16 and Np == N and dy.dtype == BF16:
+                _lib.call("mi_colsum_bf16", ptr(dy2), ptr(gb), M, N, N, st)
+            else:
+                gb.add_(dy.reshape(M, N).float().sum(0))
             db = _finish_grad(bias, gb)
         return dx, dw, db, None
 

@@ -39,3 +39,11 @@ signature("mi_augment", P, P, I, I, I, I, I, I, I, U32, P, P, P)
 signature("mi_im2col", P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_add_bf16", P, P, P, L, P)
 signature("mi_checksum", P, L, P, P)
+
+# gemm_conv.hip (epilogue-fused NT GEMM)
+signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)
+
+# transformer.hip
+signature("mi_layernorm_fwd", P, P, P, P, P, P, I, I, F, P)
+signature("mi_layernorm_bwd", P, P, P, P, P, P, P, P, P, I, I, P)
+signature("mi_colsum_bf16", P, P, I, I, I, P)

@@ -1,0 +1,221 @@
+"""Transformer (ViT-B/16) ops on the native gfx950 kernels.
+
+``encoder_layer`` runs one pre-LN encoder block (torchvision ``EncoderBlock`` semantics:
+``y = x + proj(attn(ln_1(x)))``, ``z = y + fc2(gelu(fc1(ln_2(y))))``) as ONE autograd node
+with an explicit backward, so every elementwise op rides on a kernel that runs anyway:
+
+  forward                                   backward
+  ln_1            mi_layernorm_fwd          dz -> fc2: colsum(db2), TN(dW2), NT+gelu' epilogue -> du
+  qkv = h1 Wqkvᵀ  NT (+bias)                du -> fc1: colsum, TN, NT -> dh2
+  attention       attention kernel          dy = dz + ln_2ᵀ(dh2)       (LN bwd, residual add fused)
+  y = x + o Woᵀ   NT, residual epilogue     dy -> proj: colsum, TN, NT -> do -> attention bwd -> dqkv
+  ln_2            mi_layernorm_fwd          dqkv -> colsum, TN, NT -> dh1
+  g = gelu(h2W1ᵀ) NT, GELU epilogue         dx = dy + ln_1ᵀ(dh1)       (LN bwd, residual add fused)
+  z = y + g W2ᵀ   NT, residual epilogue
+
+No torch elementwise kernels, no autograd-inserted residual-gradient adds, and the bias
+gradients are column sums of the bf16 gradient (never a fp32 copy).  Weight gradients go
+straight into the flat fp32 gradient buffer of the DP engine (``functional._grad_buffer``).
+
+Reference: the ViT-B/16 config is a BASELINE.json target (config 5), not part of the
+reference repo; semantics follow torchvision ``vision_transformer.EncoderBlock``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from . import kernels as _k  # noqa: F401
+from ._lib import ptr, stream_of
+from .functional import BF16, _finish_grad, _grad_buffer, weight_bf16
+
+F32 = torch.float32
+EPI_NONE, EPI_GELU, EPI_GELU_BWD, EPI_RESIDUAL = 0, 1, 2, 3
+
+
+# ------------------------------------------------------------------ primitives
+def _ln_fwd(x2, w, b, eps):
+    M, D = x2.shape
+    y = torch.empty_like(x2)
+    mean = torch.empty(M, dtype=F32, device=x2.device)
+    rstd = torch.empty(M, dtype=F32, device=x2.device)
+    _lib.call("mi_layernorm_fwd", ptr(x2), ptr(w), ptr(b), ptr(y), ptr(mean), ptr(rstd), M, D, float(eps),
+              stream_of(x2))
+    return y, mean, rstd
+
+
+def _ln_bwd(dy2, x2, w, b, mean, rstd, dres=None):
+    """dx (+dres), and dW / dB accumulated into the parameters' gradient sinks."""
+    M, D = x2.shape
+    dx = torch.empty_like(x2)
+    gw, gb = _grad_buffer(w), _grad_buffer(b)
+    _lib.call("mi_layernorm_bwd", ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(gw),
+              ptr(gb), M, D, stream_of(x2))
+    return dx, _finish_grad(w, gw), _finish_grad(b, gb)
+
+
+def _gemm(a2, w16, bias=None, epi=EPI_NONE, aux=None):
+    """bf16 out[M][N] = a2[M][K] · w16[N][K]ᵀ (+bias) with the fused epilogue ``epi``."""
+    M, K = a2.shape
+    N = w16.shape[0]
+    out = torch.empty((M, N), dtype=BF16, device=a2.device)
+    if epi == EPI_GELU:
+        aux = torch.empty((M, N), dtype=BF16, device=a2.device)
+    _lib.call("mi_gemm_nt_epi", ptr(a2), ptr(w16), ptr(out), ptr(bias), ptr(aux), epi, M, N, K, K, K, N,
+              stream_of(a2))
+    return (out, aux) if epi == EPI_GELU else out
+
+
+def _wgrad(weight, dy2, x2):
+    g = _grad_buffer(weight)
+    M, N = dy2.shape
+    K = x2.shape[1]
+    _lib.call("mi_gemm_tn", ptr(dy2), ptr(x2), ptr(g), N, K, M, N, K, K, stream_of(dy2))
+    return _finish_grad(weight, g)
+
+
+def _bgrad(bias, dy2):
+    g = _grad_buffer(bias)
+    M, N = dy2.shape
+    _lib.call("mi_colsum_bf16", ptr(dy2), ptr(g), M, N, N, stream_of(dy2))
+    return _finish_grad(bias, g)
+
+
+def _dgrad(dy2, w16, epi=EPI_NONE, aux=None):
+    """dX[M][K] = dY[M][N] · W[N][K] (NT against the transposed bf16 weight)."""
+    return _gemm(dy2, w16.t().contiguous(), None, epi, aux)
+
+
+# ------------------------------------------------------------------ attention
+def _attn_fwd(qkv2, B, T, H, need_grad):
+    """softmax(q kᵀ/√d) v over the packed [B·T][3·H·Dh] projection; returns o [B·T][H·Dh]."""
+    D3 = qkv2.shape[1]
+    Dh = D3 // (3 * H)
+    if not need_grad:
+        q, k, v = qkv2.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
+        o4 = F.scaled_dot_product_attention(q, k, v)
+        return o4.transpose(1, 2).reshape(B * T, H * Dh), None
+    with torch.enable_grad():
+        leaf = qkv2.detach().requires_grad_()
+        q, k, v = leaf.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
+        o4 = F.scaled_dot_product_attention(q, k, v)
+    return o4.detach().transpose(1, 2).reshape(B * T, H * Dh), (leaf, o4)
+
+
+def _attn_bwd(state, do2, B, T, H):
+    leaf, o4 = state
+    Dh = do2.shape[1] // H
+    (dqkv,) = torch.autograd.grad(o4, leaf, do2.view(B, T, H, Dh).transpose(1, 2))
+    return dqkv.contiguous()
+
+
+# ------------------------------------------------------------------ encoder layer
+PARAM_ORDER = ("ln_1.weight", "ln_1.bias", "self_attention.in_proj_weight", "self_attention.in_proj_bias",
+               "self_attention.out_proj.weight", "self_attention.out_proj.bias", "ln_2.weight", "ln_2.bias",
+               "mlp.0.weight", "mlp.0.bias", "mlp.3.weight", "mlp.3.bias")
+
+
+def _layer_forward(x2, B, T, heads, eps, params, need_grad):
+    ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
+    h1, m1, r1 = _ln_fwd(x2, ln1w, ln1b, eps)
+    qkv = _gemm(h1, weight_bf16(wqkv), bqkv)
+    o, attn = _attn_fwd(qkv, B, T, heads, need_grad)
+    y = _gemm(o, weight_bf16(wo), bo, EPI_RESIDUAL, x2)
+    h2, m2, r2 = _ln_fwd(y, ln2w, ln2b, eps)
+    g, u = _gemm(h2, weight_bf16(w1), b1, EPI_GELU)
+    z = _gemm(g, weight_bf16(w2), b2, EPI_RESIDUAL, y)
+    saved = (x2, h1, m1, r1, qkv, o, y, h2, m2, r2, u, g) if need_grad else None
+    return z, saved, attn
+
+
+class _EncoderLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, heads, eps, *params):
+        B, T, D = x.shape
+        x2 = x.reshape(B * T, D)
+        if x2.dtype != BF16:
+            x2 = x2.to(BF16)
+        x2 = x2.contiguous()
+        z, saved, attn = _layer_forward(x2, B, T, heads, eps, params, True)
+        ctx.save_for_backward(*saved, *params)
+        ctx.attn = attn
+        ctx.dims = (B, T, D, heads)
+        ctx.in_dtype = x.dtype
+        return z.view(B, T, D)
+
+    @staticmethod
+    def backward(ctx, dz):
+        B, T, D, heads = ctx.dims
+        (x2, h1, m1, r1, qkv, o, y, h2, m2, r2, u, g, ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2,
+         b2) = ctx.saved_tensors
+        dz2 = dz.reshape(B * T, D)
+        if dz2.dtype != BF16:
+            dz2 = dz2.to(BF16)
+        dz2 = dz2.contiguous()
+        # MLP
+        d_b2 = _bgrad(b2, dz2)
+        d_w2 = _wgrad(w2, dz2, g)
+        du = _dgrad(dz2, weight_bf16(w2), EPI_GELU_BWD, u)
+        d_b1 = _bgrad(b1, du)
+        d_w1 = _wgrad(w1, du, h2)
+        dh2 = _dgrad(du, weight_bf16(w1))
+        dy, d_ln2w, d_ln2b = _ln_bwd(dh2, y, ln2w, ln2b, m2, r2, dres=dz2)
+        # attention
+        d_bo = _bgrad(bo, dy)
+        d_wo = _wgrad(wo, dy, o)
+        do = _dgrad(dy, weight_bf16(wo))
+        dqkv = _attn_bwd(ctx.attn, do, B, T, heads)
+        ctx.attn = None
+        d_bqkv = _bgrad(bqkv, dqkv)
+        d_wqkv = _wgrad(wqkv, dqkv, h1)
+        dh1 = _dgrad(dqkv, weight_bf16(wqkv))
+        dx, d_ln1w, d_ln1b = _ln_bwd(dh1, x2, ln1w, ln1b, m1, r1, dres=dy)
+        dx = dx.view(B, T, D)
+        if ctx.in_dtype != BF16:
+            dx = dx.to(ctx.in_dtype)
+        return (dx, None, None, d_ln1w, d_ln1b, d_wqkv, d_bqkv, d_wo, d_bo, d_ln2w, d_ln2b, d_w1, d_b1, d_w2,
+                d_b2)
+
+
+def encoder_layer(x, heads, eps, params):
+    """x [B, T, D] (cuda) -> [B, T, D] bf16.  ``params`` in ``PARAM_ORDER``."""
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
+        return _EncoderLayer.apply(x, heads, eps, *params)
+    B, T, D = x.shape
+    x2 = x.reshape(B * T, D).to(BF16).contiguous()
+    z, _, _ = _layer_forward(x2, B, T, heads, eps, params, False)
+    return z.view(B, T, D)
+
+
+# ------------------------------------------------------------------ standalone LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if x2.dtype != BF16:
+            x2 = x2.to(BF16)
+        x2 = x2.contiguous()
+        y, mean, rstd = _ln_fwd(x2, w, b, eps)
+        ctx.save_for_backward(x2, w, b, mean, rstd)
+        ctx.shape = shape
+        ctx.in_dtype = x.dtype
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b, mean, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(x2.shape)
+        if dy2.dtype != BF16:
+            dy2 = dy2.to(BF16)
+        dx, dw, db = _ln_bwd(dy2.contiguous(), x2, w, b, mean, rstd)
+        dx = dx.view(ctx.shape)
+        if ctx.in_dtype != BF16:
+            dx = dx.to(ctx.in_dtype)
+        return dx, dw, db, None
+
+
+def layer_norm(x, weight, bias, eps):
+    """Native LayerNorm over the last dim (bf16 out, fp32 affine parameters)."""
+    return _LayerNorm.apply(x, weight, bias, eps)

@@ -63,11 +63,17 @@ def main():
     _lib.load().mi_set_glds(1); _lib.load().mi_set_nt_stages(a.stages)
 
     tot = {"fwd": [0, 0], "dgrad": [0, 0], "wgrad": [0, 0]}
-    print("| N C H K R s | count | fwd TF (ms) | dgrad TF (ms) | wgrad TF (ms) | stock fwd/dgrad/wgrad TF |")
-    print("|---|---:|---:|---:|---:|---:|")
+    print("| N C H K R s | count | fwd TF (ms) | dgrad TF (ms) | wgrad TF (ms) | roof ms (mem/mfma) | stock fwd/dgrad/wgrad TF |")
+    print("|---|---:|---:|---:|---:|---:|---:|")
+    roof_tot = 0.0
     for (N, C, H, K, R, s, p, cnt) in conv_shapes(a.model, a.batch, a.size):
         P = (H + 2 * p - R) // s + 1
         flops = 2.0 * N * P * P * K * C * R * R
+        # roofline: 2.3 PFLOP/s dense bf16 MFMA, 6 TB/s achievable HBM; activations read+written once
+        act = 2.0 * (N * H * H * C + N * P * P * K)
+        t_mem, t_mma = act / 6e9, flops / 2.3e12
+        roof = max(t_mem, t_mma)
+        roof_tot += 3 * roof * cnt
         x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
         w = (torch.randn(K, C, R, R, device="cuda") * 0.05).to(BF).contiguous(memory_format=CL)
         dy = torch.randn(N, K, P, P, device="cuda").to(BF).contiguous(memory_format=CL)
@@ -105,9 +111,10 @@ def main():
                 tot[k][1] += flops * cnt
             else:
                 cells.append("im2col")
-        print(f"| {N} {C} {H} {K} {R} {s} | {cnt} | {cells[0]} | {cells[1]} | {cells[2]} | {stock} |", flush=True)
+        print(f"| {N} {C} {H} {K} {R} {s} | {cnt} | {cells[0]} | {cells[1]} | {cells[2]} | {t_mem:.3f}/{t_mma:.3f} | {stock} |", flush=True)
     for k, (t, f) in tot.items():
         print(f"\n**{k}**: {t:.2f} ms per step-equivalent, {f / t / 1e9:.0f} TFLOP/s aggregate")
+    print(f"\n**roofline** (fwd+dgrad+wgrad, convs with C%64==0): {roof_tot:.2f} ms")
 
 
 if __name__ == "__main__":
