@@ -1,0 +1,331 @@
+// Exact softmax attention for short sequences (ViT-B/16: T = 197 tokens, head dim 64) on gfx950
+// MFMA, reading the packed QKV projection [B*T][3*H*64] and writing O [B*T][H*64] / dQKV
+// [B*T][3*H*64] in place -- no head split / merge copies around the kernel.
+//
+// One workgroup (4 waves) per (batch, head); the head's whole K and V (or Q and dO) live in LDS
+// (T <= 256 keys: <= 72 KB), so softmax is exact in one pass (no online rescaling).  Every
+// product is a v_mfma_f32_16x16x32_bf16 in "transposed" form so that an accumulator feeds the
+// next MFMA as its B operand straight from registers:
+//
+//   S^T[key][q] = K Q^T          lane: q = lane&15, keys 4g..4g+3 of the tile (g = lane>>4)
+//   O^T[dh][q]  = V^T P^T        B = P^T with the k index permuted: k-slot 8g+j <-> key
+//                                 4g+j (j<4, tile 2s) / 16+4g+j-4 (j>=4, tile 2s+1) -- exactly the
+//                                 four keys x two tiles the lane already holds; A = V^T fetched
+//                                 with the same permutation by ds_read_b64_tr_b16 (4 rows x 16 cols
+//                                 transposed per 16-lane group) from the row-major V tile.
+//
+// backward: (1) dQ kernel per q tile: P^T, dP^T = V dO^T, dS^T = P^T (dP^T - D), dQ^T = K^T dS^T,
+//               D = rowsum(dO * O) written for (2);
+//           (2) dK/dV kernel per key tile: P, dP = dO V^T in [q][key] form, dV^T += dO^T P,
+//               dK^T += Q^T dS, reduction over q in registers (no atomics).
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 64;     // head dim
+constexpr int KSTR = 72;   // LDS row stride (elements): 144 B -> conflict-free 16-B row reads
+                           // and 4-row transposed reads
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ bf16x8 g16(const bf16_t* p) { return __builtin_bit_cast(bf16x8, *(const uint4*)p); }
+
+__device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0)); }
+
+// A^T fragment for an MFMA whose k index is permuted as above: rows r_lo + q4 and r_hi + q4
+// (q4 = (lane&15)>>2) of a row-major [rows][KSTR] LDS tile, column block col0 + 4*(lane&3).
+__device__ __forceinline__ bf16x8 tr8(const bf16_t* t, int r_lo, int r_hi, int col) {
+  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, t + r_lo * KSTR + col));
+  short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, t + r_hi * KSTR + col));
+  short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v8);
+}
+
+__device__ __forceinline__ bf16x8 pack_perm(f32x4 a, f32x4 b) {
+  bf16x8 r;
+  r[0] = (__bf16)a[0]; r[1] = (__bf16)a[1]; r[2] = (__bf16)a[2]; r[3] = (__bf16)a[3];
+  r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void store4bf(bf16_t* p, f32x4 v, float s) {
+  *(uint2*)p = make_uint2(pack2bf(v[0] * s, v[1] * s), pack2bf(v[2] * s, v[3] * s));
+}
+
+// rows [0, TP) of a [T][ld] bf16 matrix (64 columns at col0) -> LDS [TP][KSTR], zero rows >= T
+__device__ __forceinline__ void stage_rows(bf16_t* dst, const bf16_t* src, int ld, int T, int TP) {
+  for (int c = threadIdx.x; c < TP * 8; c += 256) {
+    const int row = c >> 3, part = c & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < T) v = *(const uint4*)(src + (size_t)row * ld + part * 8);
+    *(uint4*)&dst[row * KSTR + part * 8] = v;
+  }
+}
+
+template <int NK2>  // keys padded to 32 * NK2 >= T
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                          float* __restrict__ lse, int T, int H, float sl2) {
+  constexpr int TP = 32 * NK2, NKT = 2 * NK2;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * KSTR];
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
+  stage_rows(Ks, base + D, ld, T, TP);
+  stage_rows(Vs, base + 2 * D, ld, T, TP);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  const int nqt = (T + 15) >> 4;
+  for (int qt = wv; qt < nqt; qt += 4) {
+    const int q = qt * 16 + li;
+    const bool qv = q < T;
+    bf16x8 qf[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) qf[h2] = qv ? g16(base + (size_t)q * ld + 32 * h2 + 8 * g) : zero8();
+    f32x4 s[NKT];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) acc = mfma(*(const bf16x8*)&Ks[(kt * 16 + li) * KSTR + 32 * h2 + 8 * g], qf[h2], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (kt * 16 + 4 * g + r >= T) acc[r] = -INFINITY;
+        m = fmaxf(m, acc[r]);
+      }
+      s[kt] = acc;
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float ms = m * sl2;
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[kt][r] * sl2 - ms);
+        s[kt][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 oa[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oa[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NK2; ++ks) {
+      const bf16x8 pb = pack_perm(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        oa[dt] = mfma(tr8(Vs, ks * 32 + 4 * g + q4, ks * 32 + 16 + 4 * g + q4, (dt * 4 + p4) * 4), pb, oa[dt]);
+    }
+    if (qv) {
+      const float inv = 1.f / l;
+      bf16_t* orow = o + ((size_t)b * T + q) * D + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4bf(orow + dt * 16 + 4 * g, oa[dt], inv);
+      if (g == 0) lse[(size_t)bh * T + q] = (ms + log2f(l)) * LN2;
+    }
+  }
+}
+
+template <int NK2>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+                                                             const bf16_t* __restrict__ o,
+                                                             const bf16_t* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             float* __restrict__ dvec, bf16_t* __restrict__ dqkv,
+                                                             int T, int H, float sl2, float scale) {
+  constexpr int TP = 32 * NK2;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * KSTR];
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
+  stage_rows(Ks, base + D, ld, T, TP);
+  stage_rows(Vs, base + 2 * D, ld, T, TP);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  const int nqt = (T + 15) >> 4;
+  for (int qt = wv; qt < nqt; qt += 4) {
+    const int q = qt * 16 + li;
+    const bool qv = q < T;
+    const size_t orow = ((size_t)b * T + q) * D + h * HD;
+    bf16x8 qf[2], df[2];
+    float dd = 0.f;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      qf[h2] = qv ? g16(base + (size_t)q * ld + 32 * h2 + 8 * g) : zero8();
+      df[h2] = qv ? g16(dout + orow + 32 * h2 + 8 * g) : zero8();
+      const bf16x8 of = qv ? g16(o + orow + 32 * h2 + 8 * g) : zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dd += (float)df[h2][j] * (float)of[j];
+    }
+    dd += __shfl_xor(dd, 16, 64);
+    dd += __shfl_xor(dd, 32, 64);
+    const float l2 = qv ? lse[(size_t)bh * T + q] * LOG2E : 0.f;
+    if (qv && g == 0) dvec[(size_t)bh * T + q] = dd;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dQ^T = K^T dS^T accumulated one 32-key step at a time (P comes from the saved LSE)
+#pragma unroll 1
+    for (int ks = 0; ks < NK2; ++ks) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int kt = 2 * ks + t;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          s = mfma(*(const bf16x8*)&Ks[(kt * 16 + li) * KSTR + 32 * h2 + 8 * g], qf[h2], s);
+          dp = mfma(*(const bf16x8*)&Vs[(kt * 16 + li) * KSTR + 32 * h2 + 8 * g], df[h2], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool valid = qv && (kt * 16 + 4 * g + r < T);
+          const float p = valid ? exp2f(s[r] * sl2 - l2) : 0.f;
+          ds[t][r] = p * (dp[r] - dd);
+        }
+      }
+      const bf16x8 sb = pack_perm(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = mfma(tr8(Ks, ks * 32 + 4 * g + q4, ks * 32 + 16 + 4 * g + q4, (dt * 4 + p4) * 4), sb, dq[dt]);
+    }
+    if (qv) {
+      bf16_t* drow = dqkv + ((size_t)b * T + q) * ld + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4bf(drow + dt * 16 + 4 * g, dq[dt], scale);
+    }
+  }
+}
+
+template <int NK2>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
+                                                              const bf16_t* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ dvec,
+                                                              bf16_t* __restrict__ dqkv, int T, int H, float sl2,
+                                                              float scale) {
+  constexpr int TP = 32 * NK2;
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[TP * KSTR];
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[TP * KSTR];
+  __shared__ float Ls[TP], Dv[TP];
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
+  stage_rows(Qs, base, ld, T, TP);
+  stage_rows(Ds, dout + (size_t)b * T * D + h * HD, D, T, TP);
+  for (int i = threadIdx.x; i < TP; i += 256) {
+    Ls[i] = i < T ? lse[(size_t)bh * T + i] * LOG2E : INFINITY;  // padded queries: P = 0
+    Dv[i] = i < T ? dvec[(size_t)bh * T + i] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  const int nkt = (T + 15) >> 4;
+  for (int kt = wv; kt < nkt; kt += 4) {
+    const int key = kt * 16 + li;
+    const bool kv = key < T;
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      kf[h2] = kv ? g16(base + (size_t)key * ld + D + 32 * h2 + 8 * g) : zero8();
+      vf[h2] = kv ? g16(base + (size_t)key * ld + 2 * D + 32 * h2 + 8 * g) : zero8();
+    }
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
+#pragma unroll 1
+    for (int qs = 0; qs < NK2; ++qs) {
+      f32x4 P[2], S[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int row = (2 * qs + t) * 16 + li;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          s = mfma(*(const bf16x8*)&Qs[row * KSTR + 32 * h2 + 8 * g], kf[h2], s);
+          dp = mfma(*(const bf16x8*)&Ds[row * KSTR + 32 * h2 + 8 * g], vf[h2], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = (2 * qs + t) * 16 + 4 * g + r;
+          const float p = kv ? exp2f(s[r] * sl2 - Ls[qq]) : 0.f;
+          P[t][r] = p;
+          S[t][r] = p * (dp[r] - Dv[qq]);
+        }
+      }
+      const bf16x8 pb = pack_perm(P[0], P[1]), sb = pack_perm(S[0], S[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int r0 = qs * 32 + 4 * g + q4, r1 = r0 + 16, col = (dt * 4 + p4) * 4;
+        dv[dt] = mfma(tr8(Ds, r0, r1, col), pb, dv[dt]);
+        dk[dt] = mfma(tr8(Qs, r0, r1, col), sb, dk[dt]);
+      }
+    }
+    if (kv) {
+      bf16_t* drow = dqkv + ((size_t)b * T + key) * ld + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store4bf(drow + D + dt * 16 + 4 * g, dk[dt], scale);
+        store4bf(drow + 2 * D + dt * 16 + 4 * g, dv[dt], 1.f);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+#define MI_ATT_SWITCH(NK2, LAUNCH)                                                                       \
+  switch (NK2) {                                                                                         \
+    case 1: LAUNCH(1); break;                                                                            \
+    case 2: LAUNCH(2); break;                                                                            \
+    case 3: LAUNCH(3); break;                                                                            \
+    case 4: LAUNCH(4); break;                                                                            \
+    case 5: LAUNCH(5); break;                                                                            \
+    case 6: LAUNCH(6); break;                                                                            \
+    case 7: LAUNCH(7); break;                                                                            \
+    case 8: LAUNCH(8); break;                                                                            \
+    default: return (int)hipErrorInvalidValue;                                                          \
+  }
+
+MI_API int mi_attn_max_seq() { return 256; }
+
+// qkv [B*T][3*H*64] bf16 (q | k | v, heads contiguous), o [B*T][H*64] bf16, lse [B*H][T] fp32
+MI_API int mi_attn_fwd(const void* qkv, void* o, float* lse, int B, int T, int H, float scale, hipStream_t st) {
+  if (T <= 0 || T > 256 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * LOG2E;
+#define L(N)                                                                                             \
+  hipLaunchKernelGGL(attn_fwd_kernel<N>, dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, T, \
+                     H, sl2)
+  MI_ATT_SWITCH((T + 31) / 32, L)
+#undef L
+  return (int)hipGetLastError();
+}
+
+// dout [B*T][H*64]; dqkv [B*T][3*H*64] fully written; dvec [B*H][T] fp32 scratch
+MI_API int mi_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse, float* dvec, void* dqkv,
+                       int B, int T, int H, float scale, hipStream_t st) {
+  if (T <= 0 || T > 256 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * LOG2E;
+#define L(N)                                                                                             \
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<N>, dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)o, \
+                     (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
+  MI_ATT_SWITCH((T + 31) / 32, L)
+#undef L
+#define L(N)                                                                                             \
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel<N>, dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv,          \
+                     (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
+  MI_ATT_SWITCH((T + 31) / 32, L)
+#undef L
+  return (int)hipGetLastError();
+}

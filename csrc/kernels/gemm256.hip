@@ -1,0 +1,272 @@
+// Deep-pipelined 256x256 NT GEMM for gfx950: C[M][N] = A[M][K] · B[N][K]^T (+bias, fused
+// bf16 epilogue ops), bf16 operands, fp32 accumulation.  Used for the large plain GEMMs
+// (ViT-B/16 projections / MLP, large-batch linear layers); gemm_conv.hip keeps the small
+// shapes and the implicit-GEMM convolutions.
+//
+// Why a second NT kernel: the 128x128 single-stage loop waits vmcnt(0) + barrier every k-step
+// (rocprofv3: SQ_WAIT_ANY ~50 % of wave cycles at M=50432 N=3072 K=768).  Here global loads stay
+// in flight across barriers:
+//
+//  * block 256x256, 8 waves (2 along M x 4 along N), wave tile 128x64 = 8x4 MFMA 16x16 tiles;
+//  * one "phase" per output quadrant (mq, nq) of the wave tile, order (0,0) (0,1) (1,1) (1,0):
+//    16 MFMAs of 16x16x32 over one BK=64 k-tile, A fragments reused in phases 0->1 and 2->3,
+//    B fragments in 1->2;
+//  * LDS = 2 k-tile buffers x 4 "parts" of 16 KB: A part mq = the 64-row slices of both wave
+//    rows that quadrant row mq reads, B part nq likewise for the columns, so a phase needs just
+//    one A part and one B part of its k-tile;
+//  * every phase issues one part (2 x 16-B buffer_load ... lds per thread) for a future k-tile,
+//    scheduled so each part lands >= 3 phases before it is read:
+//        phase 0: B0[t+1]  1: A1[t+1]  2: A0[t+2]  3: B1[t+2];
+//  * fragments are read from LDS ahead of their MFMAs (B one phase ahead in a second slot, A
+//    right after the MFMAs that last use its registers), so LDS latency overlaps MFMA execution;
+//  * waits are counted, never 0 in the loop: phase 1 vmcnt(6) (retires A1[t]), phase 3 vmcnt(4)
+//    (retires B0[t+1], A0[t+1]), each followed by the only two raw s_barriers of the k-tile (no
+//    __syncthreads, which would drain the queue); loads past the last k-tile are issued as
+//    zero-fill dummies so the counts hold in the tail;
+//  * LDS images are lane-linear (direct-to-LDS), XOR-swizzled on the source side so the 16-row
+//    ds_read_b128 fragment reads spread over the banks;
+//  * XCD-aware, M-grouped tile order (GROUP_M 8) for L2 reuse of the B panel.
+#include "common.h"
+#include "epilogue.h"
+
+namespace {
+
+constexpr int G_BM = 256, G_BN = 256, G_BK = 64;
+constexpr int PART_U4 = 128 * 8;      // 128 rows x 8 x 16-B chunks = 16 KB
+constexpr int GROUP_M = 8;
+constexpr uint32_t OOB = 0xFFFFFFF0u;
+
+struct G256Args {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  const float* bias;
+  bf16_t* aux;
+  int epi;
+  int M, N, K, lda, ldb, ldc;
+  int out_f32, accumulate;
+  int tiles_m, tiles_n;
+  int a_bytes, b_bytes;
+};
+
+__device__ __forceinline__ void vm_wait6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
+__device__ __forceinline__ void vm_wait4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// raw barrier that is also a compiler memory barrier: LDS reads of a phase must not be hoisted
+// above the barrier that publishes their part (the builtin s_barrier is not a memory op)
+__device__ __forceinline__ void phase_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * 4 * PART_U4];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // tile order: XCD remap, then GROUP_M-row groups sweeping N
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int group = bid / (GROUP_M * a.tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(a.tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % (GROUP_M * a.tiles_n)) % gsz;
+  const int tn = (bid % (GROUP_M * a.tiles_n)) / gsz;
+  const int m0 = tm * G_BM, n0 = tn * G_BN;
+  const int nk = (a.K + G_BK - 1) / G_BK;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
+
+  // per-thread load geometry, fixed across k-tiles: 2 chunks per part, LDS rows p = (i*512+tid)/8.
+  // Byte offset at k-tile t = base + 128 t while t < klim (row in range and chunk inside K),
+  // else the out-of-range offset (zero fill) -- one compare / add / select per load in the loop.
+  // Rows past M / N need no test: their offsets lie beyond the buffer resource's range (the
+  // range is exactly the operand), which zero-fills.
+  uint32_t a_vo[2][2], b_vo[2][2];
+  int klim[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = i * 512 + tid, p = idx >> 3, c = idx & 7;
+    const int gk = (c ^ (p & 7)) * 8;  // source-side swizzle: LDS chunk c of row p holds global chunk c^(p&7)
+    klim[i] = gk < a.K ? (a.K - gk + G_BK - 1) / G_BK : 0;
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      a_vo[part][i] = (uint32_t)((m0 + (p >> 6) * 128 + part * 64 + (p & 63)) * a.lda + gk) * 2u;
+      b_vo[part][i] = (uint32_t)((n0 + (p >> 5) * 64 + part * 32 + (p & 31)) * a.ldb + gk) * 2u;
+    }
+  }
+
+  // issue part `part` of operand `which` (0 = A, 1 = B) for k-tile t (zero-fill past the end)
+  auto issue = [&](int t, int which, int part) {
+    uint4* dst = smem + ((t & 1) * 4 + which * 2 + part) * PART_U4;
+    const uint32_t kb = (uint32_t)t * (G_BK * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t vo = t < klim[i] ? (which == 0 ? a_vo[part][i] : b_vo[part][i]) + kb : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(which == 0 ? rsA : rsB, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo,
+                                               0, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment registers: one A set (re-read right after the MFMAs that last use it, so the LDS
+  // latency overlaps their execution) and two B slots that swap roles each k-tile (the loop body
+  // is unrolled x2 so every slot is a fixed register set)
+  bf16x8 af[4][2], bx[2][2], by[2][2];
+  auto read_a = [&](bf16x8 (&f)[4][2], int t, int mq) {
+    const uint4* src = smem + ((t & 1) * 4 + mq) * PART_U4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        f[i][kk] = __builtin_bit_cast(bf16x8, src[(wm * 64 + i * 16 + fr) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
+  };
+  auto read_b = [&](bf16x8 (&f)[2][2], int t, int nq) {
+    const uint4* src = smem + ((t & 1) * 4 + 2 + nq) * PART_U4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        f[j][kk] = __builtin_bit_cast(bf16x8, src[(wn * 32 + j * 16 + fr) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
+  };
+  auto mma = [&](const bf16x8 (&af)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq * 4 + i][nq * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
+  };
+
+  // One k-tile = 4 quadrant phases:
+  //   q0: issue B0[t+1]; read B1[t] -> bn;                        MFMA (A0, B0[t] in bc)
+  //   q1: vmcnt(6) (A1[t] landed) + barrier; issue A1[t+1];       MFMA (A0, bn); read A1[t] -> af
+  //   q2: issue A0[t+2];                                          MFMA (A1, bn)
+  //   q3: vmcnt(4) (B0[t+1], A0[t+1] landed) + barrier; issue B1[t+2]; read B0[t+1] -> bn;
+  //                                                               MFMA (A1, bc); read A0[t+1] -> af
+  // Only q1 / q3 need a barrier: every restaged region was last read >= 1 barrier earlier by
+  // reads whose MFMAs every wave has executed before passing it.
+  auto ktile = [&](int t, bf16x8 (&bc)[2][2], bf16x8 (&bn)[2][2]) {
+    issue(t + 1, 1, 0);
+    read_b(bn, t, 1);
+    mma(af, bc, 0, 0);
+    vm_wait6();
+    phase_barrier();
+    issue(t + 1, 0, 1);
+    mma(af, bn, 0, 1);
+    read_a(af, t, 1);
+    issue(t + 2, 0, 0);
+    mma(af, bn, 1, 1);
+    vm_wait4();
+    phase_barrier();
+    issue(t + 2, 1, 1);
+    const bool more = t + 1 < nk;
+    if (more) read_b(bn, t + 1, 0);
+    mma(af, bc, 1, 0);
+    if (more) read_a(af, t + 1, 0);
+  };
+
+  // prologue: the loads steady state would have issued before k-tile 0, then A0[0] / B0[0]
+  issue(0, 0, 0); issue(0, 1, 1); issue(0, 1, 0); issue(0, 0, 1); issue(1, 0, 0); issue(1, 1, 1);
+  vm_wait6();
+  phase_barrier();
+  read_a(af, 0, 0);
+  read_b(bx, 0, 0);
+  // static priority for the second-dispatched half: the two waves sharing a SIMD stop running in
+  // lockstep, so one's MFMAs overlap the other's LDS reads / barrier waits
+  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  for (int t = 0; t < nk; t += 2) {
+    ktile(t, bx, by);
+    if (t + 1 < nk) ktile(t + 1, by, bx);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy loads of the tail still target LDS
+  __syncthreads();
+
+  // ------------------------------------------------------------------ epilogue
+  // lane holds D[n = 16j + 4fq + r][m = 16i + fr] of each 16x16 tile (weights-first MFMA)
+  if (a.out_f32) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + fr;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * fq;
+        if (n >= a.N) continue;
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if (a.bias) { v0 += a.bias[n]; v1 += a.bias[n + 1]; v2 += a.bias[n + 2]; v3 += a.bias[n + 3]; }
+        float* dst = (float*)a.C + (size_t)m * a.ldc + n;
+        if (a.accumulate) { const float4 o = *(float4*)dst; v0 += o.x; v1 += o.y; v2 += o.z; v3 += o.w; }
+        *(float4*)dst = make_float4(v0, v1, v2, v3);
+      }
+    }
+    return;
+  }
+  // bf16: each wave stages 64 rows x 64 cols at a time in its own LDS slice, then 16-B row stores
+  constexpr int CST = 72;  // padded row stride (elements)
+  bf16_t* Ct = (bf16_t*)smem + wid * 64 * CST;
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + 4 * fq;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = (a.bias && n + r < a.N) ? a.bias[n + r] : 0.f;
+  }
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = acc[mq * 4 + i][j];
+        *(uint2*)&Ct[(i * 16 + fr) * CST + j * 16 + 4 * fq] =
+            make_uint2(pack2bf(v[0] + bv[j][0], v[1] + bv[j][1]), pack2bf(v[2] + bv[j][2], v[3] + bv[j][3]));
+      }
+    lgkm_wait0();
+    const int cc = lane & 7;
+    const int n = n0 + wn * 64 + cc * 8;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int rl = s * 8 + (lane >> 3);
+      const int m = m0 + wm * 128 + mq * 64 + rl;
+      const uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
+      if (m < a.M && n < a.N) {
+        const size_t off = (size_t)m * a.ldc + n;
+        const uint4 o = a.epi ? epilogue_op(a.epi, v, a.aux + off) : v;
+        *(uint4*)((bf16_t*)a.C + off) = o;
+      }
+    }
+    lgkm_wait0();  // this wave's reads of the slice retire before the next quadrant row overwrites it
+  }
+}
+
+int rsrc_bytes256(int64_t elems) {
+  const int64_t b = elems * 2;
+  return (b > 0x7fffffffLL) ? 0 : (int)b;
+}
+
+}  // namespace
+
+// Returns hipErrorInvalidValue when the shape is outside this kernel's contract (caller falls
+// back to the 128x128 kernel).
+MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bias, void* aux, int epi, int M, int N,
+                         int K, int lda, int ldb, int ldc, int out_f32, int accumulate, hipStream_t st) {
+  if (K % 8 != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (epi && (out_f32 || !aux)) || M <= 0 || N <= 0)
+    return (int)hipErrorInvalidValue;
+  G256Args a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.aux = (bf16_t*)aux; a.epi = epi;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.out_f32 = out_f32; a.accumulate = accumulate;
+  a.tiles_m = cdiv(M, G_BM); a.tiles_n = cdiv(N, G_BN);
+  a.a_bytes = rsrc_bytes256((int64_t)M * lda);
+  a.b_bytes = rsrc_bytes256((int64_t)N * ldb);
+  if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm256_nt_kernel, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}

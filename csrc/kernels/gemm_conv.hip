@@ -19,6 +19,7 @@
 //    fragments are read transposed with ds_read_b64_tr_b16; split-K over the
 //    (huge) N*P*Q reduction with fp32 atomics into the fp32 gradient buffer.
 #include "common.h"
+#include "epilogue.h"
 #include <algorithm>
 #include <cstdlib>
 
@@ -90,33 +91,6 @@ struct TNArgs {
 
 constexpr int BK = 64;
 
-// erf-form GELU (nn.GELU default) and its derivative
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678f)); }
-__device__ __forceinline__ float gelu_grad_f(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678f)) + x * 0.39894228f * __expf(-0.5f * x * x);
-}
-
-// elementwise op on one 16-byte chunk (8 bf16) of the bf16 epilogue; aux has C's layout
-__device__ __forceinline__ uint4 epilogue_op(int epi, uint4 v, bf16_t* aux) {
-  float f[8];
-  unpack8(v, f);
-  if (epi == 1) {
-    *(uint4*)aux = v;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) f[q] = gelu_f(f[q]);
-  } else {
-    float g[8];
-    unpack8(*(const uint4*)aux, g);
-    if (epi == 2) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) f[q] *= gelu_grad_f(g[q]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) f[q] += g[q];
-    }
-  }
-  return pack8(f);
-}
 
 // ----------------------------------------------------------------- NT kernel
 // modes: 0 plain GEMM, 1 conv fwd, 2 conv dgrad (stride-1 or masked), 3 conv dgrad
@@ -787,11 +761,28 @@ MI_API int mi_conv_wtrans(const void* w, void* wt, int K, int RS, int C, hipStre
   return (int)hipGetLastError();
 }
 
+// Large plain GEMMs go to the deep-pipelined 256x256 kernel (gemm256.hip) when they fill the
+// chip with at least one wave of 256x256 tiles; MI355X_DP_GEMM256=0 disables it (A/B runs).
+extern "C" int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bias, void* aux, int epi, int M,
+                             int N, int K, int lda, int ldb, int ldc, int out_f32, int accumulate, hipStream_t st);
+static int g_gemm256 = -1;
+static bool use_gemm256(int M, int N, int K) {
+  if (g_gemm256 < 0) {
+    const char* e = getenv("MI355X_DP_GEMM256");
+    g_gemm256 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_gemm256 && K >= 128 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= 256;
+}
+
+MI_API void mi_set_gemm256(int on) { g_gemm256 = on ? 1 : 0; }
+
 // Plain GEMM, "NT": C[M][N] = A[M][K] * B[N][K]^T (+bias[N]); A, B bf16; C bf16 or fp32.
 MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias, float* stats,
                       int M, int N, int K, int lda, int ldb, int ldc,
                       int out_f32, int accumulate, hipStream_t st) {
   if (K % 8 != 0 || N % 4 != 0 || (!out_f32 && N % 8 != 0)) return (int)hipErrorInvalidValue;
+  if (!stats && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && use_gemm256(M, N, K))
+    return mi_gemm256_nt(A, B, C, bias, nullptr, 0, M, N, K, lda, ldb, ldc, out_f32, accumulate, st);
   NTArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.stats = out_f32 ? nullptr : stats;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
@@ -802,11 +793,14 @@ MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias, 
   return (int)dispatch_nt(a, st);
 }
 
+
 // NT GEMM with a bf16 elementwise epilogue (NTArgs::epi): transformer MLP / residual fusion.
 MI_API int mi_gemm_nt_epi(const void* A, const void* B, void* C, const float* bias, void* aux, int epi,
                           int M, int N, int K, int lda, int ldb, int ldc, hipStream_t st) {
   if (K % 8 != 0 || N % 8 != 0 || ldc % 8 != 0 || epi < 0 || epi > 3 || (epi && !aux))
     return (int)hipErrorInvalidValue;
+  if (use_gemm256(M, N, K) && lda % 8 == 0 && ldb % 8 == 0)
+    return mi_gemm256_nt(A, B, C, bias, aux, epi, M, N, K, lda, ldb, ldc, 0, 0, st);
   NTArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.stats = nullptr;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;

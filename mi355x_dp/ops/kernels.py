@@ -47,3 +47,12 @@ signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)
 signature("mi_layernorm_fwd", P, P, P, P, P, P, I, I, F, P)
 signature("mi_layernorm_bwd", P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_colsum_bf16", P, P, I, I, I, P)
+
+# attention.hip
+signature("mi_attn_max_seq")
+signature("mi_attn_fwd", P, P, P, I, I, I, F, P)
+signature("mi_attn_bwd", P, P, P, P, P, P, I, I, I, F, P)
+
+# gemm256.hip
+signature("mi_gemm256_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, I, P)
+signature("mi_set_gemm256", I)

@@ -88,10 +88,21 @@ def _dgrad(dy2, w16, epi=EPI_NONE, aux=None):
 
 
 # ------------------------------------------------------------------ attention
+def native_attention_ok(T, head_dim):
+    return head_dim == 64 and 0 < T <= 256
+
+
 def _attn_fwd(qkv2, B, T, H, need_grad):
-    """softmax(q kᵀ/√d) v over the packed [B·T][3·H·Dh] projection; returns o [B·T][H·Dh]."""
+    """softmax(q kᵀ/√d) v over the packed [B·T][3·H·Dh] projection; returns o [B·T][H·Dh].
+    Native kernel (csrc/kernels/attention.hip) for Dh = 64, T <= 256 (ViT-B/16: T = 197)."""
     D3 = qkv2.shape[1]
     Dh = D3 // (3 * H)
+    scale = 1.0 / (Dh ** 0.5)
+    if native_attention_ok(T, Dh):
+        o = torch.empty((B * T, H * Dh), dtype=BF16, device=qkv2.device)
+        lse = torch.empty((B * H * T,), dtype=F32, device=qkv2.device)
+        _lib.call("mi_attn_fwd", ptr(qkv2), ptr(o), ptr(lse), B, T, H, float(scale), stream_of(qkv2))
+        return o, (("native", lse, o) if need_grad else None)
     if not need_grad:
         q, k, v = qkv2.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
         o4 = F.scaled_dot_product_attention(q, k, v)
@@ -100,14 +111,45 @@ def _attn_fwd(qkv2, B, T, H, need_grad):
         leaf = qkv2.detach().requires_grad_()
         q, k, v = leaf.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
         o4 = F.scaled_dot_product_attention(q, k, v)
-    return o4.detach().transpose(1, 2).reshape(B * T, H * Dh), (leaf, o4)
+    return o4.detach().transpose(1, 2).reshape(B * T, H * Dh), ("sdpa", leaf, o4)
 
 
-def _attn_bwd(state, do2, B, T, H):
-    leaf, o4 = state
+def _attn_bwd(state, qkv2, do2, B, T, H):
     Dh = do2.shape[1] // H
+    if state[0] == "native":
+        _, lse, o = state
+        dqkv = torch.empty_like(qkv2)
+        dvec = torch.empty((B * H * T,), dtype=F32, device=qkv2.device)
+        _lib.call("mi_attn_bwd", ptr(qkv2), ptr(o), ptr(do2), ptr(lse), ptr(dvec), ptr(dqkv), B, T, H,
+                  float(1.0 / (Dh ** 0.5)), stream_of(qkv2))
+        return dqkv
+    _, leaf, o4 = state
     (dqkv,) = torch.autograd.grad(o4, leaf, do2.view(B, T, H, Dh).transpose(1, 2))
     return dqkv.contiguous()
+
+
+def attention(qkv2, B, T, H):
+    """Differentiable packed-QKV attention (standalone use / tests)."""
+    return _Attention.apply(qkv2, B, T, H)
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv2, B, T, H):
+        qkv2 = qkv2.to(BF16).contiguous()
+        o, state = _attn_fwd(qkv2, B, T, H, True)
+        ctx.state = state
+        ctx.dims = (B, T, H)
+        ctx.save_for_backward(qkv2)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        (qkv2,) = ctx.saved_tensors
+        B, T, H = ctx.dims
+        dqkv = _attn_bwd(ctx.state, qkv2, do.to(BF16).contiguous(), B, T, H)
+        ctx.state = None
+        return dqkv, None, None, None
 
 
 # ------------------------------------------------------------------ encoder layer
@@ -165,7 +207,7 @@ class _EncoderLayer(torch.autograd.Function):
         d_bo = _bgrad(bo, dy)
         d_wo = _wgrad(wo, dy, o)
         do = _dgrad(dy, weight_bf16(wo))
-        dqkv = _attn_bwd(ctx.attn, do, B, T, heads)
+        dqkv = _attn_bwd(ctx.attn, qkv, do, B, T, heads)
         ctx.attn = None
         d_bqkv = _bgrad(bqkv, dqkv)
         d_wqkv = _wgrad(wqkv, dqkv, h1)
