@@ -1,0 +1,192 @@
+// Native gradient-bucket reducer for the mi355x_dp data-parallel engine (SURVEY.md §2.3 N1:
+// the counterpart of torch DDP's C++ Reducer, reached by the reference through
+// torch.nn.parallel.DistributedDataParallel at cifar10-distributed-smddp-gpu.py:148).
+//
+// The gradients of every parameter live in ONE flat fp32 buffer (mi355x_dp.parallel.flat),
+// so a bucket is a contiguous slice -- no copy-in / copy-out kernels.  This object owns:
+//
+//  * the link-aware bucket planner: bucket sizes from an alpha-beta model of a ring
+//    all-reduce over point-to-point xGMI (7 links x ~153 GB/s per MI355X): the first bucket
+//    small (communication starts after the first few backward kernels), the LAST bucket
+//    small (its all-reduce is the exposed tail after backward ends), the middle ones large
+//    enough that the per-collective latency is <= ~10 % of the transfer;
+//  * grad-ready bookkeeping: backward kernels (or post-accumulate hooks) call mark_ready(i);
+//    when every parameter of the next bucket in order is ready, its all-reduce is launched
+//    on the process group -- in the same order on every rank, so collectives match;
+//  * the comm itself is asynchronous on the backend's side stream (RCCL / native smddp
+//    backend: the collective waits on an event of the producing stream, Work::wait makes
+//    the consumer stream wait on the completion event -- no host synchronisation);
+//  * finish(): launch buckets whose parameters never got a gradient (unused parameters:
+//    their zeroed slice is still reduced, matching DDP's find_unused_parameters=False
+//    semantics where every rank participates) and wait for all outstanding work.
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Types.hpp>
+#include <torch/csrc/distributed/c10d/Work.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <vector>
+
+namespace mi_ddp {
+
+// Ring all-reduce time model T(S) = alpha + 2 (W-1)/W * S / B.  Returns the bucket size at
+// which alpha is `overhead` of T, clamped to [min_bytes, max_bytes].
+int64_t link_aware_cap(int world, double link_gbps, int links, double alpha_us, double overhead, int64_t min_bytes,
+                       int64_t max_bytes) {
+  if (world <= 1) return max_bytes;
+  // a ring uses one link per direction; RCCL runs several rings over disjoint links
+  const double rings = std::max(1, std::min(links, world - 1));
+  const double bw = link_gbps * 1e9 * rings;                         // bytes / s
+  const double factor = 2.0 * (world - 1) / world;
+  const double s = alpha_us * 1e-6 * (1.0 - overhead) / overhead * bw / factor;
+  return std::max(min_bytes, std::min(max_bytes, (int64_t)s));
+}
+
+// Greedy contiguous buckets over tensors in backward order.  The first bucket is capped at
+// `first`, the last at `last` (planned from the end), the rest at `cap`.
+std::vector<std::vector<int64_t>> plan_buckets(const std::vector<int64_t>& bytes, int64_t cap, int64_t first,
+                                               int64_t last) {
+  const int64_t n = (int64_t)bytes.size();
+  std::vector<std::vector<int64_t>> out;
+  if (n == 0) return out;
+  // tail bucket: the trailing tensors up to `last` bytes (at least one)
+  int64_t tail_begin = n - 1, acc = bytes[n - 1];
+  while (tail_begin > 0 && acc + bytes[tail_begin - 1] <= last) acc += bytes[--tail_begin];
+  std::vector<int64_t> cur;
+  int64_t cur_bytes = 0, lim = first;
+  for (int64_t i = 0; i < tail_begin; ++i) {
+    if (!cur.empty() && cur_bytes + bytes[i] > lim) {
+      out.push_back(cur);
+      cur.clear();
+      cur_bytes = 0;
+      lim = cap;
+    }
+    cur.push_back(i);
+    cur_bytes += bytes[i];
+  }
+  if (!cur.empty()) out.push_back(cur);
+  std::vector<int64_t> tail;
+  for (int64_t i = tail_begin; i < n; ++i) tail.push_back(i);
+  out.push_back(tail);
+  return out;
+}
+
+class Reducer {
+ public:
+  Reducer(at::Tensor flat_grad, std::vector<int64_t> offsets, std::vector<int64_t> numels,
+          std::vector<std::vector<int64_t>> buckets, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t align)
+      : grad_(std::move(flat_grad)), offsets_(std::move(offsets)), numels_(std::move(numels)),
+        buckets_(std::move(buckets)), pg_(std::move(pg)) {
+    TORCH_CHECK(offsets_.size() == numels_.size(), "offsets / numels mismatch");
+    const int64_t np = (int64_t)offsets_.size();
+    bucket_of_.assign(np, -1);
+    for (size_t b = 0; b < buckets_.size(); ++b) {
+      TORCH_CHECK(!buckets_[b].empty(), "empty bucket");
+      int64_t lo = INT64_MAX, hi = 0;
+      for (int64_t i : buckets_[b]) {
+        TORCH_CHECK(i >= 0 && i < np && bucket_of_[i] < 0, "bad bucket plan");
+        bucket_of_[i] = (int64_t)b;
+        lo = std::min(lo, offsets_[i]);
+        hi = std::max(hi, offsets_[i] + numels_[i]);
+      }
+      hi = std::min(grad_.numel(), (hi + align - 1) / align * align);
+      ranges_.emplace_back(lo, hi);
+    }
+    for (int64_t i = 0; i < np; ++i) TORCH_CHECK(bucket_of_[i] >= 0, "parameter ", i, " not in any bucket");
+    reset();
+  }
+
+  void reset() {
+    std::lock_guard<std::mutex> g(mu_);
+    pending_.assign(buckets_.size(), 0);
+    for (size_t b = 0; b < buckets_.size(); ++b) pending_[b] = (int64_t)buckets_[b].size();
+    ready_.assign(buckets_.size(), false);
+    param_ready_.assign(offsets_.size(), false);
+    works_.clear();
+    next_ = 0;
+  }
+
+  void mark_ready(int64_t i) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(i >= 0 && i < (int64_t)param_ready_.size(), "parameter index out of range");
+    if (param_ready_[i]) return;
+    param_ready_[i] = true;
+    const int64_t b = bucket_of_[i];
+    if (--pending_[b] == 0) {
+      ready_[b] = true;
+      launch_ready_locked();
+    }
+  }
+
+  void finish() {
+    std::vector<c10::intrusive_ptr<c10d::Work>> works;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      std::fill(ready_.begin(), ready_.end(), true);
+      launch_ready_locked();
+      works.swap(works_);
+    }
+    for (auto& w : works) w->wait();
+  }
+
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  int64_t launched() const { return next_; }
+  int64_t comm_calls() const { return comm_calls_; }
+  int64_t comm_bytes() const { return comm_bytes_; }
+  std::vector<std::pair<int64_t, int64_t>> ranges() const { return ranges_; }
+  std::vector<std::vector<int64_t>> buckets() const { return buckets_; }
+
+ private:
+  void launch_ready_locked() {
+    while (next_ < (int64_t)buckets_.size() && ready_[next_]) {
+      if (pg_ && pg_->getSize() > 1) {
+        const auto& r = ranges_[next_];
+        std::vector<at::Tensor> ts{grad_.narrow(0, r.first, r.second - r.first)};
+        c10d::AllreduceOptions opts;
+        opts.reduceOp = c10d::ReduceOp::SUM;
+        works_.push_back(pg_->allreduce(ts, opts));
+        ++comm_calls_;
+        comm_bytes_ += (r.second - r.first) * grad_.element_size();
+      }
+      ++next_;
+    }
+  }
+
+  at::Tensor grad_;
+  std::vector<int64_t> offsets_, numels_;
+  std::vector<std::vector<int64_t>> buckets_;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  std::vector<std::pair<int64_t, int64_t>> ranges_;
+  std::vector<int64_t> bucket_of_, pending_;
+  std::vector<bool> ready_, param_ready_;
+  std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  int64_t next_ = 0, comm_calls_ = 0, comm_bytes_ = 0;
+  std::mutex mu_;
+};
+
+}  // namespace mi_ddp
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  namespace py = pybind11;
+  m.doc() = "mi355x_dp native gradient-bucket reducer";
+  m.def("link_aware_cap", &mi_ddp::link_aware_cap, py::arg("world"), py::arg("link_gbps") = 153.0,
+        py::arg("links") = 7, py::arg("alpha_us") = 25.0, py::arg("overhead") = 0.1,
+        py::arg("min_bytes") = int64_t(4) << 20, py::arg("max_bytes") = int64_t(64) << 20);
+  m.def("plan_buckets", &mi_ddp::plan_buckets, py::arg("bytes"), py::arg("cap"), py::arg("first"), py::arg("last"));
+  py::class_<mi_ddp::Reducer>(m, "Reducer")
+      .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>, std::vector<std::vector<int64_t>>,
+                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t>(),
+           py::arg("flat_grad"), py::arg("offsets"), py::arg("numels"), py::arg("buckets"), py::arg("process_group"),
+           py::arg("align") = 64)
+      .def("reset", &mi_ddp::Reducer::reset)
+      .def("mark_ready", &mi_ddp::Reducer::mark_ready, py::call_guard<py::gil_scoped_release>())
+      .def("finish", &mi_ddp::Reducer::finish, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("num_buckets", &mi_ddp::Reducer::num_buckets)
+      .def_property_readonly("launched", &mi_ddp::Reducer::launched)
+      .def_property_readonly("comm_calls", &mi_ddp::Reducer::comm_calls)
+      .def_property_readonly("comm_bytes", &mi_ddp::Reducer::comm_bytes)
+      .def_property_readonly("ranges", &mi_ddp::Reducer::ranges)
+      .def_property_readonly("buckets", &mi_ddp::Reducer::buckets);
+}

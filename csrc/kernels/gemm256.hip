@@ -246,6 +246,175 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   }
 }
 
+// ----------------------------------------------------------------- TN (weight gradients)
+// C[M][N] (fp32) += sum_k A[k][M] B[k][N] over this block's k range (split-K: fp32 atomics).
+// Same phase / part / wait schedule as the NT kernel; the parts are k-major images
+// [64 k][128 cols] (two 64-col slices, one per wave row / column group) and the MFMA fragments
+// are gathered with ds_read_b64_tr_b16 (4 k-rows x 16 cols transposed per 16-lane group).  8-byte
+// units of row k are XOR-swizzled by tr_swz(k) (applied on the load side, 16-B granular) so the
+// 4 rows of a transposed read and the 4 lane groups hit different banks.
+struct G256TNArgs {
+  const bf16_t* A;  // [K][lda]
+  const bf16_t* B;  // [K][ldb]
+  float* C;         // [M][ldc]
+  int M, N, K, lda, ldb, ldc;
+  int tiles_m, tiles_n, splits, kt_per_split;
+  int a_bytes, b_bytes;
+};
+
+__device__ __forceinline__ int tr_swz32(int k) { return (4 * (k & 3) + 16 * ((k >> 3) & 1)) & 31; }
+
+__global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * 4 * PART_U4];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+
+  const int nblk_tile = a.tiles_m * a.tiles_n;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / nblk_tile, tb = bid - split * nblk_tile;
+  const int group = tb / (GROUP_M * a.tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(a.tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (tb % (GROUP_M * a.tiles_n)) % gsz;
+  const int tn = (tb % (GROUP_M * a.tiles_n)) / gsz;
+  const int m0 = tm * G_BM, n0 = tn * G_BN;
+  const int kt0 = split * a.kt_per_split;
+  const int nk = min(a.kt_per_split, (a.K + G_BK - 1) / G_BK - kt0);
+  if (nk <= 0) return;
+  const int kbeg = kt0 * G_BK;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
+
+  // load geometry: chunk idx = i*512 + tid -> part row k = idx>>4, LDS chunk c = idx&15 holding
+  // global chunk c ^ swz(k): cols (c'>>3)*128 + part*64 + (c'&7)*8 of the block's 256 (A: m, B: n)
+  uint32_t a_vo[2][2], b_vo[2][2];
+  int klim[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = i * 512 + tid, k = idx >> 4, c = idx & 15;
+    const int gc = c ^ (tr_swz32(k) >> 1);
+    const int kk = kbeg + k;
+    klim[i] = kk < a.K ? min(nk, (a.K - kk + G_BK - 1) / G_BK) : 0;
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const int col = (gc >> 3) * 128 + part * 64 + (gc & 7) * 8;
+      const int ma = m0 + col, nb = n0 + col;
+      a_vo[part][i] = ma < a.M ? (uint32_t)(kk * a.lda + ma) * 2u : OOB;
+      b_vo[part][i] = nb < a.N ? (uint32_t)(kk * a.ldb + nb) * 2u : OOB;
+    }
+  }
+  const uint32_t a_kstep = (uint32_t)(G_BK * a.lda) * 2u, b_kstep = (uint32_t)(G_BK * a.ldb) * 2u;
+
+  auto issue = [&](int t, int which, int part) {
+    uint4* dst = smem + ((t & 1) * 4 + which * 2 + part) * PART_U4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t base = which == 0 ? a_vo[part][i] : b_vo[part][i];
+      const uint32_t vo = (t < klim[i] && base != OOB) ? base + (uint32_t)t * (which == 0 ? a_kstep : b_kstep) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(which == 0 ? rsA : rsB, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo,
+                                               0, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], bx[2][2], by[2][2];
+  // transposed fragment: cols base..base+15 (lane col li), k rows kk*32 + 8g + {0..7}
+  auto tr_frag = [&](const uint4* part_img, int colbase, int kk) {
+    const uint2* img = (const uint2*)part_img;  // [64 k][32 units of 8 B]
+    const int u = colbase / 4 + p4;
+    const int k1 = kk * 32 + 8 * g + q4, k2 = k1 + 4;
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, &img[k1 * 32 + (u ^ tr_swz32(k1))]));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, &img[k2 * 32 + (u ^ tr_swz32(k2))]));
+    short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v8);
+  };
+  auto read_a = [&](bf16x8 (&f)[4][2], int t, int mq) {
+    const uint4* src = smem + ((t & 1) * 4 + mq) * PART_U4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) f[i][kk] = tr_frag(src, wm * 64 + i * 16, kk);
+  };
+  auto read_b = [&](bf16x8 (&f)[2][2], int t, int nq) {
+    const uint4* src = smem + ((t & 1) * 4 + 2 + nq) * PART_U4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) f[j][kk] = tr_frag(src, (wn >> 1) * 64 + (wn & 1) * 32 + j * 16, kk);
+  };
+  auto mma = [&](const bf16x8 (&af_)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq * 4 + i][nq * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af_[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
+  };
+  auto ktile = [&](int t, bf16x8 (&bc)[2][2], bf16x8 (&bn)[2][2]) {
+    issue(t + 1, 1, 0);
+    read_b(bn, t, 1);
+    mma(af, bc, 0, 0);
+    vm_wait6();
+    phase_barrier();
+    issue(t + 1, 0, 1);
+    mma(af, bn, 0, 1);
+    read_a(af, t, 1);
+    issue(t + 2, 0, 0);
+    mma(af, bn, 1, 1);
+    vm_wait4();
+    phase_barrier();
+    issue(t + 2, 1, 1);
+    const bool more = t + 1 < nk;
+    if (more) read_b(bn, t + 1, 0);
+    mma(af, bc, 1, 0);
+    if (more) read_a(af, t + 1, 0);
+  };
+
+  issue(0, 0, 0); issue(0, 1, 1); issue(0, 1, 0); issue(0, 0, 1); issue(1, 0, 0); issue(1, 1, 1);
+  vm_wait6();
+  phase_barrier();
+  read_a(af, 0, 0);
+  read_b(bx, 0, 0);
+  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  for (int t = 0; t < nk; t += 2) {
+    ktile(t, bx, by);
+    if (t + 1 < nk) ktile(t + 1, by, bx);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // lane holds D[n = 16j + 4g + r][m = 16i + li]: C[m][n..n+3]
+  // B part nq holds, for wave column wn, cols (wn>>1)*128 + nq*64 + (wn&1)*32 + j*16 of the tile
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + li;
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nq = j >> 1, jj = j & 1;
+      const int n = n0 + (wn >> 1) * 128 + nq * 64 + (wn & 1) * 32 + jj * 16 + 4 * g;
+      if (n >= a.N) continue;
+      float* dst = a.C + (size_t)m * a.ldc + n;
+      const f32x4 v = acc[i][j];
+      if (a.splits > 1) {
+        atomicAdd(dst, v[0]); atomicAdd(dst + 1, v[1]); atomicAdd(dst + 2, v[2]); atomicAdd(dst + 3, v[3]);
+      } else {
+        const float4 o = *(float4*)dst;
+        *(float4*)dst = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+      }
+    }
+  }
+}
+
 int rsrc_bytes256(int64_t elems) {
   const int64_t b = elems * 2;
   return (b > 0x7fffffffLL) ? 0 : (int)b;
@@ -268,5 +437,26 @@ MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bia
   a.b_bytes = rsrc_bytes256((int64_t)N * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(gemm256_nt_kernel, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// C[M][N] (fp32) += A[K][M]^T B[K][N]; split-K chosen to fill the chip.
+MI_API int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+                         hipStream_t st) {
+  if (M % 8 != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || M <= 0 || N <= 0 || K <= 0)
+    return (int)hipErrorInvalidValue;
+  G256TNArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.tiles_m = cdiv(M, G_BM); a.tiles_n = cdiv(N, G_BN);
+  const int tiles = a.tiles_m * a.tiles_n, nkt = cdiv(K, G_BK);
+  // about one wave of blocks (1 block per CU), >= 8 k-tiles per split
+  int splits = max(1, min((256 + tiles / 2) / tiles, nkt / 8));
+  a.kt_per_split = cdiv(nkt, splits);
+  a.splits = cdiv(nkt, a.kt_per_split);
+  a.a_bytes = rsrc_bytes256((int64_t)K * lda);
+  a.b_bytes = rsrc_bytes256((int64_t)K * ldb);
+  if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm256_tn_kernel, dim3(tiles * a.splits), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }

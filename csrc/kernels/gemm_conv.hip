@@ -776,6 +776,15 @@ static bool use_gemm256(int M, int N, int K) {
 
 MI_API void mi_set_gemm256(int on) { g_gemm256 = on ? 1 : 0; }
 
+// TN: the 256x256 kernel wins only without heavy split-K (>= 128 output tiles); weight-gradient
+// shapes with few output tiles (ViT: 9-36) stay on the 128x128 split-K kernel (L2 locality).
+extern "C" int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+                             hipStream_t st);
+static bool use_gemm256_tn(int M, int N, int K) {
+  use_gemm256(0, 0, 0);  // env init
+  return g_gemm256 && K >= 1024 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= 128;
+}
+
 // Plain GEMM, "NT": C[M][N] = A[M][K] * B[N][K]^T (+bias[N]); A, B bf16; C bf16 or fp32.
 MI_API int mi_gemm_nt(const void* A, const void* B, void* C, const float* bias, float* stats,
                       int M, int N, int K, int lda, int ldb, int ldc,
@@ -815,6 +824,7 @@ MI_API int mi_gemm_nt_epi(const void* A, const void* B, void* C, const float* bi
 MI_API int mi_gemm_tn(const void* A, const void* B, float* C, int M, int N, int K,
                       int lda, int ldb, int ldc, hipStream_t st) {
   if (M % 8 != 0 || N % 8 != 0) return (int)hipErrorInvalidValue;
+  if (lda % 8 == 0 && ldb % 8 == 0 && use_gemm256_tn(M, N, K)) return mi_gemm256_tn(A, B, C, M, N, K, lda, ldb, ldc, st);
   TNArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.mode = 0;

@@ -102,10 +102,20 @@ def build_comm(force=False, verbose=True):
     return _smddp_build.build(srcs, NATIVE, force=force, verbose=verbose)
 
 
+def build_reducer(force=False, verbose=True):
+    """csrc/ddp/reducer.cpp -> mi355x_dp/_native/_reducer_ext*.so (libtorch + c10d only)."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "ddp", "*.cpp")))
+    if not srcs:
+        return None
+    from mi355x_dp.parallel import _smddp_build
+    return _smddp_build.build(srcs, NATIVE, force=force, verbose=verbose, name="_reducer_ext", hip=False)
+
+
 def build_all(force=False, verbose=True):
     outs = [build_kernels(force, verbose), build_launcher(force, verbose)]
     try:
         outs.append(build_comm(force, verbose))
+        outs.append(build_reducer(force, verbose))
     except ImportError:
         pass
     return [o for o in outs if o]
@@ -120,5 +130,7 @@ if __name__ == "__main__":
         build_launcher(force)
     elif what == "comm":
         build_comm(force)
+    elif what == "reducer":
+        build_reducer(force)
     else:
         build_all(force)

@@ -56,3 +56,4 @@ signature("mi_attn_bwd", P, P, P, P, P, P, I, I, I, F, P)
 # gemm256.hip
 signature("mi_gemm256_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, I, P)
 signature("mi_set_gemm256", I)
+signature("mi_gemm256_tn", P, P, P, I, I, I, I, I, I, P)

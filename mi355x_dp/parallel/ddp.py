@@ -9,10 +9,14 @@ Design (MI355X-first):
     parameters are ready and every earlier bucket has been launched -- so all
     ranks issue collectives in the same order and the RCCL stream overlaps the
     rest of backward on the compute stream.
-  * bucket sizes are chosen for xGMI: a small first bucket (starts comm early),
-    then ``bucket_cap_mb`` (default 32 MB: at ~7 x 153 GB/s per GPU a 32 MB
-    ring all-reduce is ~0.1-0.4 ms, long enough to amortise launch latency,
-    short enough to keep the tail after the last backward kernel small).
+  * bucket sizes are chosen for xGMI by the native reducer's link-aware planner
+    (csrc/ddp/reducer.cpp): a small first bucket (starts comm early), a small LAST
+    bucket (its all-reduce is the exposed tail), and middle buckets sized from an
+    alpha-beta model of a ring all-reduce over 7 x 153 GB/s links so per-collective
+    latency stays <= ~10 % (``bucket_cap_mb`` / MI355X_DP_BUCKET_MB override it).
+  * bucket bookkeeping and in-order launch run in the C++ ``Reducer`` (the
+    counterpart of DDP's C++ Reducer); a pure-Python twin is
+    kept for builds without the extension (MI355X_DP_PY_REDUCER=1 forces it).
   * averaging (1/world) is folded into the fused optimizer kernel
     (``grad_scale``) instead of a separate scaling pass; ``average=True`` in
     ``finish_gradient_sync`` scales explicitly for foreign optimizers.
@@ -21,6 +25,7 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import functools
 import os
 from typing import List, Optional
 
@@ -30,8 +35,10 @@ import torch.nn as nn
 
 from .flat import FlatBuffers, FlatParams
 
-DEFAULT_BUCKET_MB = float(os.environ.get("MI355X_DP_BUCKET_MB", "32"))
+_ENV_BUCKET_MB = os.environ.get("MI355X_DP_BUCKET_MB")
+DEFAULT_BUCKET_MB = float(_ENV_BUCKET_MB) if _ENV_BUCKET_MB else None  # None: link-aware planner
 DEFAULT_FIRST_BUCKET_MB = float(os.environ.get("MI355X_DP_FIRST_BUCKET_MB", "2"))
+DEFAULT_LAST_BUCKET_MB = float(os.environ.get("MI355X_DP_LAST_BUCKET_MB", "4"))
 
 
 def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int) -> List[List[int]]:
@@ -60,9 +67,9 @@ class DataParallel(nn.Module):
         loss = F.cross_entropy(model(x), y); loss.backward(); opt.step(); opt.zero_grad()
     """
 
-    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = DEFAULT_BUCKET_MB,
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = DEFAULT_BUCKET_MB,
                  first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB, broadcast_buffers: bool = True,
-                 bf16_copy: bool = True):
+                 bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -78,8 +85,20 @@ class DataParallel(nn.Module):
         self.flat = FlatParams(params, bf16_copy=bf16_copy, kernel_layout_ids=kernel_ids)
         self.buffers = FlatBuffers(list(module.buffers()))
 
+        from . import _reducer_native
+        native = _reducer_native.load()
         sizes = [p.numel() * 4 for p in self.flat.params]
-        self.buckets = plan_buckets(sizes, int(bucket_cap_mb * 2**20), int(first_bucket_mb * 2**20))
+        if bucket_cap_mb is None:
+            cap = (native.link_aware_cap(self.world_size) if native is not None
+                   else int(32 * 2**20))
+        else:
+            cap = int(bucket_cap_mb * 2**20)
+        self.bucket_cap_bytes = cap
+        if native is not None:
+            self.buckets = [list(b) for b in native.plan_buckets(sizes, cap, int(first_bucket_mb * 2**20),
+                                                                 min(cap, int(last_bucket_mb * 2**20)))]
+        else:
+            self.buckets = plan_buckets(sizes, cap, int(first_bucket_mb * 2**20))
         self.bucket_of = {}
         for b, idxs in enumerate(self.buckets):
             for i in idxs:
@@ -95,11 +114,20 @@ class DataParallel(nn.Module):
         self._works = []
         self._next = 0
         self._param_ready = [False] * len(self.flat.params)
-        self.comm_calls = 0
+        self._py_comm_calls = 0
 
+        self.reducer = None
+        if native is not None:
+            pg = None
+            if self.distributed and self.world_size > 1:
+                pg = process_group if process_group is not None else dist.distributed_c10d._get_default_group()
+            self.reducer = native.Reducer(self.flat.grad, [int(o) for o in self.flat.offsets],
+                                          [p.numel() for p in self.flat.params], self.buckets, pg, 64)
         for i, p in enumerate(self.flat.params):
-            p._mi_on_grad_ready = self._make_ready_cb(i)
-            p.register_post_accumulate_grad_hook(self._make_hook(i))
+            cb = functools.partial(self.reducer.mark_ready, i) if self.reducer is not None \
+                else self._make_ready_cb(i)
+            p._mi_on_grad_ready = cb
+            p.register_post_accumulate_grad_hook(self._make_hook(i, cb))
 
         if self.distributed and self.world_size > 1:
             # one broadcast of the whole flat parameter buffer (+ buffers) from rank 0
@@ -109,18 +137,30 @@ class DataParallel(nn.Module):
             self.flat.refresh_bf16()
         self._reset()
 
+    @property
+    def comm_calls(self) -> int:
+        return self.reducer.comm_calls if self.reducer is not None else self._py_comm_calls
+
+    @property
+    def native_reducer(self) -> bool:
+        return self.reducer is not None
+
     # -------------------------------------------------------------- hooks
     def _make_ready_cb(self, i):
         def cb():
             self._mark_ready(i)
         return cb
 
-    def _make_hook(self, i):
+    @staticmethod
+    def _make_hook(i, cb):
         def hook(p):
-            self._mark_ready(i)
+            cb()
         return hook
 
     def _reset(self):
+        if self.reducer is not None:
+            self.reducer.reset()
+            return
         for b, idxs in enumerate(self.buckets):
             self._pending[b] = len(idxs)
             self._ready[b] = False
@@ -149,7 +189,7 @@ class DataParallel(nn.Module):
         lo, hi = self.bucket_ranges[b]
         w = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
         self._works.append(w)
-        self.comm_calls += 1
+        self._py_comm_calls += 1
 
     # ------------------------------------------------------------ public
     def forward(self, *args, **kwargs):
@@ -160,6 +200,11 @@ class DataParallel(nn.Module):
 
     def finish_gradient_sync(self, average: bool = False):
         """Launch any bucket not yet launched (unused params), then wait for all."""
+        if self.reducer is not None:
+            self.reducer.finish()
+            if average and self.world_size > 1:
+                self.flat.grad.mul_(1.0 / self.world_size)
+            return
         for b in range(len(self.buckets)):
             self._ready[b] = True
         self._launch_ready()

@@ -66,3 +66,17 @@ def test_gemm256_epilogues(epi):
     else:
         run(A, B, C, aux=aux, epi=3)
         assert rel_err(C, ref + aux.float()) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 3072, 50432 // 16), (2304, 768, 1000), (264, 136, 200), (512, 256, 64),
+                                   (3072, 768, 6304)])
+def test_gemm256_tn(M, N, K):
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    A = (torch.rand(K, M, device="cuda") * 2 - 1).to(BF)
+    B = (torch.rand(K, N, device="cuda") * 2 - 1).to(BF)
+    C = torch.randn(M, N, device="cuda")
+    ref = C + A.float().t() @ B.float()
+    _lib.call("mi_gemm256_tn", ptr(A), ptr(B), ptr(C), M, N, K, M, N, N, stream_of(A))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 1e-4

@@ -60,7 +60,7 @@ def _worker_engine_body(rank, world, port, q, backend):
         opt.zero_grad()
         torch.nn.functional.cross_entropy(m(x[shard]), y[shard]).backward()
         opt.step()
-    q.put((rank, m.flat.data.clone(), len(m.buckets), m.comm_calls))
+    q.put((rank, m.flat.data.clone().numpy(), len(m.buckets), m.comm_calls))  # by value: the child may exit first
     dist.destroy_process_group()
 
 
@@ -72,7 +72,8 @@ def test_engine_matches_single_process(backend):
     ps = [ctx.Process(target=_worker_engine, args=(r, 2, port, q, backend)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict((r, (d, nb, nc)) for r, d, nb, nc in [q.get(timeout=120) for _ in ps])
+    res = dict((r, (torch.from_numpy(d) if not isinstance(d, Exception) else d, nb, nc))
+               for r, d, nb, nc in [q.get(timeout=120) for _ in ps])
     for p in ps:
         p.join(60)
     for r, (d, _, _) in res.items():
@@ -146,3 +147,63 @@ def test_flat_params_layout_and_state_dict():
     assert w.is_contiguous(memory_format=torch.channels_last)
     assert w.data_ptr() >= e.flat.data.data_ptr()
     assert w.grad is not None and w.grad.data_ptr() >= e.flat.grad.data_ptr()
+
+
+def test_native_reducer_planner():
+    from mi355x_dp.parallel import _reducer_native
+    ext = _reducer_native.load()
+    if ext is None:
+        pytest.skip("native reducer not built")
+    sizes = [4] * 10 + [100] + [4] * 5
+    b = ext.plan_buckets(sizes, 16, 8, 12)
+    flat = [i for bb in b for i in bb]
+    assert flat == list(range(len(sizes)))            # contiguous, in order, complete
+    assert sum(sizes[i] for i in b[0]) <= 8            # small first bucket
+    assert sum(sizes[i] for i in b[-1]) <= 12          # small last (exposed-tail) bucket
+    # link-aware cap grows with world size (more rings over more links), clamped
+    caps = [ext.link_aware_cap(w) for w in (2, 4, 8)]
+    assert caps[0] <= caps[1] <= caps[2] <= 64 << 20 and caps[0] >= 4 << 20
+
+
+def _worker_reducer(rank, world, port, q, py):
+    try:
+        if py:
+            os.environ["MI355X_DP_PY_REDUCER"] = "1"
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01)
+        opt = FlatSGD(m, lr=0.05, momentum=0.9)
+        x, y = _data()
+        shard = slice(rank * 8, (rank + 1) * 8)
+        for _ in range(2):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x[shard]), y[shard]).backward()
+            opt.step()
+        q.put((rank, m.native_reducer, m.flat.data.clone().numpy(), m.comm_calls))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, -1))
+        raise
+
+
+def test_native_reducer_matches_python_reducer():
+    from mi355x_dp.parallel import _reducer_native
+    if _reducer_native.load() is None:
+        pytest.skip("native reducer not built")
+    out = {}
+    for py in (False, True):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _port()
+        ps = [ctx.Process(target=_worker_reducer, args=(r, 2, port, q, py)) for r in range(2)]
+        for p in ps:
+            p.start()
+        res = [q.get(timeout=120) for _ in ps]
+        for p in ps:
+            p.join(60)
+        for r, native, d, calls in res:
+            assert not isinstance(native, Exception), repr(native)
+            assert native is (not py)
+            assert calls > 2
+        out[py] = res[0][2]
+    assert (out[False] == out[True]).all()

@@ -11,7 +11,7 @@ import torch
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", default="nt", choices=["nt", "nt256", "tn", "blas"])
+    ap.add_argument("--op", default="nt", choices=["nt", "nt256", "tn", "tn256", "blas", "blas_tn"])
     ap.add_argument("--M", type=int, default=50432)
     ap.add_argument("--N", type=int, default=3072)
     ap.add_argument("--K", type=int, default=768)
@@ -36,6 +36,10 @@ def main():
             _lib.call("mi_gemm_nt", ptr(A), ptr(B), ptr(C), ptr(None), ptr(None), M, N, K, K, K, N, 0, 0, st)
         elif a.op == "nt256":
             _lib.call("mi_gemm256_nt", ptr(A), ptr(B), ptr(C), ptr(None), ptr(None), 0, M, N, K, K, K, N, 0, 0, st)
+        elif a.op == "tn256":
+            _lib.call("mi_gemm256_tn", ptr(dY), ptr(A), ptr(dW), N, K, M, N, K, K, st)
+        elif a.op == "blas_tn":
+            torch.matmul(dY.t(), A)
         elif a.op == "tn":
             _lib.call("mi_gemm_tn", ptr(dY), ptr(A), ptr(dW), N, K, M, N, K, K, st)
         else:
