@@ -40,11 +40,15 @@ def parse():
     p.add_argument("--backend", default=os.environ.get("MI355X_DP_BACKEND", "nccl"))
     p.add_argument("--bucket-mb", type=float, default=None)
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the step as one captured HIP graph (launch-bound small-batch configs)")
     return p.parse_args()
 
 
 def main():
     args = parse()
+    if args.graph and args.warmup < 2:
+        args.warmup = 2  # the graph is captured during warmup, never inside the timed region
     import torch
     import torch.distributed as dist
 
@@ -79,14 +83,28 @@ def main():
     images = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev, generator=g)
     labels = torch.randint(0, args.num_classes, (B,), dtype=torch.int64, device=dev, generator=g)
 
-    def step(i):
-        x = augment(images, 8, IMAGENET_MEAN, IMAGENET_STD, pad=0, flip=True, seed=i)  # 3 ch + 5 zero pad
+    pad = 4 if S <= 64 else 0  # CIFAR-style random crop for small images (reference transforms)
+    x_static = torch.empty((B, 8, S, S), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+
+    def core():
         engine.zero_grad()
-        out = engine(x)
+        out = engine(x_static)
         loss = cross_entropy(out, labels)
         loss.backward()
         opt.step()
         return loss
+
+    graphed = None
+
+    def step(i):
+        nonlocal graphed
+        augment(images, 8, IMAGENET_MEAN, IMAGENET_STD, pad=pad, flip=True, seed=i, out=x_static)  # 3 ch + 5 zero
+        if args.graph and i >= 1:  # capture after one eager step (optimizer first-step semantics)
+            if graphed is None:
+                from mi355x_dp.graphs import GraphedStep
+                graphed = GraphedStep(core, warmup=1)
+            return graphed()
+        return core()
 
     t_w0 = time.time()
     for i in range(args.warmup):
@@ -144,6 +162,7 @@ def main():
                 "optimizer": "SGD(momentum=0.9, wd=1e-4), fp32 master weights, bf16 compute",
                 "backend": args.backend if world > 1 else "none",
                 "buckets": len(engine.buckets),
+                "hip_graph": bool(args.graph),
             },
             "loss_first_warmup": round(first_loss, 4),
             "loss_last": round(last_loss, 4),

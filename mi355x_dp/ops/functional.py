@@ -498,21 +498,32 @@ def checksum(x: torch.Tensor) -> float:
 
 
 # ============================================================ input pipeline
-def augment(images_u8, out_channels, mean, std, pad=4, flip=True, seed=0):
+_AUG_CONST = {}
+
+
+def augment(images_u8, out_channels, mean, std, pad=4, flip=True, seed=0, out=None):
     """uint8 NHWC [N,H,W,C] -> bf16 channels_last [N,Cout,H,W]: random crop (zero padding
     ``pad``) + horizontal flip + normalize, all on the GPU (replaces the reference's per-sample
-    PIL transforms, cifar10-distributed-smddp-gpu.py:55-62)."""
+    PIL transforms, cifar10-distributed-smddp-gpu.py:55-62).  ``out``: write into a static
+    buffer (the input of a captured HIP-graph step)."""
     N, H, W, C = images_u8.shape
     dev = images_u8.device
-    mean_t = torch.zeros(max(out_channels, C), dtype=torch.float32, device=dev)
-    stdinv_t = torch.ones(max(out_channels, C), dtype=torch.float32, device=dev)
-    mean_t[:C] = torch.tensor(mean, dtype=torch.float32)
-    stdinv_t[:C] = 1.0 / torch.tensor(std, dtype=torch.float32)
+    key = (str(dev), max(out_channels, C), C, tuple(mean), tuple(std))
+    if key not in _AUG_CONST:  # device constants built once (no per-step host->device copies)
+        mean_t = torch.zeros(max(out_channels, C), dtype=torch.float32, device=dev)
+        stdinv_t = torch.ones(max(out_channels, C), dtype=torch.float32, device=dev)
+        mean_t[:C] = torch.tensor(mean, dtype=torch.float32)
+        stdinv_t[:C] = 1.0 / torch.tensor(std, dtype=torch.float32)
+        _AUG_CONST[key] = (mean_t, stdinv_t)
+    mean_t, stdinv_t = _AUG_CONST[key]
     if not images_u8.is_cuda:
         x = images_u8.float().div(255.0).permute(0, 3, 1, 2)
         x = (x - mean_t[:C].view(1, C, 1, 1)) * stdinv_t[:C].view(1, C, 1, 1)
         return x
-    out = torch.empty((N, out_channels, H, W), dtype=BF16, device=dev, memory_format=CL)
+    if out is None:
+        out = torch.empty((N, out_channels, H, W), dtype=BF16, device=dev, memory_format=CL)
+    elif not (out.shape == (N, out_channels, H, W) and out.dtype == BF16 and out.is_contiguous(memory_format=CL)):
+        raise ValueError("augment(out=...) needs a bf16 channels_last [N, Cout, H, W] tensor")
     _lib.call("mi_augment", ptr(images_u8.contiguous()), ptr(out), N, H, W, C, out_channels, int(pad), int(flip),
               seed & 0xFFFFFFFF, ptr(mean_t), ptr(stdinv_t), stream_of(images_u8))
     return out
