@@ -273,8 +273,12 @@ __global__ __launch_bounds__(NT) void add_bf16_kernel(const bf16_t* __restrict__
   }
 }
 
-// sum of squares / checksum of an fp32 buffer (replica-divergence detector)
-__global__ __launch_bounds__(NT) void checksum_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out) {
+// position-weighted checksum of an fp32 buffer (replica-divergence detector).  Deterministic:
+// block partials land in fixed slots and one block sums them in a fixed order, so identical
+// buffers give bit-identical checksums on every rank (an atomic reduction would not).
+constexpr int CK_BLOCKS = 1024;
+__global__ __launch_bounds__(NT) void checksum_partial_kernel(const float* __restrict__ x, int64_t n,
+                                                              double* __restrict__ part) {
   __shared__ double red[NT / 64];
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
@@ -283,7 +287,18 @@ __global__ __launch_bounds__(NT) void checksum_kernel(const float* __restrict__ 
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(NT) void checksum_final_kernel(const double* __restrict__ part, int nparts,
+                                                            double* __restrict__ out) {
+  __shared__ double red[NT / 64];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += NT) s += part[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
 }
 
 }  // namespace
@@ -368,7 +383,10 @@ MI_API int mi_add_bf16(const void* a, const void* b, void* o, int64_t n, hipStre
   return (int)hipGetLastError();
 }
 
+// out: >= 1 + 1024 doubles (out[0] = checksum, the rest block partials)
 MI_API int mi_checksum(const float* x, int64_t n, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(checksum_kernel, dim3(std::min<int64_t>(1024, (n + NT - 1) / NT)), dim3(NT), 0, st, x, n, out);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(CK_BLOCKS, (n + NT - 1) / NT));
+  hipLaunchKernelGGL(checksum_partial_kernel, dim3(nb), dim3(NT), 0, st, x, n, out + 1);
+  hipLaunchKernelGGL(checksum_final_kernel, dim3(1), dim3(NT), 0, st, out + 1, nb, out);
   return (int)hipGetLastError();
 }

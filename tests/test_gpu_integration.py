@@ -80,3 +80,39 @@ def test_reference_gpu_script_unmodified(tmp_path):
     assert sd["module.fc.weight"].shape == (1000, 512)
     assert all(v.is_contiguous() for v in sd.values())
     assert sum(v.numel() for k, v in sd.items() if "running" not in k and "num_batches" not in k) == 11689512
+
+
+def test_two_ranks_one_gpu_gloo(tmp_path):
+    """Multi-rank GPU engine path without a second GPU: 2 ranks share cuda:0 over gloo (CUDA
+    tensors), exercising DataParallel + native reducer bucket launches + FlatSGD on device;
+    replicas must stay bit-identical and match each other's losses."""
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, sys, torch, torch.distributed as dist\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "dist.init_process_group('gloo')\n"
+        "rank = dist.get_rank()\n"
+        "torch.cuda.set_device(0)\n"
+        "from mi355x_dp.models import get_model\n"
+        "from mi355x_dp.ops import augment, cross_entropy, checksum\n"
+        "from mi355x_dp.parallel import DataParallel, FlatSGD\n"
+        "torch.manual_seed(rank)  # different init per rank: the engine must broadcast rank 0's\n"
+        "eng = DataParallel(get_model('resnet18', num_classes=10).cuda(), bucket_cap_mb=8)\n"
+        "assert eng.native_reducer and len(eng.buckets) > 2\n"
+        "opt = FlatSGD(eng, lr=0.02, momentum=0.9)\n"
+        "g = torch.Generator(device='cuda').manual_seed(100 + rank)\n"
+        "u8 = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, device='cuda', generator=g)\n"
+        "y = torch.randint(0, 10, (16,), device='cuda', generator=g)\n"
+        "for i in range(3):\n"
+        "    x = augment(u8, 8, (0.5,0.5,0.5), (0.25,0.25,0.25), pad=4, seed=i)\n"
+        "    eng.zero_grad(); cross_entropy(eng(x), y).backward(); opt.step()\n"
+        "torch.cuda.synchronize()\n"
+        "c = torch.tensor([checksum(eng.flat.data)], dtype=torch.float64)\n"
+        "cs = [torch.zeros_like(c) for _ in range(2)]; dist.all_gather(cs, c)\n"
+        "assert cs[0].item() == cs[1].item(), cs\n"
+        "print('RANK_OK', rank, eng.comm_calls, flush=True)\n"
+        "dist.destroy_process_group()\n")
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2", str(script)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env={**os.environ, "PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("RANK_OK") == 2
