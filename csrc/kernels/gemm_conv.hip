@@ -73,7 +73,13 @@ struct NTArgs {
   int a_bytes, b_bytes;  // buffer-resource ranges (GLDS path): A / B extents in bytes
   bf16_t* aux;       // bf16 epilogue operand, same layout as C (see epi)
   int epi;           // bf16 epilogue op: 0 none, 1 GELU (aux <- pre-activation, C <- gelu),
-                     // 2 GELU backward (C <- acc * gelu'(aux)), 3 residual (C <- acc + aux)
+                     // 2 GELU backward (C <- acc * gelu'(aux)), 3 residual / accumulate (C <- acc + aux),
+                     // 4 BatchNorm backward of the layer that produced this conv's input:
+                     //   C <- dz = acc * [aux > 0] (relu mask on the BN output aux, if bn_relu),
+                     //   stats <- per-channel (sum dz, sum dz * (aux2 - mean)), aux2 = BN input
+  const bf16_t* aux2;
+  const float* mean;
+  int bn_relu;
   ConvGeom g;
 };
 
@@ -140,7 +146,17 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     fPQ = a.g.fPQc[cls]; fQ = a.g.fQc[cls];
     Mrows = (a.M / (a.g.P * a.g.Q)) * a.g.Pc[cls] * a.g.Qc[cls];
   }
-  if (m0 >= Mrows) return;
+  if (m0 >= Mrows) {
+    // empty tile of a parity class: its statistics rows still have to be defined
+    if (a.stats) {
+      const int prow = blockIdx.y * a.tiles_m + tm;
+      for (int c = threadIdx.x; c < 2 * BN; c += 256) {
+        const int which = c / BN, col = c - which * BN;
+        if (n0 + col < a.N) a.stats[((size_t)prow * 2 + which) * a.N + n0 + col] = 0.f;
+      }
+    }
+    return;
+  }
 
   // glds writes lane-linear pieces (LDS row rbase+32i, physical chunk chk): the XOR swizzle is on
   // the SOURCE, this lane fetches logical chunk lc of its rows (row & 7 == rbase & 7 for all i).
@@ -354,14 +370,34 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     if (n < a.N) {
       const size_t off = row_off(m) + n;
       uint4 o = v;
-      if (a.epi) o = epilogue_op(a.epi, v, a.aux + off);
-      *(uint4*)((bf16_t*)a.C + off) = o;
-    }
-    if (a.stats) {
-      float f[8];
-      unpack8(v, f);
+      if (a.epi == 4) {
+        // BN backward: dz = dy * relu mask; stats (sum dz, sum dz * (x - mean)) of the rounded dz
+        float f[8], xv[8], mu[8];
+        unpack8(v, f);
+        if (a.bn_relu) {
+          float yv[8];
+          unpack8(*(const uint4*)(a.aux + off), yv);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
+          for (int q = 0; q < 8; ++q) f[q] = yv[q] > 0.f ? f[q] : 0.f;
+        }
+        o = pack8(f);
+        if (a.stats) {
+          unpack8(*(const uint4*)(a.aux2 + off), xv);
+          *(float4*)&mu[0] = *(const float4*)(a.mean + n);
+          *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * (xv[q] - mu[q]); }
+        }
+      } else {
+        if (a.epi) o = epilogue_op(a.epi, v, a.aux + off);
+        if (a.stats) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
+        }
+      }
+      *(uint4*)((bf16_t*)a.C + off) = o;
     }
   }
   if (a.stats) {
@@ -728,6 +764,48 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
   a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);
   if (stride == 2) {
     // parity-class decomposition: class (ph, pw) rows only visit taps r = ph+pad (mod 2)
+    a.mode = 3;
+    for (int c = 0; c < 4; ++c) {
+      const int ph = c / 2, pw = c % 2;
+      a.g.Pc[c] = (H - ph + 1) / 2;
+      a.g.Qc[c] = (W - pw + 1) / 2;
+      a.g.fPQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Pc[c] * a.g.Qc[c]));
+      a.g.fQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Qc[c]));
+    }
+  }
+  return (int)dispatch_nt(a, st);
+}
+
+// Statistics-slab rows written by mi_conv2d_dgrad_ex with stats (all parity classes).
+MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride) {
+  const int M = Nb * H * W;
+  const int bm = nt_choice(M, C) == 2 ? 64 : 128;
+  if (stride == 1) return cdiv(M, bm);
+  int mrows = 0;
+  for (int c = 0; c < 4; ++c) mrows = std::max(mrows, Nb * ((H - c / 2 + 1) / 2) * ((W - c % 2 + 1) / 2));
+  return 4 * cdiv(mrows, bm);
+}
+
+// Conv dgrad with a fused epilogue: epi 3 accumulates into aux (dx = dgrad + aux; aux may alias
+// dx -- the residual-gradient sum of a block input), epi 4 emits dz of the BatchNorm that produced
+// this conv's input (aux = BN output y for the relu mask, aux2 = BN input, mean = its batch
+// mean) plus its backward statistics into `stats` ([mi_dgrad_stat_rows][2][C]).
+MI_API int mi_conv2d_dgrad_ex(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                              int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                              const float* mean, int bn_relu, float* stats, hipStream_t st) {
+  if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4) || (epi && !aux && bn_relu) ||
+      (epi == 3 && !aux) || (epi == 4 && stats && (!aux2 || !mean)))
+    return (int)hipErrorInvalidValue;
+  NTArgs a{};
+  a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
+  a.M = Nb * H * W; a.N = C; a.K = R * S * K;
+  a.lda = 0; a.ldb = a.K; a.ldc = C; a.mode = 2; a.out_f32 = 0; a.accumulate = 0;
+  a.epi = epi; a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu;
+  a.stats = (epi == 4) ? stats : nullptr;
+  a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
+  a.b_bytes = rsrc_bytes((int64_t)C * a.K);
+  a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);
+  if (stride == 2) {
     a.mode = 3;
     for (int c = 0; c < 4; ++c) {
       const int ph = c / 2, pw = c % 2;

@@ -382,6 +382,23 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
   return (int)hipGetLastError();
 }
 
+// BN training backward from statistics a conv dgrad epilogue already produced (epi 4):
+// dz (relu already applied), part[pre_rows][2][C] = per-tile (sum dz, sum dz * (x - mean)).
+// Skips the statistics pass; dres (optional) <- dz (the residual branch's gradient).
+MI_API int mi_bn_bwd_train_pre(const void* dz, const void* x, void* dx, void* dres, int M, int C, const float* gamma,
+                               const float* save_mean, const float* save_invstd, float* dgamma, float* dbeta,
+                               float* coef, float* part, int pre_rows, hipStream_t st) {
+  if (C % 8 != 0 || pre_rows <= 0) return (int)hipErrorInvalidValue;
+  const float* fin = part;
+  const int nblk = tall_slab_split(part, pre_rows, C, st, fin);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
+                     save_mean, save_invstd, dgamma, dbeta, coef);
+  int64_t nvec = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dz, (const bf16_t*)nullptr,
+                     (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, 0);
+  return (int)hipGetLastError();
+}
+
 MI_API int mi_bn_bwd_eval(const void* dy, const void* y, const float* scale, void* dx, void* dres, int M, int C,
                           int relu, hipStream_t st) {
   int64_t nvec = (int64_t)M * C / 8;

@@ -16,7 +16,13 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+import os
+
+from mi355x_dp.ops import resblock as _rb
 from .layers import BatchNorm2d, Conv2d, GlobalAvgPool2d, Linear, MaxPool2d, ReLU, conv_bn, to_device_input
+
+# one fused autograd node per residual block on the native training path (MI355X_DP_FUSED_BLOCKS=0: per-op)
+FUSED_BLOCKS = os.environ.get("MI355X_DP_FUSED_BLOCKS", "1") != "0"
 
 
 def conv3x3(in_planes, out_planes, stride=1):
@@ -41,6 +47,8 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        if FUSED_BLOCKS and _rb.fusable(self, x):
+            return _rb.res_block(self, x)
         identity = x
         out = conv_bn(self.conv1, self.bn1, x, relu=True)
         if self.downsample is not None:
@@ -65,6 +73,8 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        if FUSED_BLOCKS and _rb.fusable(self, x):
+            return _rb.res_block(self, x)
         identity = x
         out = conv_bn(self.conv1, self.bn1, x, relu=True)
         out = conv_bn(self.conv2, self.bn2, out, relu=True)

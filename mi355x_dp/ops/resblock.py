@@ -1,0 +1,261 @@
+"""ResNet residual blocks (torchvision BasicBlock / Bottleneck) as ONE autograd node each.
+
+Per-op autograd (conv -> BN -> ...) leaves two kinds of memory traffic on the table in the
+backward pass, which at ResNet-50 / batch 256 is bandwidth-bound outside the convolutions:
+
+* the gradient of a block input is a SUM (conv1's data gradient + the residual path); autograd
+  materialises both and adds them with a separate elementwise kernel;
+* every BatchNorm backward re-reads dy, y and x once for its statistics pass and once more for
+  its apply pass.
+
+With the block as one node the backward is scheduled explicitly:
+
+  bn3 backward (relu mask + residual): dres is written straight into the block's dx buffer
+  (identity shortcut) or the downsample BN's gradient;
+  conv3 dgrad with epilogue 4: emits dz2 = dgrad * [y2 > 0] AND bn2's backward statistics
+  (sum dz2, sum dz2 * (c2 - mean2)) from the same registers -> bn2 needs no statistics pass
+  and its apply pass reads dz2, c2 only (no y2);
+  conv2 dgrad with epilogue 4 for bn1 likewise;
+  conv1 (and downsample) dgrad with epilogue 3: accumulate into dx in place -- no add kernel.
+
+Forward is the same kernel sequence as the per-op path (conv epilogue emits the BN forward
+statistics, BN apply fuses residual + ReLU).  Weight gradients go into the flat fp32 gradient
+buffer of the DP engine.  Reference: torchvision BasicBlock / Bottleneck semantics, reached by
+the reference through ``torchvision.models.resnet18`` (cifar10-distributed-smddp-gpu.py:30-32).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import kernels as _k  # noqa: F401
+from ._lib import ptr, stream_of
+from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, weight_bf16
+
+F32 = torch.float32
+EPI_ACCUM, EPI_BN_BWD = 3, 4
+
+
+def _out_hw(h, r, stride, pad):
+    return (h + 2 * pad - r) // stride + 1
+
+
+class _ConvSpec:
+    __slots__ = ("w", "stride", "pad")
+
+    def __init__(self, conv):
+        self.w = conv.weight
+        self.stride = int(conv.stride[0])
+        self.pad = int(conv.padding[0])
+
+
+class _BNSpec:
+    __slots__ = ("w", "b", "rm", "rv", "nbt", "momentum", "eps")
+
+    def __init__(self, bn):
+        self.w, self.b = bn.weight, bn.bias
+        self.rm, self.rv, self.nbt = bn.running_mean, bn.running_var, bn.num_batches_tracked
+        self.momentum = float(bn.momentum)
+        self.eps = float(bn.eps)
+
+
+# ----------------------------------------------------------------------- forward pieces
+def _conv_fwd_stats(x, spec):
+    N, C, H, W = x.shape
+    w16 = weight_bf16(spec.w)
+    K, _, R, S = spec.w.shape
+    P, Q = _out_hw(H, R, spec.stride, spec.pad), _out_hw(W, S, spec.stride, spec.pad)
+    lib = _lib.load()
+    rows = lib.mi_nt_stat_rows(N * P * Q, K)
+    slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=x.device)
+    y = torch.empty((N, K, P, Q), dtype=BF16, device=x.device, memory_format=CL)
+    _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), ptr(slab), N, H, W, C, K, R, S, spec.stride,
+              spec.pad, P, Q, 0, stream_of(x))
+    return y, slab, rows
+
+
+def _bn_fwd(c, slab, rows, bn, relu, res=None):
+    N, C, H, W = c.shape
+    dev = c.device
+    y = torch.empty_like(c, memory_format=CL)
+    mean = torch.empty(C, dtype=F32, device=dev)
+    invstd = torch.empty(C, dtype=F32, device=dev)
+    scale = torch.empty(C, dtype=F32, device=dev)
+    shift = torch.empty(C, dtype=F32, device=dev)
+    _lib.call("mi_bn_fwd_train", ptr(c), ptr(res), ptr(y), N * H * W, C, bn.eps, bn.momentum, ptr(bn.w), ptr(bn.b),
+              ptr(bn.rm), ptr(bn.rv), ptr(bn.nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(slab),
+              int(rows), int(relu), stream_of(c))
+    return y, mean, invstd
+
+
+# ---------------------------------------------------------------------- backward pieces
+def _wgrad(x, dy, spec):
+    N, C, H, W = x.shape
+    K, _, R, S = spec.w.shape
+    P, Q = dy.shape[2], dy.shape[3]
+    g = _grad_buffer(spec.w)
+    _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dy), ptr(g), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
+              stream_of(dy))
+    return _finish_grad(spec.w, g)
+
+
+def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0, stats=None):
+    N, C, H, W = x_shape
+    K, _, R, S = spec.w.shape
+    P, Q = dy.shape[2], dy.shape[3]
+    w16 = weight_bf16(spec.w)
+    wt = torch.empty((C, R, S, K), dtype=BF16, device=dy.device)
+    st = stream_of(dy)
+    _lib.call("mi_conv_wtrans", ptr(w16), ptr(wt), K, R * S, C, st)
+    _lib.call("mi_conv2d_dgrad_ex", ptr(dy), ptr(wt), ptr(out), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
+              int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), st)
+    return out
+
+
+def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev):
+    """conv dgrad fused with the relu mask + backward statistics of the BN that produced the conv's
+    input: returns (dz, slab, rows)."""
+    N, C, H, W = y_prev.shape
+    lib = _lib.load()
+    rows = lib.mi_dgrad_stat_rows(N, H, W, C, dy.shape[2], dy.shape[3], spec.stride)
+    slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dy.device)
+    dz = torch.empty_like(y_prev, memory_format=CL)
+    _dgrad(dy, spec, y_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab)
+    return dz, slab, rows
+
+
+def _bn_bwd(dy, y, c, bn, mean, invstd, relu, dres=None):
+    """full BN backward (statistics pass included) -> dc, (dgamma, dbeta) for autograd."""
+    N, C, H, W = c.shape
+    M = N * H * W
+    dev = c.device
+    dc = torch.empty_like(c, memory_format=CL)
+    gw, gb = _grad_buffer(bn.w), _grad_buffer(bn.b)
+    lib = _lib.load()
+    part = torch.empty((lib.mi_bn_partial_rows(M, C) + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dev)
+    coef = torch.empty((3, C), dtype=F32, device=dev)
+    _lib.call("mi_bn_bwd_train", ptr(dy), ptr(y), ptr(c), ptr(dc), ptr(dres), M, C, ptr(bn.w), ptr(mean),
+              ptr(invstd), ptr(gw), ptr(gb), ptr(coef), ptr(part), int(relu), stream_of(c))
+    return dc, _finish_grad(bn.w, gw), _finish_grad(bn.b, gb)
+
+
+def _bn_bwd_pre(dz, c, bn, mean, invstd, slab, rows):
+    """BN backward from dgrad-epilogue statistics (dz already relu-masked)."""
+    N, C, H, W = c.shape
+    dc = torch.empty_like(c, memory_format=CL)
+    gw, gb = _grad_buffer(bn.w), _grad_buffer(bn.b)
+    coef = torch.empty((3, C), dtype=F32, device=c.device)
+    _lib.call("mi_bn_bwd_train_pre", ptr(dz), ptr(c), ptr(dc), ptr(None), N * H * W, C, ptr(bn.w), ptr(mean),
+              ptr(invstd), ptr(gw), ptr(gb), ptr(coef), ptr(slab), int(rows), stream_of(c))
+    return dc, _finish_grad(bn.w, gw), _finish_grad(bn.b, gb)
+
+
+# -------------------------------------------------------------------------- the block
+class _ResBlock(torch.autograd.Function):
+    """inputs: x, *params (in ``_param_list`` order).  ``specs`` = (convs, bns, has_ds) where the
+    main-path convs/bns are [conv1, conv2(, conv3)] / [bn1, bn2(, bn3)] and the downsample pair,
+    if any, is appended last."""
+
+    @staticmethod
+    def forward(ctx, x, specs, *params):
+        ctx.params_order = params
+        convs, bns, has_ds = specs
+        n_main = len(convs) - (1 if has_ds else 0)
+        x = _nhwc(x)
+        saved_c, saved_y, saved_m, saved_i = [], [], [], []
+        h = x
+        for i in range(n_main):
+            c, slab, rows = _conv_fwd_stats(h, convs[i])
+            last = i == n_main - 1
+            if last:
+                if has_ds:
+                    cd, slabd, rowsd = _conv_fwd_stats(x, convs[-1])
+                    yd, md, isd = _bn_fwd(cd, slabd, rowsd, bns[-1], relu=False)
+                    res = yd
+                else:
+                    res = x
+                y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True, res=res)
+            else:
+                y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True)
+            saved_c.append(c); saved_y.append(y); saved_m.append(m); saved_i.append(inv)
+            h = y
+        tensors = [x] + saved_c + saved_y + saved_m + saved_i
+        if has_ds:
+            tensors += [cd, md, isd]
+        ctx.save_for_backward(*tensors)
+        ctx.specs = specs
+        ctx.n_main = n_main
+        return h
+
+    @staticmethod
+    def backward(ctx, dout):
+        convs, bns, has_ds = ctx.specs
+        n = ctx.n_main
+        t = ctx.saved_tensors
+        x = t[0]
+        cs, ys, ms, invs = t[1:1 + n], t[1 + n:1 + 2 * n], t[1 + 2 * n:1 + 3 * n], t[1 + 3 * n:1 + 4 * n]
+        if has_ds:
+            cd, md, isd = t[1 + 4 * n:]
+        dout = _nhwc(dout)
+        grads = {}
+        dx = torch.empty_like(x, memory_format=CL)
+        # last BN: relu + residual; dres -> dx (identity) or the downsample BN's output gradient
+        dyd = torch.empty_like(ys[-1], memory_format=CL) if has_ds else None
+        dc, gw, gb = _bn_bwd(dout, ys[-1], cs[-1], bns[n - 1], ms[-1], invs[-1], relu=1,
+                             dres=dyd if has_ds else dx)
+        grads[id(bns[n - 1].w)], grads[id(bns[n - 1].b)] = gw, gb
+        for i in range(n - 1, 0, -1):
+            inp = ys[i - 1]
+            grads[id(convs[i].w)] = _wgrad(inp, dc, convs[i])
+            dz, slab, rows = _dgrad_bn(dc, convs[i], inp, cs[i - 1], ms[i - 1])
+            dc, gw, gb = _bn_bwd_pre(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
+            grads[id(bns[i - 1].w)], grads[id(bns[i - 1].b)] = gw, gb
+        grads[id(convs[0].w)] = _wgrad(x, dc, convs[0])
+        if has_ds:
+            dcd, gw, gb = _bn_bwd(dyd, dyd, cd, bns[-1], md, isd, relu=0)
+            grads[id(bns[-1].w)], grads[id(bns[-1].b)] = gw, gb
+            grads[id(convs[-1].w)] = _wgrad(x, dcd, convs[-1])
+            _dgrad(dcd, convs[-1], x.shape, dx)                            # dx = dgrad_ds
+        _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx)                   # dx += dgrad_1
+        out = [dx, None]
+        for p in ctx.params_order:
+            out.append(grads.get(id(p)))
+        return tuple(out)
+
+
+def _specs(block):
+    convs = [block.conv1, block.conv2] + ([block.conv3] if hasattr(block, "conv3") else [])
+    bns = [block.bn1, block.bn2] + ([block.bn3] if hasattr(block, "bn3") else [])
+    has_ds = block.downsample is not None
+    if has_ds:
+        convs.append(block.downsample[0])
+        bns.append(block.downsample[1])
+    return convs, bns, has_ds
+
+
+def fusable(block, x) -> bool:
+    """The fused node covers the native training path: CUDA, grad enabled, BN in training mode
+    with running statistics and a fixed momentum, every conv a native MFMA conv (C % 64 == 0)."""
+    from mi355x_dp.models.layers import BatchNorm2d, Conv2d
+    if not (x.is_cuda and torch.is_grad_enabled() and block.training):
+        return False
+    convs, bns, _ = _specs(block)
+    for c in convs:
+        if not isinstance(c, Conv2d) or c.bias is not None or c.groups != 1 or c.in_channels % 64 != 0 \
+                or c.out_channels % 64 != 0 or c.stride[0] > 2 or c.dilation[0] != 1 or c.stride[0] != c.stride[1]:
+            return False
+    for b in bns:
+        if not isinstance(b, BatchNorm2d) or not b.track_running_stats or not b.affine or b.momentum is None:
+            return False
+    return True
+
+
+def res_block(block, x):
+    """Run a BasicBlock / Bottleneck as one fused autograd node (caller checked ``fusable``)."""
+    convs, bns, has_ds = _specs(block)
+    cspecs = tuple(_ConvSpec(c) for c in convs)
+    bspecs = tuple(_BNSpec(b) for b in bns)
+    params = [c.w for c in cspecs]
+    for b in bspecs:
+        params += [b.w, b.b]
+    return _ResBlock.apply(x, (cspecs, bspecs, has_ds), *params)

@@ -1,0 +1,129 @@
+"""Fused residual blocks (mi355x_dp.ops.resblock: one autograd node per block, BN-backward
+statistics in the dgrad epilogue, in-place residual-gradient accumulation) against the per-op
+native path on the same weights / inputs."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6))
+
+
+def _run(name, fused, x, y, seed=0):
+    import mi355x_dp.models.resnet as R
+    from mi355x_dp.models import get_model
+    from mi355x_dp.ops import cross_entropy
+    old = R.FUSED_BLOCKS
+    R.FUSED_BLOCKS = fused
+    try:
+        torch.manual_seed(seed)
+        m = get_model(name, num_classes=10).cuda()
+        with torch.no_grad():  # non-trivial BN affine parameters
+            for mod in m.modules():
+                if isinstance(mod, torch.nn.BatchNorm2d):
+                    mod.weight.uniform_(0.5, 1.5)
+                    mod.bias.uniform_(-0.2, 0.2)
+        # (the stem weight gradient depends on every block's input gradient, so the dx chain
+        # through all blocks is covered without an input gradient)
+        loss = cross_entropy(m(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads = {n: p.grad.detach().float().clone() for n, p in m.named_parameters()}
+        bufs = {n: b.detach().float().clone() for n, b in m.named_buffers()}
+        return float(loss), grads, bufs
+    finally:
+        R.FUSED_BLOCKS = old
+
+
+def _fp32_ref(name, x, y):
+    """stock-PyTorch fp32 model (same architecture / names) with the same initial weights"""
+    from mi355x_dp.models import get_model
+    from mi355x_dp.models.stock import stock_resnet
+    torch.manual_seed(0)
+    m = get_model(name, num_classes=10)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.2, 0.2)
+    ref = stock_resnet(name, num_classes=10)
+    ref.load_state_dict(m.state_dict())
+    ref = ref.cuda().float()
+    loss = torch.nn.functional.cross_entropy(ref(x), y)
+    loss.backward()
+    return float(loss), {n: p.grad.detach().float() for n, p in ref.named_parameters()}
+
+
+@pytest.mark.parametrize("name,size", [("resnet18", 32), ("resnet50", 64), ("resnet34", 40)])
+def test_fused_blocks_match_per_op(name, size):
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(8, 3, size, size, device="cuda", generator=g)
+    y = torch.randint(0, 10, (8,), device="cuda", generator=g)
+    l0, g0, b0 = _run(name, False, x, y)
+    l1, g1, b1 = _run(name, True, x, y)
+    lr, gr = _fp32_ref(name, x, y)
+    assert l1 == pytest.approx(l0, rel=1e-3)
+    for n in b0:
+        assert rel_err(b1[n], b0[n]) < 1e-3, n
+    worst = []
+    for n in g0:
+        e_per_op, e_fused = rel_err(g0[n], gr[n]), rel_err(g1[n], gr[n])
+        worst.append((e_fused - e_per_op, n, e_fused, e_per_op))
+        # fused must be as accurate as the per-op bf16 path (vs fp32), up to rounding noise
+        assert e_fused <= 1.25 * e_per_op + 0.01, (n, e_fused, e_per_op)
+    print(sorted(worst)[-3:])
+
+
+def test_fused_block_used_in_training():
+    import mi355x_dp.models.resnet as R
+    from mi355x_dp.models import get_model
+    from mi355x_dp.ops import resblock
+    m = get_model("resnet50").cuda()
+    x = torch.randn(2, 3, 64, 64, device="cuda")
+    assert R.FUSED_BLOCKS and resblock.fusable(m.layer1[0], torch.empty(1, device="cuda"))
+    out = m.layer1[0](m.maxpool(R.conv_bn(m.conv1, m.bn1, R.to_device_input(x), relu=True)))
+    assert type(out.grad_fn).__name__.startswith("_ResBlock")
+
+
+@pytest.mark.parametrize("inpl,planes,stride,ds,size", [(256, 64, 1, False, 28), (256, 128, 2, True, 28),
+                                                        (64, 64, 1, True, 16), (512, 256, 2, True, 14)])
+def test_single_bottleneck_fused_vs_per_op(inpl, planes, stride, ds, size):
+    """one block in isolation (well conditioned): input gradient, parameter gradients and BN
+    running statistics of the fused node match the per-op native path to bf16 rounding"""
+    import mi355x_dp.models.resnet as R
+    from mi355x_dp.models.layers import BatchNorm2d
+    res = {}
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x0 = torch.randn(16, inpl, size, size, device="cuda", generator=g).to(torch.bfloat16)
+    x0 = x0.contiguous(memory_format=torch.channels_last)
+    dout = torch.randn(16, planes * 4, size // stride, size // stride, device="cuda", generator=g)
+    for fused in (False, True):
+        torch.manual_seed(3)
+        down = torch.nn.Sequential(R.conv1x1(inpl, planes * 4, stride), BatchNorm2d(planes * 4)) if ds else None
+        blk = R.Bottleneck(inpl, planes, stride, down).cuda()
+        with torch.no_grad():
+            for mod in blk.modules():
+                if isinstance(mod, torch.nn.BatchNorm2d):
+                    mod.weight.uniform_(0.5, 1.5)
+                    mod.bias.uniform_(-0.2, 0.2)
+        old = R.FUSED_BLOCKS
+        R.FUSED_BLOCKS = fused
+        try:
+            x = x0.clone().requires_grad_()
+            out = blk(x)
+            assert (type(out.grad_fn).__name__ == "_ResBlockBackward") == fused
+            out.backward(dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        finally:
+            R.FUSED_BLOCKS = old
+        torch.cuda.synchronize()
+        res[fused] = (out.float(), x.grad.float(), {n: p.grad.float() for n, p in blk.named_parameters()},
+                      {n: b.float() for n, b in blk.named_buffers()})
+    (o0, dx0, g0, b0), (o1, dx1, g1, b1) = res[False], res[True]
+    assert rel_err(o1, o0) < 1e-2
+    assert rel_err(dx1, dx0) < 2e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 2e-2, n
+    for n in b0:
+        assert rel_err(b1[n], b0[n]) < 1e-4, n
