@@ -62,3 +62,27 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 }
 
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// fast unsigned division by a runtime constant (host-built magic numbers)
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) { f.mul = 0; f.shift = 0; return f; }
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  f.mul = (uint32_t)m;
+  f.shift = s;
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  if (f.d == 1) return x;
+  uint32_t t = __umulhi(x, f.mul);
+  return (t + ((x - t) >> 1)) >> (f.shift - 1);
+}
+

@@ -42,11 +42,20 @@ struct G256Args {
   void* C;
   const float* bias;
   bf16_t* aux;
-  int epi;
+  int epi;              // bf16 epilogue op (epilogue.h), 4 = BN backward (see gemm_conv.hip NTArgs)
   int M, N, K, lda, ldb, ldc;
   int out_f32, accumulate;
   int tiles_m, tiles_n;
   int a_bytes, b_bytes;
+  // conv modes (1 = forward, gathers x; 2 = stride-1 data gradient, gathers dy): A rows are the
+  // output pixels (img, p, q) of a P x Q grid, k = (tap r, tap s, channel) of a gathered NHWC
+  // tensor [.., H, W, Cs] with Cs % 64 == 0 (one k-tile = one tap x 64 channels)
+  int H, W, Cs, S, stride, pad;
+  FastDiv fPQ, fQ, fS, fCpt;
+  float* stats;         // per-channel partial statistics, one slab row per (256-row tile, wave row)
+  const bf16_t* aux2;   // epi 4: BN input x
+  const float* mean;    // epi 4: BN batch mean
+  int bn_relu;
 };
 
 __device__ __forceinline__ void vm_wait6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
@@ -56,6 +65,7 @@ __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0
 // above the barrier that publishes their part (the builtin s_barrier is not a memory op)
 __device__ __forceinline__ void phase_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+template <int MODE>
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   __shared__ __attribute__((aligned(16))) uint4 smem[2 * 4 * PART_U4];  // 128 KB
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -76,12 +86,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
 
   // per-thread load geometry, fixed across k-tiles: 2 chunks per part, LDS rows p = (i*512+tid)/8.
-  // Byte offset at k-tile t = base + 128 t while t < klim (row in range and chunk inside K),
-  // else the out-of-range offset (zero fill) -- one compare / add / select per load in the loop.
-  // Rows past M / N need no test: their offsets lie beyond the buffer resource's range (the
-  // range is exactly the operand), which zero-fills.
+  // plain: byte offset at k-tile t = base + 128 t while t < klim (chunk inside K), else the
+  // out-of-range offset (zero fill).  Rows past M / N need no test: their offsets lie beyond the
+  // buffer resource's range (the range is exactly the operand), which zero-fills.
+  // conv: A row = output pixel; per k-tile the tap (r, s) and channel block are wave-uniform,
+  // the row's gathered pixel (hb + r, wb + s) is range-checked (zero padding = zero fill).
   uint32_t a_vo[2][2], b_vo[2][2];
   int klim[2];
+  int a_hw[2][2];  // conv: gathered-pixel origin (hb << 16 | wb & 0xffff), row validity in bit 15 of wb
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int idx = i * 512 + tid, p = idx >> 3, c = idx & 7;
@@ -89,8 +101,23 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     klim[i] = gk < a.K ? (a.K - gk + G_BK - 1) / G_BK : 0;
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
-      a_vo[part][i] = (uint32_t)((m0 + (p >> 6) * 128 + part * 64 + (p & 63)) * a.lda + gk) * 2u;
+      const int m = m0 + (p >> 6) * 128 + part * 64 + (p & 63);
       b_vo[part][i] = (uint32_t)((n0 + (p >> 5) * 64 + part * 32 + (p & 31)) * a.ldb + gk) * 2u;
+      if constexpr (MODE == 0) {
+        a_vo[part][i] = (uint32_t)(m * a.lda + gk) * 2u;
+        a_hw[part][i] = 0;
+      } else {
+        const uint32_t mm = m < a.M ? (uint32_t)m : 0u;
+        const uint32_t img = fdiv(mm, a.fPQ);
+        const uint32_t rem = mm - img * a.fPQ.d;
+        const uint32_t pp = fdiv(rem, a.fQ);
+        const uint32_t qq = rem - pp * a.fQ.d;
+        const int hb = MODE == 1 ? (int)pp * a.stride - a.pad : (int)pp + a.pad;
+        const int wb = MODE == 1 ? (int)qq * a.stride - a.pad : (int)qq + a.pad;
+        // element offset of the gathered pixel (hb, wb) channel gk (may be negative: padding)
+        a_vo[part][i] = (uint32_t)((((int)img * a.H + hb) * a.W + wb) * a.Cs + gk);
+        a_hw[part][i] = m < a.M ? (hb << 16) | (wb & 0xffff) : (int)0x80008000;  // invalid row: h = -32768
+      }
     }
   }
 
@@ -98,11 +125,30 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   auto issue = [&](int t, int which, int part) {
     uint4* dst = smem + ((t & 1) * 4 + which * 2 + part) * PART_U4;
     const uint32_t kb = (uint32_t)t * (G_BK * 2);
+    if (which == 1 || MODE == 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t vo = t < klim[i] ? (which == 0 ? a_vo[part][i] : b_vo[part][i]) + kb : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(which == 0 ? rsA : rsB, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo,
-                                               0, 0, 0);
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t vo = t < klim[i] ? (which == 0 ? a_vo[part][i] : b_vo[part][i]) + kb : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(which == 0 ? rsA : rsB, LDS_PTR(void, dst + i * 512 + wid * 64),
+                                                 16, vo, 0, 0, 0);
+      }
+    } else {
+      // wave-uniform tap / channel block of k-tile t
+      const int tt = t < nk ? t : 0;
+      const int tap = (int)fdiv((uint32_t)tt, a.fCpt);
+      const int c0 = (tt - tap * (int)a.fCpt.d) * 64;
+      const int r = (int)fdiv((uint32_t)tap, a.fS);
+      const int sx = tap - r * a.S;
+      const int dh = MODE == 1 ? r : -r, dw = MODE == 1 ? sx : -sx;
+      const int toff = (dh * a.W + dw) * a.Cs + c0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int hw = a_hw[part][i];
+        const int h = (hw >> 16) + dh, w = ((int)(short)(hw & 0xffff)) + dw;
+        const bool ok = t < nk && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const uint32_t vo = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0, 0);
+      }
     }
   };
 
@@ -132,7 +178,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
       for (int kk = 0; kk < 2; ++kk)
         f[j][kk] = __builtin_bit_cast(bf16x8, src[(wn * 32 + j * 16 + fr) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
   };
-  auto mma = [&](const bf16x8 (&af)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
+  auto mma = [&](const bf16x8 (&af_)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -140,7 +186,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af_[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
   };
 
   // One k-tile = 4 quadrant phases:
@@ -208,7 +254,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     }
     return;
   }
-  // bf16: each wave stages 64 rows x 64 cols at a time in its own LDS slice, then 16-B row stores
+  // bf16: each wave stages 64 rows x 64 cols at a time in its own LDS slice, then 16-B row stores.
+  // Optional per-channel statistics: the wave's 128 rows x 64 columns go to slab row tm*2 + wm.
   constexpr int CST = 72;  // padded row stride (elements)
   bf16_t* Ct = (bf16_t*)smem + wid * 64 * CST;
   float bv[4][4];
@@ -217,6 +264,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     const int n = n0 + wn * 64 + j * 16 + 4 * fq;
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[j][r] = (a.bias && n + r < a.N) ? a.bias[n + r] : 0.f;
+  }
+  const int cc = lane & 7;
+  const int n = n0 + wn * 64 + cc * 8;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8];
+  if (a.epi == 4 && a.stats && n < a.N) {
+    *(float4*)&mu[0] = *(const float4*)(a.mean + n);
+    *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
   }
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq) {
@@ -229,8 +284,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
             make_uint2(pack2bf(v[0] + bv[j][0], v[1] + bv[j][1]), pack2bf(v[2] + bv[j][2], v[3] + bv[j][3]));
       }
     lgkm_wait0();
-    const int cc = lane & 7;
-    const int n = n0 + wn * 64 + cc * 8;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int rl = s * 8 + (lane >> 3);
@@ -238,12 +291,60 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
       const uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
       if (m < a.M && n < a.N) {
         const size_t off = (size_t)m * a.ldc + n;
-        const uint4 o = a.epi ? epilogue_op(a.epi, v, a.aux + off) : v;
+        uint4 o = v;
+        if (a.epi == 4) {
+          float f[8];
+          unpack8(v, f);
+          if (a.bn_relu) {
+            float yv[8];
+            unpack8(*(const uint4*)(a.aux + off), yv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = yv[q] > 0.f ? f[q] : 0.f;
+          }
+          o = pack8(f);
+          if (a.stats) {
+            float xv[8];
+            unpack8(*(const uint4*)(a.aux2 + off), xv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * (xv[q] - mu[q]); }
+          }
+        } else {
+          if (a.epi) o = epilogue_op(a.epi, v, a.aux + off);
+          if (a.stats) {
+            float f[8];
+            unpack8(v, f);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
+          }
+        }
         *(uint4*)((bf16_t*)a.C + off) = o;
       }
     }
     lgkm_wait0();  // this wave's reads of the slice retire before the next quadrant row overwrites it
   }
+  if (a.stats) {
+    // reduce over the 8 lanes sharing a column chunk (lane >> 3), lanes 0..7 write the slab row
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        s1[q] += __shfl_xor(s1[q], o, 64);
+        s2[q] += __shfl_xor(s2[q], o, 64);
+      }
+    }
+    if (lane < 8 && n < a.N) {
+      float* row = a.stats + (size_t)(tm * 2 + wm) * 2 * a.N;
+      *(float4*)(row + n) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+      *(float4*)(row + n + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
+      *(float4*)(row + a.N + n) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+      *(float4*)(row + a.N + n + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
+    }
+  }
+}
+
+int rsrc_bytes256(int64_t elems) {
+  const int64_t b = elems * 2;
+  return (b > 0x7fffffffLL) ? 0 : (int)b;
 }
 
 // ----------------------------------------------------------------- TN (weight gradients)
@@ -415,10 +516,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
   }
 }
 
-int rsrc_bytes256(int64_t elems) {
-  const int64_t b = elems * 2;
-  return (b > 0x7fffffffLL) ? 0 : (int)b;
-}
 
 }  // namespace
 
@@ -436,7 +533,7 @@ MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bia
   a.a_bytes = rsrc_bytes256((int64_t)M * lda);
   a.b_bytes = rsrc_bytes256((int64_t)N * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm256_nt_kernel, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+  hipLaunchKernelGGL(gemm256_nt_kernel<0>, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -458,5 +555,37 @@ MI_API int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, i
   a.b_bytes = rsrc_bytes256((int64_t)K * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(gemm256_tn_kernel, dim3(tiles * a.splits), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Implicit-GEMM convolution on the 256x256 pipeline.  mode 1 = forward: gathered = x [Nb,H,W,Cs],
+// rows = output pixels [Nb,P,Q], B = w [N][R][S][Cs]; mode 2 = stride-1 data gradient:
+// gathered = dy [Nb,H,W,Cs] (H,W = the forward output grid, Cs = forward K), rows = dx pixels
+// [Nb,P,Q], B = wt [N][R][S][Cs].  Cs % 64 == 0.  stats: [2 * cdiv(M, 256)][2][N] partials
+// (forward: sum / sum of squares; epi 4: BN-backward sums).  C bf16 [M][N].
+MI_API int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                           const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
+                           int Q, int R, int S, int stride, int pad, int N, hipStream_t st) {
+  if ((mode != 1 && mode != 2) || Cs % 64 != 0 || N % 8 != 0 || (mode == 2 && stride != 1) ||
+      !(epi == 0 || epi == 3 || epi == 4) || (epi == 3 && !aux) || (epi == 4 && bn_relu && !aux) ||
+      (epi == 4 && stats && (!aux2 || !mean)))
+    return (int)hipErrorInvalidValue;
+  G256Args a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = nullptr;
+  a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu; a.epi = epi;
+  a.stats = stats;
+  a.M = Nb * P * Q; a.N = N; a.K = R * S * Cs; a.lda = 0; a.ldb = a.K; a.ldc = N;
+  a.out_f32 = 0; a.accumulate = 0;
+  a.H = H; a.W = W; a.Cs = Cs; a.S = S; a.stride = stride; a.pad = pad;
+  a.fPQ = make_fastdiv((uint32_t)(P * Q)); a.fQ = make_fastdiv((uint32_t)Q);
+  a.fS = make_fastdiv((uint32_t)S); a.fCpt = make_fastdiv((uint32_t)(Cs / 64));
+  a.tiles_m = cdiv(a.M, G_BM); a.tiles_n = cdiv(N, G_BN);
+  a.a_bytes = rsrc_bytes256((int64_t)Nb * H * W * Cs);
+  a.b_bytes = rsrc_bytes256((int64_t)N * a.K);
+  if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  if (mode == 1)
+    hipLaunchKernelGGL(gemm256_nt_kernel<1>, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL(gemm256_nt_kernel<2>, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }

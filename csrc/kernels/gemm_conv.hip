@@ -25,29 +25,6 @@
 
 namespace {
 
-// ---------------------------------------------------------------- fast division
-struct FastDiv {
-  uint32_t d, mul, shift;
-};
-
-static FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  if (d == 1) { f.mul = 0; f.shift = 0; return f; }
-  uint32_t s = 0;
-  while ((1u << s) < d) ++s;
-  uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
-  f.mul = (uint32_t)m;
-  f.shift = s;
-  return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
-  if (f.d == 1) return x;
-  uint32_t t = __umulhi(x, f.mul);
-  return (t + ((x - t) >> 1)) >> (f.shift - 1);
-}
-
 struct ConvGeom {
   int H, W, Cs;      // gathered tensor spatial dims / channels (NHWC)
   int P, Q;          // "row pixel" spatial dims: rows index (n, p, q)
@@ -727,6 +704,36 @@ MI_API int mi_set_nt_stages(int stages) {
   return 0;
 }
 
+// Convolutions with >= 256 output channels and enough 256x256 tiles run on the deep-pipelined
+// kernel (gemm256.hip): forward and stride-1 data gradient (MI355X_DP_GEMM256=0 disables;
+// MI355X_DP_CONV256_MIN_TILES sets the minimum tile count, default 96).
+extern "C" int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                               const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs,
+                               int P, int Q, int R, int S, int stride, int pad, int N, hipStream_t st);
+static int g_gemm256_env = -1, g_conv256_min_tiles = -1;
+static bool use_gemm256_conv(int M, int N, int Cs) {
+  if (g_gemm256_env < 0) {
+    const char* e = std::getenv("MI355X_DP_GEMM256");
+    g_gemm256_env = (e && e[0] == '0') ? 0 : 1;
+    const char* t = std::getenv("MI355X_DP_CONV256_MIN_TILES");
+    g_conv256_min_tiles = t ? std::atoi(t) : 96;
+  }
+  return g_gemm256_env && Cs % 64 == 0 && N % 8 == 0 && N >= 256 &&
+         (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_conv256_min_tiles;
+}
+
+MI_API void mi_set_conv256_min_tiles(int t) {
+  use_gemm256_conv(0, 0, 0);  // env init
+  g_conv256_min_tiles = t;
+}
+
+// Statistics-slab rows written by a conv forward (M output pixels, N channels, Cs input channels).
+MI_API int mi_conv_stat_rows(int M, int N, int Cs) {
+  if (use_gemm256_conv(M, N, Cs)) return 2 * cdiv(M, 256);
+  const int bm = nt_choice(M, N) == 2 ? 64 : 128;
+  return cdiv(M, bm);
+}
+
 // Rows of the per-channel statistics slab written by a conv/GEMM forward with M rows, N cols.
 MI_API int mi_nt_stat_rows(int M, int N) {
   const int bm = nt_choice(M, N) == 2 ? 64 : 128;
@@ -739,6 +746,9 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
                          int Nb, int H, int W, int C, int K, int R, int S,
                          int stride, int pad, int P, int Q, int out_f32, hipStream_t st) {
   if ((C % 64 != 0 && C != 8) || K % 8 != 0) return (int)hipErrorInvalidValue;
+  if (!out_f32 && !bias && use_gemm256_conv(Nb * P * Q, K, C))
+    return mi_gemm256_conv(1, x, w, y, stats, 0, nullptr, nullptr, nullptr, 0, Nb, H, W, C, P, Q, R, S, stride, pad,
+                           K, st);
   NTArgs a{};
   a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias; a.stats = stats;
   a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
@@ -754,6 +764,9 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
   if (K % 64 != 0 || C % 8 != 0 || stride > 2) return (int)hipErrorInvalidValue;
+  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K))
+    return mi_gemm256_conv(2, dy, wt, dx, nullptr, 0, nullptr, nullptr, nullptr, 0, Nb, P, Q, K, H, W, R, S, 1, pad, C,
+                           st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
@@ -777,8 +790,9 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
 }
 
 // Statistics-slab rows written by mi_conv2d_dgrad_ex with stats (all parity classes).
-MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride) {
+MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride, int K) {
   const int M = Nb * H * W;
+  if (stride == 1 && use_gemm256_conv(M, C, K)) return 2 * cdiv(M, 256);
   const int bm = nt_choice(M, C) == 2 ? 64 : 128;
   if (stride == 1) return cdiv(M, bm);
   int mrows = 0;
@@ -796,6 +810,9 @@ MI_API int mi_conv2d_dgrad_ex(const void* dy, const void* wt, void* dx, int Nb, 
   if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4) || (epi && !aux && bn_relu) ||
       (epi == 3 && !aux) || (epi == 4 && stats && (!aux2 || !mean)))
     return (int)hipErrorInvalidValue;
+  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K))
+    return mi_gemm256_conv(2, dy, wt, dx, epi == 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
+                           bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;

@@ -80,3 +80,80 @@ def test_gemm256_tn(M, N, K):
     _lib.call("mi_gemm256_tn", ptr(A), ptr(B), ptr(C), M, N, K, M, N, N, stream_of(A))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < 1e-4
+
+
+CONV256 = [  # N, C, H, K, R, stride, pad
+    (2, 64, 14, 256, 1, 1, 0), (2, 256, 14, 256, 3, 1, 1), (3, 128, 9, 512, 3, 2, 1), (2, 512, 7, 320, 1, 1, 0),
+    (1, 64, 30, 256, 3, 1, 1)]
+
+
+@pytest.fixture
+def conv256_forced():
+    from mi355x_dp.ops import _lib
+    lib = _lib.load()
+    lib.mi_set_conv256_min_tiles(1)
+    yield lib
+    lib.mi_set_conv256_min_tiles(96)
+
+
+@pytest.mark.parametrize("shape", CONV256)
+def test_conv256_fwd_stats_and_dgrad(shape, conv256_forced):
+    """conv forward (+ BN statistics epilogue) and stride-1 dgrad (plain / accumulate / BN-backward
+    epilogues) on the 256x256 kernel vs the 128x128 kernel and an fp32 reference"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    lib = conv256_forced
+    N, C, H, K, R, s, p = shape
+    CL = torch.channels_last
+    P = (H + 2 * p - R) // s + 1
+    x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.05).to(BF).contiguous(memory_format=CL)
+    st = stream_of(x)
+    M = N * P * P
+    rows = lib.mi_conv_stat_rows(M, K, C)
+    assert rows == 2 * ((M + 255) // 256)
+    slab = torch.full((rows + 64, 2, K), float("nan"), device="cuda")
+    y = torch.empty(N, K, P, P, dtype=BF, device="cuda", memory_format=CL)
+    _lib.call("mi_conv2d_fwd", ptr(x), ptr(w), ptr(y), ptr(None), ptr(slab), N, H, H, C, K, R, R, s, p, P, P, 0, st)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), None, s, p)
+    assert rel_err(y, ref) < 1e-2
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, K)
+    assert rel_err(slab[:rows, 0].sum(0), yf.sum(0)) < 1e-3
+    assert rel_err(slab[:rows, 1].sum(0), (yf * yf).sum(0)) < 1e-3
+    if s != 1:
+        return
+    # dgrad: dx = conv_transpose(dy, w)
+    dy = torch.randn(N, K, P, P, device="cuda").to(BF).contiguous(memory_format=CL)
+    wt = torch.empty(C, R, R, K, dtype=BF, device="cuda")
+    _lib.call("mi_conv_wtrans", ptr(w), ptr(wt), K, R * R, C, st)
+    refdx = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), s, p)
+    dx = torch.empty_like(x)
+    _lib.call("mi_conv2d_dgrad", ptr(dy), ptr(wt), ptr(dx), N, H, H, C, K, R, R, s, p, P, P, st)
+    torch.cuda.synchronize()
+    assert rel_err(dx, refdx) < 1e-2
+    if C < 256:
+        return  # the dgrad output has C columns: only C >= 256 runs on the 256-wide tiles
+    # epi 3: accumulate into an existing gradient
+    base = torch.randn_like(x, dtype=torch.float32).to(BF).contiguous(memory_format=CL)
+    acc = base.clone()
+    _lib.call("mi_conv2d_dgrad_ex", ptr(dy), ptr(wt), ptr(acc), N, H, H, C, K, R, R, s, p, P, P, 3, ptr(acc),
+              ptr(None), ptr(None), 0, ptr(None), st)
+    torch.cuda.synchronize()
+    assert rel_err(acc, refdx + base.float()) < 1e-2
+    # epi 4: relu mask of the producing BN's output + its backward statistics
+    ybn = torch.randn_like(x, dtype=torch.float32).to(BF).contiguous(memory_format=CL)
+    xbn = torch.randn_like(x, dtype=torch.float32).to(BF).contiguous(memory_format=CL)
+    mean = torch.randn(C, device="cuda") * 0.1
+    r2 = lib.mi_dgrad_stat_rows(N, H, H, C, P, P, 1, K)
+    slab2 = torch.full((r2 + 64, 2, C), float("nan"), device="cuda")
+    dz = torch.empty_like(x)
+    _lib.call("mi_conv2d_dgrad_ex", ptr(dy), ptr(wt), ptr(dz), N, H, H, C, K, R, R, s, p, P, P, 4, ptr(ybn),
+              ptr(xbn), ptr(mean), 1, ptr(slab2), st)
+    torch.cuda.synchronize()
+    dzr = refdx * (ybn.float() > 0)
+    assert rel_err(dz, dzr) < 1e-2
+    dzf = dz.float().permute(0, 2, 3, 1).reshape(-1, C)
+    xf = xbn.float().permute(0, 2, 3, 1).reshape(-1, C)
+    assert rel_err(slab2[:r2, 0].sum(0), dzf.sum(0)) < 1e-3
+    assert rel_err(slab2[:r2, 1].sum(0), (dzf * (xf - mean)).sum(0)) < 1e-3
