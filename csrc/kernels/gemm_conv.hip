@@ -678,8 +678,20 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   return hipGetLastError();
 }
 
+// split-K block target of the TN (weight-gradient) kernels: every split adds its tile into the
+// fp32 gradient with atomics, whose chip-wide rate (~1.3 TB/s of added bytes) makes the atomic
+// volume ~ blocks x tile area the cost to balance against occupancy (MI355X_DP_TN_BLOCKS)
+static int g_tn_blocks = -1;
+static int tn_target_blocks() {
+  if (g_tn_blocks < 0) {
+    const char* e = std::getenv("MI355X_DP_TN_BLOCKS");
+    g_tn_blocks = e ? std::max(64, std::atoi(e)) : 768;
+  }
+  return g_tn_blocks;
+}
+
 hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
-  const int target = 1024;
+  const int target = tn_target_blocks();
   bool n64 = a.N <= 64;
   bool m64 = a.M <= 64;
   if (m64 && n64) return launch_tn<64, 64>(a, st, target);
