@@ -269,7 +269,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   const int n = n0 + wn * 64 + cc * 8;
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[8];
-  if (a.epi == 4 && a.stats && n < a.N) {
+  if (a.epi >= 4 && a.stats && n < a.N) {
     *(float4*)&mu[0] = *(const float4*)(a.mean + n);
     *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
   }
@@ -292,9 +292,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
       if (m < a.M && n < a.N) {
         const size_t off = (size_t)m * a.ldc + n;
         uint4 o = v;
-        if (a.epi == 4) {
+        if (a.epi >= 4) {
           float f[8];
           unpack8(v, f);
+          if (a.epi == 5) {  // dy = this dgrad + the gradient already in C (residual sum)
+            float c0[8];
+            unpack8(*(const uint4*)((const bf16_t*)a.C + off), c0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] += c0[q];
+          }
           if (a.bn_relu) {
             float yv[8];
             unpack8(*(const uint4*)(a.aux + off), yv);
@@ -567,8 +573,8 @@ MI_API int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, floa
                            const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
                            int Q, int R, int S, int stride, int pad, int N, hipStream_t st) {
   if ((mode != 1 && mode != 2) || Cs % 64 != 0 || N % 8 != 0 || (mode == 2 && stride != 1) ||
-      !(epi == 0 || epi == 3 || epi == 4) || (epi == 3 && !aux) || (epi == 4 && bn_relu && !aux) ||
-      (epi == 4 && stats && (!aux2 || !mean)))
+      !(epi == 0 || epi == 3 || epi == 4 || epi == 5) || (epi == 3 && !aux) || (epi >= 4 && bn_relu && !aux) ||
+      (epi >= 4 && stats && (!aux2 || !mean)))
     return (int)hipErrorInvalidValue;
   G256Args a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = nullptr;

@@ -54,6 +54,7 @@ struct NTArgs {
                      // 4 BatchNorm backward of the layer that produced this conv's input:
                      //   C <- dz = acc * [aux > 0] (relu mask on the BN output aux, if bn_relu),
                      //   stats <- per-channel (sum dz, sum dz * (aux2 - mean)), aux2 = BN input
+                     // 5: as 4 on acc + C (the gradient already in C: a block input's residual sum)
   const bf16_t* aux2;
   const float* mean;
   int bn_relu;
@@ -347,10 +348,17 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     if (n < a.N) {
       const size_t off = row_off(m) + n;
       uint4 o = v;
-      if (a.epi == 4) {
+      if (a.epi >= 4) {
         // BN backward: dz = dy * relu mask; stats (sum dz, sum dz * (x - mean)) of the rounded dz
+        // (epi 5: dy = this dgrad + the gradient already in C -- a block input's residual sum)
         float f[8], xv[8], mu[8];
         unpack8(v, f);
+        if (a.epi == 5) {
+          float c0[8];
+          unpack8(*(const uint4*)((const bf16_t*)a.C + off), c0);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] += c0[q];
+        }
         if (a.bn_relu) {
           float yv[8];
           unpack8(*(const uint4*)(a.aux + off), yv);
@@ -819,18 +827,18 @@ MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int str
 MI_API int mi_conv2d_dgrad_ex(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
                               const float* mean, int bn_relu, float* stats, hipStream_t st) {
-  if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4) || (epi && !aux && bn_relu) ||
-      (epi == 3 && !aux) || (epi == 4 && stats && (!aux2 || !mean)))
+  if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4 || epi == 5) ||
+      (epi && !aux && bn_relu) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)))
     return (int)hipErrorInvalidValue;
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K))
-    return mi_gemm256_conv(2, dy, wt, dx, epi == 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
+    return mi_gemm256_conv(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
                            bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
   a.lda = 0; a.ldb = a.K; a.ldc = C; a.mode = 2; a.out_f32 = 0; a.accumulate = 0;
   a.epi = epi; a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu;
-  a.stats = (epi == 4) ? stats : nullptr;
+  a.stats = (epi >= 4) ? stats : nullptr;
   a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
   a.b_bytes = rsrc_bytes((int64_t)C * a.K);
   a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);

@@ -16,7 +16,10 @@ With the block as one node the backward is scheduled explicitly:
   (sum dz2, sum dz2 * (c2 - mean2)) from the same registers -> bn2 needs no statistics pass
   and its apply pass reads dz2, c2 only (no y2);
   conv2 dgrad with epilogue 4 for bn1 likewise;
-  conv1 (and downsample) dgrad with epilogue 3: accumulate into dx in place -- no add kernel.
+  conv1 (and downsample) dgrad with epilogue 3: accumulate into dx in place -- no add kernel;
+  when the block input is the previous block's output, epilogue 5 instead: accumulate, then
+  the previous block's final relu mask + its last-BN backward statistics, handed over so the
+  previous block skips its statistics pass and uses the buffer as its residual gradient.
 
 Forward is the same kernel sequence as the per-op path (conv epilogue emits the BN forward
 statistics, BN apply fuses residual + ReLU).  Weight gradients go into the flat fp32 gradient
@@ -33,7 +36,15 @@ from ._lib import ptr, stream_of
 from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, weight_bf16
 
 F32 = torch.float32
-EPI_ACCUM, EPI_BN_BWD = 3, 4
+EPI_ACCUM, EPI_BN_BWD, EPI_ACCUM_BN_BWD = 3, 4, 5
+
+# Cross-block hand-off: the dgrad that completes block k+1's input gradient (residual sum) also
+# applies block k's final relu mask and emits block k's last-BN backward statistics (epilogue 5).
+# The statistics are parked here keyed by the gradient buffer; block k's backward takes them
+# only if it receives that very buffer unmodified (same storage, same version) -- otherwise
+# it runs its own statistics pass, which is still correct because re-masking is idempotent.
+_HANDOFF = {}
+HANDOFF_USED = [0]  # diagnostics: backward passes that consumed a hand-off
 
 
 def _out_hw(h, r, stride, pad):
@@ -157,7 +168,7 @@ class _ResBlock(torch.autograd.Function):
     if any, is appended last."""
 
     @staticmethod
-    def forward(ctx, x, specs, *params):
+    def forward(ctx, x, specs, prev_bnsrc, *params):
         ctx.params_order = params
         convs, bns, has_ds = specs
         n_main = len(convs) - (1 if has_ds else 0)
@@ -185,6 +196,8 @@ class _ResBlock(torch.autograd.Function):
         ctx.save_for_backward(*tensors)
         ctx.specs = specs
         ctx.n_main = n_main
+        ctx.out_bnsrc = (saved_c[-1], saved_m[-1])   # read by the next block (input = this output)
+        ctx.prev_bnsrc = prev_bnsrc
         return h
 
     @staticmethod
@@ -198,11 +211,23 @@ class _ResBlock(torch.autograd.Function):
             cd, md, isd = t[1 + 4 * n:]
         dout = _nhwc(dout)
         grads = {}
-        dx = torch.empty_like(x, memory_format=CL)
-        # last BN: relu + residual; dres -> dx (identity) or the downsample BN's output gradient
-        dyd = torch.empty_like(ys[-1], memory_format=CL) if has_ds else None
-        dc, gw, gb = _bn_bwd(dout, ys[-1], cs[-1], bns[n - 1], ms[-1], invs[-1], relu=1,
-                             dres=dyd if has_ds else dx)
+        hand = _HANDOFF.pop((dout.data_ptr(), dout.device.index), None)
+        if hand is not None and not (hand[2] == dout._version and hand[3] == cs[-1].data_ptr()
+                                     and dout.is_contiguous(memory_format=CL)):
+            hand = None
+        if hand is not None:
+            HANDOFF_USED[0] += 1
+            # dout is already dz3 (masked) with bn3's statistics computed by the next block: it IS
+            # the residual-path gradient, so it doubles as dyd / the initial dx (no copy)
+            dc, gw, gb = _bn_bwd_pre(dout, cs[-1], bns[n - 1], ms[-1], invs[-1], hand[0], hand[1])
+            dyd = dout if has_ds else None
+            dx = torch.empty_like(x, memory_format=CL) if has_ds else dout
+        else:
+            dx = torch.empty_like(x, memory_format=CL)
+            # last BN: relu + residual; dres -> dx (identity) or the downsample BN's output gradient
+            dyd = torch.empty_like(ys[-1], memory_format=CL) if has_ds else None
+            dc, gw, gb = _bn_bwd(dout, ys[-1], cs[-1], bns[n - 1], ms[-1], invs[-1], relu=1,
+                                 dres=dyd if has_ds else dx)
         grads[id(bns[n - 1].w)], grads[id(bns[n - 1].b)] = gw, gb
         for i in range(n - 1, 0, -1):
             inp = ys[i - 1]
@@ -216,8 +241,21 @@ class _ResBlock(torch.autograd.Function):
             grads[id(bns[-1].w)], grads[id(bns[-1].b)] = gw, gb
             grads[id(convs[-1].w)] = _wgrad(x, dcd, convs[-1])
             _dgrad(dcd, convs[-1], x.shape, dx)                            # dx = dgrad_ds
-        _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx)                   # dx += dgrad_1
-        out = [dx, None]
+        if ctx.prev_bnsrc is not None:
+            # dx = mask_prev * (dx + dgrad_1) + the previous block's last-BN backward statistics
+            c_prev, m_prev = ctx.prev_bnsrc
+            N, C, H, W = x.shape
+            lib = _lib.load()
+            rows = lib.mi_dgrad_stat_rows(N, H, W, C, dc.shape[2], dc.shape[3], convs[0].stride,
+                                          convs[0].w.shape[0])
+            slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dx.device)
+            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab)
+            _HANDOFF[(dx.data_ptr(), dx.device.index)] = (slab, rows, dx._version, c_prev.data_ptr())
+        else:
+            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx)               # dx += dgrad_1
+        ctx.prev_bnsrc = None
+        ctx.out_bnsrc = None
+        out = [dx, None, None]
         for p in ctx.params_order:
             out.append(grads.get(id(p)))
         return tuple(out)
@@ -258,4 +296,8 @@ def res_block(block, x):
     params = [c.w for c in cspecs]
     for b in bspecs:
         params += [b.w, b.b]
-    return _ResBlock.apply(x, (cspecs, bspecs, has_ds), *params)
+    prev = x.grad_fn
+    prev_bnsrc = getattr(prev, "out_bnsrc", None) if type(prev).__name__ == "_ResBlockBackward" else None
+    if prev_bnsrc is None:
+        _HANDOFF.clear()  # first block of a forward: drop hand-offs a skipped backward left behind
+    return _ResBlock.apply(x, (cspecs, bspecs, has_ds), prev_bnsrc, *params)

@@ -127,3 +127,45 @@ def test_single_bottleneck_fused_vs_per_op(inpl, planes, stride, ds, size):
         assert rel_err(g1[n], g0[n]) < 2e-2, n
     for n in b0:
         assert rel_err(b1[n], b0[n]) < 1e-4, n
+
+
+def test_block_chain_handoff_matches_per_op():
+    """three consecutive fused blocks (identity, downsample, identity): the cross-block hand-off
+    (epilogue 5) is used and gradients match the per-op path"""
+    import mi355x_dp.models.resnet as R
+    from mi355x_dp.models.layers import BatchNorm2d
+    from mi355x_dp.ops import resblock
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x0 = torch.randn(16, 256, 28, 28, device="cuda", generator=g).to(torch.bfloat16)
+    x0 = x0.contiguous(memory_format=torch.channels_last)
+    dout = torch.randn(16, 512, 14, 14, device="cuda", generator=g).to(torch.bfloat16)
+    dout = dout.contiguous(memory_format=torch.channels_last)
+    res = {}
+    for fused in (False, True):
+        torch.manual_seed(4)
+        down = torch.nn.Sequential(R.conv1x1(256, 512, 2), BatchNorm2d(512))
+        net = torch.nn.Sequential(R.Bottleneck(256, 64), R.Bottleneck(256, 128, 2, down),
+                                  R.Bottleneck(512, 128)).cuda()
+        with torch.no_grad():
+            for mod in net.modules():
+                if isinstance(mod, torch.nn.BatchNorm2d):
+                    mod.weight.uniform_(0.5, 1.5)
+                    mod.bias.uniform_(-0.2, 0.2)
+        old = R.FUSED_BLOCKS
+        R.FUSED_BLOCKS = fused
+        used0 = resblock.HANDOFF_USED[0]
+        try:
+            x = x0.clone().requires_grad_()
+            out = net(x)
+            out.backward(dout)
+        finally:
+            R.FUSED_BLOCKS = old
+        torch.cuda.synchronize()
+        if fused:
+            assert resblock.HANDOFF_USED[0] - used0 == 2   # blocks 1 and 2 receive hand-offs
+            assert not resblock._HANDOFF                     # block 0's input is not a block output
+        res[fused] = (x.grad.float(), {n: p.grad.float() for n, p in net.named_parameters()})
+    (dx0, g0), (dx1, g1) = res[False], res[True]
+    assert rel_err(dx1, dx0) < 2e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 2e-2, n
