@@ -116,3 +116,24 @@ def test_two_ranks_one_gpu_gloo(tmp_path):
                        capture_output=True, text=True, timeout=300, env={**os.environ, "PYTHONPATH": ROOT})
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("RANK_OK") == 2
+
+
+def test_notebook2_flow_example(tmp_path):
+    """examples/notebook2_flow.py: smddp estimator fit() of a workshop-style DDP script on the GPU,
+    model.tar.gz with module.-prefixed torchvision keys, deploy() + predict()."""
+    env = {**os.environ, "MI355X_DP_S3_ROOT": str(tmp_path / "s3"), "MI355X_DP_JOBS_ROOT": str(tmp_path / "jobs"),
+           "MI355X_DP_NPROC": "1"}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "notebook2_flow.py"), "--epochs", "1",
+                        "--n-train", "2048", "--n-test", "500", "--workdir", str(tmp_path / "w")],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=900, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "Initialized the distributed environment: 'smddp' backend on 1 nodes." in out
+    assert "Test set: Average loss:" in out and "Training seconds:" in out
+    assert "PREDICT_SHAPE (4, 1000)" in out
+    import tarfile
+    tar = [l.split()[1] for l in r.stdout.splitlines() if l.startswith("MODEL_DATA")][0]
+    with tarfile.open(tar) as tf:
+        tf.extract("model.pth", path=tmp_path)
+    sd = torch.load(tmp_path / "model.pth", map_location="cpu", weights_only=True)
+    assert next(iter(sd)) == "module.conv1.weight" and sd["module.fc.weight"].shape == (1000, 512)
