@@ -20,7 +20,14 @@
 //     SURVEY.md §5.3 failure detection);
 //   * allreduce AVG maps to ncclAvg; large all-reduces can be split into link-sized
 //     chunks queued back to back (MI355X_DP_SMDDP_CHUNK_MB) so a long bucket does not
-//     hold the comm stream in one monolithic kernel.
+//     hold the comm stream in one monolithic kernel;
+//   * MI355X_DP_SMDDP_IPC=1: fp32 SUM/AVG all-reduces up to MI355X_DP_SMDDP_IPC_MB (default 4)
+//     take a one-shot path over IPC peer pointers instead of RCCL (latency-bound buckets,
+//     SURVEY.md §2.3 N4): every rank exports one buffer (2 data slots + flags) through
+//     hipIpcGetMemHandle, handles travel through the c10d store, and the kernel
+//     (csrc/kernels/ipc_allreduce.hip, resolved from the kernel library) signals / waits on
+//     flags and sums the peers' slots directly over xGMI.  In this mode the RCCL communicator is
+//     created lazily by the first collective that needs it (same op on every rank).
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/Backend.hpp>
 #include <torch/csrc/distributed/c10d/Store.hpp>
@@ -38,6 +45,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <deque>
+#include <dlfcn.h>
 #include <mutex>
 #include <thread>
 
@@ -128,20 +136,21 @@ class SmddpBackend : public c10d::Backend {
         comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(true, (c10::DeviceIndex)device)),
         timeout_(std::chrono::milliseconds((int64_t)(timeout_s * 1000))) {
     HIPCHECK(hipSetDevice(device));
-    ncclUniqueId uid;
     const std::string key = "smddp/uid";
     if (rank == 0) {
-      NCCLCHECK(ncclGetUniqueId(&uid));
-      std::vector<uint8_t> v((uint8_t*)&uid, (uint8_t*)&uid + sizeof(uid));
+      NCCLCHECK(ncclGetUniqueId(&uid_));
+      std::vector<uint8_t> v((uint8_t*)&uid_, (uint8_t*)&uid_ + sizeof(uid_));
       store_->set(key, v);
     } else {
       auto v = store_->get(key);
-      TORCH_CHECK(v.size() == sizeof(uid), "smddp: bad unique id from store");
-      memcpy(&uid, v.data(), sizeof(uid));
+      TORCH_CHECK(v.size() == sizeof(uid_), "smddp: bad unique id from store");
+      memcpy(&uid_, v.data(), sizeof(uid_));
     }
-    NCCLCHECK(ncclCommInitRank(&comm_, size, uid, rank));
     HIPCHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
     if (const char* c = std::getenv("MI355X_DP_SMDDP_CHUNK_MB")) chunk_bytes_ = (size_t)(atof(c) * (1 << 20));
+    const char* ipc = std::getenv("MI355X_DP_SMDDP_IPC");
+    if (ipc && ipc[0] == '1' && size > 1) setup_ipc();
+    if (!ipc_on_) comm();  // eager RCCL bootstrap unless the IPC path may serve the first collectives
     watchdog_ = std::thread([this] { watchdog_loop(); });
   }
 
@@ -150,7 +159,87 @@ class SmddpBackend : public c10d::Backend {
     if (watchdog_.joinable()) watchdog_.join();
     hipEventDestroy(ready_);
     if (comm_) ncclCommDestroy(comm_);
+    if (ipc_on_) {
+      hipDeviceSynchronize();
+      for (int q = 0; q < size_; ++q)
+        if (q != rank_ && ipc_base_[q]) hipIpcCloseMemHandle(ipc_base_[q]);
+      if (ipc_base_[rank_]) hipFree(ipc_base_[rank_]);
+      if (ipc_err_) hipHostFree(ipc_err_);
+    }
   }
+
+  // RCCL communicator, created on first use (ncclCommInitRank is collective: every rank reaches
+  // it in the same collective because the RCCL / IPC choice depends only on the op's shape)
+  ncclComm_t comm() {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    if (!comm_) NCCLCHECK(ncclCommInitRank(&comm_, size_, uid_, rank_));
+    return comm_;
+  }
+
+  bool ipc_enabled() const { return ipc_on_; }
+
+ private:
+  using IpcFn = int (*)(const float* const*, uint32_t* const*, int, int, float*, int64_t, uint32_t, float, int*,
+                        uint32_t, hipStream_t);
+
+  void setup_ipc() {
+    const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
+    void* h = lib ? dlopen(lib, RTLD_NOW | RTLD_GLOBAL) : nullptr;
+    ipc_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce_f32") : nullptr;
+    if (!ipc_fn_ || size_ > 8) {
+      fprintf(stderr, "smddp: IPC all-reduce unavailable (kernel library %s); using RCCL only\n", lib ? lib : "unset");
+      return;
+    }
+    if (const char* c = std::getenv("MI355X_DP_SMDDP_IPC_MB")) ipc_cap_ = (size_t)(atof(c) * (1 << 20));
+    ipc_cap_ = (ipc_cap_ + 255) & ~(size_t)255;
+    const size_t bytes = 2 * ipc_cap_ + 4096;
+    void* mine = nullptr;
+    HIPCHECK(hipMalloc(&mine, bytes));
+    HIPCHECK(hipMemset(mine, 0, bytes));
+    HIPCHECK(hipDeviceSynchronize());
+    hipIpcMemHandle_t hnd;
+    HIPCHECK(hipIpcGetMemHandle(&hnd, mine));
+    store_->set("smddp/ipc/" + std::to_string(rank_),
+                std::vector<uint8_t>((uint8_t*)&hnd, (uint8_t*)&hnd + sizeof(hnd)));
+    ipc_base_.assign(size_, nullptr);
+    ipc_base_[rank_] = mine;
+    for (int q = 0; q < size_; ++q) {
+      if (q == rank_) continue;
+      auto v = store_->get("smddp/ipc/" + std::to_string(q));
+      TORCH_CHECK(v.size() == sizeof(hipIpcMemHandle_t), "smddp: bad IPC handle from rank ", q);
+      hipIpcMemHandle_t ph;
+      memcpy(&ph, v.data(), sizeof(ph));
+      HIPCHECK(hipIpcOpenMemHandle(&ipc_base_[q], ph, hipIpcMemLazyEnablePeerAccess));
+    }
+    HIPCHECK(hipHostMalloc((void**)&ipc_err_, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    *ipc_err_ = 0;
+    HIPCHECK(hipHostGetDevicePointer((void**)&ipc_err_dev_, ipc_err_, 0));
+    ipc_on_ = true;
+  }
+
+  bool ipc_eligible(const std::vector<at::Tensor>& ts, const c10d::AllreduceOptions& opts) const {
+    if (!ipc_on_ || ts.size() != 1) return false;
+    const auto& t = ts[0];
+    return t.scalar_type() == at::kFloat && t.is_contiguous() && (size_t)t.numel() * 4 <= ipc_cap_ &&
+           (opts.reduceOp == c10d::ReduceOp::SUM || opts.reduceOp == c10d::ReduceOp::AVG);
+  }
+
+  void ipc_allreduce(at::Tensor& t, bool avg, hipStream_t s) {
+    const uint32_t epoch = ++ipc_epoch_;
+    const size_t slot = (epoch & 1) * ipc_cap_;
+    const float* data[8];
+    uint32_t* flags[8];
+    for (int q = 0; q < size_; ++q) {
+      data[q] = (const float*)((char*)ipc_base_[q] + slot);
+      flags[q] = (uint32_t*)((char*)ipc_base_[q] + 2 * ipc_cap_);
+    }
+    HIPCHECK(hipMemcpyAsync((char*)ipc_base_[rank_] + slot, t.data_ptr(), t.numel() * 4, hipMemcpyDeviceToDevice, s));
+    const int rc = ipc_fn_(data, flags, rank_, size_, (float*)t.data_ptr(), t.numel(), epoch,
+                           avg ? 1.f / size_ : 1.f, ipc_err_dev_, ipc_spin_limit_, s);
+    TORCH_CHECK(rc == 0, "smddp: IPC all-reduce launch failed with hipError ", rc);
+  }
+
+ public:
 
   const std::string getBackendName() const override { return "smddp"; }
 
@@ -182,13 +271,17 @@ class SmddpBackend : public c10d::Backend {
     char* p = (char*)t.data_ptr();
     for (size_t off = 0; off < n; off += chunk) {
       size_t cnt = std::min(chunk, n - off);
-      NCCLCHECK(ncclAllReduce(p + off * esz, p + off * esz, cnt, to_nccl(t.scalar_type()), op, comm_, s));
+      NCCLCHECK(ncclAllReduce(p + off * esz, p + off * esz, cnt, to_nccl(t.scalar_type()), op, comm(), s));
     }
   }
 
   // ------------------------------------------------------------ collectives
   c10::intrusive_ptr<c10d::Work> allreduce(std::vector<at::Tensor>& tensors,
                                            const c10d::AllreduceOptions& opts) override {
+    if (ipc_eligible(tensors, opts)) {
+      const bool avg = opts.reduceOp == c10d::ReduceOp::AVG;
+      return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) { ipc_allreduce(tensors[0], avg, s); });
+    }
     auto op = to_nccl(opts.reduceOp);
     return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) {
       NCCLCHECK(ncclGroupStart());
@@ -213,7 +306,7 @@ class SmddpBackend : public c10d::Backend {
       NCCLCHECK(ncclGroupStart());
       for (auto& t : tensors)
         NCCLCHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
-                                (int)opts.rootRank, comm_, s));
+                                (int)opts.rootRank, comm(), s));
       NCCLCHECK(ncclGroupEnd());
     });
   }
@@ -222,7 +315,7 @@ class SmddpBackend : public c10d::Backend {
     return run(c10d::OpType::REDUCE, tensors, tensors, [&](hipStream_t s) {
       for (auto& t : tensors)
         NCCLCHECK(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
-                             to_nccl(opts.reduceOp), (int)opts.rootRank, comm_, s));
+                             to_nccl(opts.reduceOp), (int)opts.rootRank, comm(), s));
     });
   }
 
@@ -230,7 +323,7 @@ class SmddpBackend : public c10d::Backend {
                                                  const c10d::AllgatherOptions&) override {
     TORCH_CHECK(out.numel() == in.numel() * size_, "smddp _allgather_base: size mismatch");
     return run(c10d::OpType::_ALLGATHER_BASE, {out, in}, {out}, [&](hipStream_t s) {
-      NCCLCHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, s));
+      NCCLCHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm(), s));
     });
   }
 
@@ -243,7 +336,7 @@ class SmddpBackend : public c10d::Backend {
     std::vector<at::Tensor> touched{in, flat};
     for (auto& o : outputs[0]) touched.push_back(o);
     return run(c10d::OpType::ALLGATHER, touched, outputs[0], [&](hipStream_t s) {
-      NCCLCHECK(ncclAllGather(in.data_ptr(), flat.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, s));
+      NCCLCHECK(ncclAllGather(in.data_ptr(), flat.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm(), s));
       c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
       for (int r = 0; r < size_; ++r) outputs[0][r].copy_(flat.narrow(0, r * in.numel(), in.numel()).view_as(in), true);
     });
@@ -254,7 +347,7 @@ class SmddpBackend : public c10d::Backend {
     TORCH_CHECK(in.numel() == out.numel() * size_, "smddp _reduce_scatter_base: size mismatch");
     return run(c10d::OpType::_REDUCE_SCATTER_BASE, {out, in}, {out}, [&](hipStream_t s) {
       NCCLCHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()),
-                                  to_nccl(opts.reduceOp), comm_, s));
+                                  to_nccl(opts.reduceOp), comm(), s));
     });
   }
 
@@ -266,7 +359,7 @@ class SmddpBackend : public c10d::Backend {
     auto flat = at::cat(inputs[0]).contiguous();
     return run(c10d::OpType::REDUCE_SCATTER, {out, flat}, outputs, [&](hipStream_t s) {
       NCCLCHECK(ncclReduceScatter(flat.data_ptr(), out.data_ptr(), out.numel(), to_nccl(out.scalar_type()),
-                                  to_nccl(opts.reduceOp), comm_, s));
+                                  to_nccl(opts.reduceOp), comm(), s));
     });
   }
 
@@ -279,8 +372,8 @@ class SmddpBackend : public c10d::Backend {
     return run(c10d::OpType::ALLTOALL_BASE, {out, in}, {out}, [&](hipStream_t s) {
       NCCLCHECK(ncclGroupStart());
       for (int r = 0; r < size_; ++r) {
-        NCCLCHECK(ncclSend((char*)in.data_ptr() + r * n * esz, n, to_nccl(in.scalar_type()), r, comm_, s));
-        NCCLCHECK(ncclRecv((char*)out.data_ptr() + r * n * esz, n, to_nccl(out.scalar_type()), r, comm_, s));
+        NCCLCHECK(ncclSend((char*)in.data_ptr() + r * n * esz, n, to_nccl(in.scalar_type()), r, comm(), s));
+        NCCLCHECK(ncclRecv((char*)out.data_ptr() + r * n * esz, n, to_nccl(out.scalar_type()), r, comm(), s));
       }
       NCCLCHECK(ncclGroupEnd());
     });
@@ -288,13 +381,13 @@ class SmddpBackend : public c10d::Backend {
 
   c10::intrusive_ptr<c10d::Work> send(std::vector<at::Tensor>& tensors, int dst, int) override {
     return run(c10d::OpType::SEND, tensors, tensors, [&](hipStream_t s) {
-      for (auto& t : tensors) NCCLCHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), dst, comm_, s));
+      for (auto& t : tensors) NCCLCHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), dst, comm(), s));
     });
   }
 
   c10::intrusive_ptr<c10d::Work> recv(std::vector<at::Tensor>& tensors, int src, int) override {
     return run(c10d::OpType::RECV, tensors, tensors, [&](hipStream_t s) {
-      for (auto& t : tensors) NCCLCHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), src, comm_, s));
+      for (auto& t : tensors) NCCLCHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), src, comm(), s));
     });
   }
 
@@ -302,7 +395,7 @@ class SmddpBackend : public c10d::Backend {
     auto t = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(c10::Device(c10::DeviceType::CUDA,
                                                                                       (c10::DeviceIndex)device_)));
     return run(c10d::OpType::BARRIER, {t}, {t}, [&](hipStream_t s) {
-      NCCLCHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), 1, ncclFloat32, ncclSum, comm_, s));
+      NCCLCHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), 1, ncclFloat32, ncclSum, comm(), s));
     }, /*blocking=*/true);
   }
 
@@ -312,6 +405,11 @@ class SmddpBackend : public c10d::Backend {
   void watchdog_loop() {
     while (!stop_) {
       std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      if (ipc_err_ && __atomic_load_n(ipc_err_, __ATOMIC_RELAXED)) {
+        fprintf(stderr, "smddp watchdog: rank %d IPC all-reduce timed out waiting for peers; aborting\n", rank_);
+        fflush(stderr);
+        std::abort();
+      }
       std::lock_guard<std::mutex> lk(mu_);
       while (!pending_.empty()) {
         auto& w = pending_.front();
@@ -323,7 +421,7 @@ class SmddpBackend : public c10d::Backend {
           fprintf(stderr, "smddp watchdog: rank %d collective did not complete within %lld ms; aborting\n", rank_,
                   (long long)timeout_.count());
           fflush(stderr);
-          ncclCommAbort(comm_);
+          if (comm_) ncclCommAbort(comm_);
           comm_ = nullptr;
           std::abort();
         }
@@ -337,6 +435,16 @@ class SmddpBackend : public c10d::Backend {
   HIPStreamMasqueradingAsCUDA comm_stream_;
   std::chrono::milliseconds timeout_;
   ncclComm_t comm_ = nullptr;
+  ncclUniqueId uid_;
+  std::mutex init_mu_;
+  bool ipc_on_ = false;
+  IpcFn ipc_fn_ = nullptr;
+  size_t ipc_cap_ = 4u << 20;
+  std::vector<void*> ipc_base_;
+  int* ipc_err_ = nullptr;      // host-mapped: the watchdog reads it without a device sync
+  int* ipc_err_dev_ = nullptr;
+  uint32_t ipc_epoch_ = 0;
+  uint32_t ipc_spin_limit_ = 4000000;  // x s_sleep(8): seconds, then the error word (never a hang)
   hipEvent_t ready_;
   size_t chunk_bytes_ = 0;
   std::mutex mu_;

@@ -41,6 +41,8 @@ def bind_local_device():
         return None
     local_rank = int(os.environ.get("LOCAL_RANK", os.environ.get("OMPI_COMM_WORLD_LOCAL_RANK", "0")))
     dev = local_rank % n
+    if os.environ.get("MI355X_DP_SMDDP_DEVICE"):  # testing: several ranks sharing one GPU (IPC path)
+        dev = int(os.environ["MI355X_DP_SMDDP_DEVICE"])
     torch.cuda.set_device(dev)
     return dev
 
@@ -62,6 +64,11 @@ def create_backend(store, rank, world_size, timeout):
             from . import _smddp_native
             mod = _smddp_native.load()
             if mod is not None:
+                if os.environ.get("MI355X_DP_SMDDP_IPC") == "1":
+                    # the one-shot IPC all-reduce kernel lives in the HIP kernel library
+                    from mi355x_dp.ops import _lib
+                    _lib.load(True)
+                    os.environ.setdefault("MI355X_DP_KERNELS_LIB", _lib.KERNEL_LIB)
                 secs = timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout)
                 return mod.create_backend(store, rank, world_size, dev, secs)
         except ImportError:

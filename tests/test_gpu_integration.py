@@ -137,3 +137,32 @@ def test_notebook2_flow_example(tmp_path):
         tf.extract("model.pth", path=tmp_path)
     sd = torch.load(tmp_path / "model.pth", map_location="cpu", weights_only=True)
     assert next(iter(sd)) == "module.conv1.weight" and sd["module.fc.weight"].shape == (1000, 512)
+
+
+def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path):
+    """SURVEY N4 one-shot IPC all-reduce in the native smddp backend: 2 ranks sharing cuda:0
+    (IPC handles opened by the peer process), many back-to-back calls (slot parity reuse),
+    SUM and AVG, sizes up to the cap; RCCL is never initialised on this path."""
+    script = tmp_path / "ipc.py"
+    script.write_text(
+        "import os, sys, torch, torch.distributed as dist\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.append({os.path.join(ROOT, 'compat')!r})\n"
+        "import smdistributed.dataparallel.torch.torch_smddp\n"
+        "dist.init_process_group(backend='smddp')\n"
+        "r, w = dist.get_rank(), dist.get_world_size()\n"
+        "for it in range(40):\n"
+        "    n = [1, 7, 1000, 65536, 1 << 20][it % 5]\n"
+        "    t = torch.arange(n, device='cuda', dtype=torch.float32) * (r + 1) + it\n"
+        "    op = dist.ReduceOp.AVG if it % 2 else dist.ReduceOp.SUM\n"
+        "    dist.all_reduce(t, op=op)\n"
+        "    base = torch.arange(n, device='cuda', dtype=torch.float32)\n"
+        "    ref = base * sum(q + 1 for q in range(w)) + it * w\n"
+        "    if op == dist.ReduceOp.AVG: ref = ref / w\n"
+        "    assert torch.allclose(t, ref, rtol=1e-6, atol=1e-3), (it, (t - ref).abs().max().item())\n"
+        "torch.cuda.synchronize()\n"
+        "print('IPC_OK', r, flush=True)\n")
+    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC": "1", "MI355X_DP_SMDDP_DEVICE": "0"}
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2", str(script)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("IPC_OK") == 2
