@@ -6,6 +6,24 @@
 
 #define MI_API extern "C" __attribute__((visibility("default")))
 
+// Device-side invariant checks of the debug build (-DMI_DEBUG, MI355X_DP_DEBUG_KERNELS=1): print
+// the failing condition with the block / thread and a value, then trap.  Compiled out otherwise.
+#ifdef MI_DEBUG
+#include <cstdio>
+#define MI_ASSERT(cond, val)                                                                          \
+  do {                                                                                                \
+    if (!(cond)) {                                                                                    \
+      printf("MI_ASSERT %s:%d (%s) block %d thread %d value %lld\n", __FILE__, __LINE__, #cond,       \
+             (int)blockIdx.x, (int)threadIdx.x, (long long)(val));                                    \
+      __builtin_trap();                                                                               \
+    }                                                                                                 \
+  } while (0)
+#else
+#define MI_ASSERT(cond, val) \
+  do {                       \
+  } while (0)
+#endif
+
 typedef uint16_t bf16_t;  // raw bf16 bits in memory
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));

@@ -147,6 +147,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const int h = (hw >> 16) + dh, w = ((int)(short)(hw & 0xffff)) + dw;
         const bool ok = t < nk && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
         const uint32_t vo = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
+        MI_ASSERT(vo == OOB || vo + 16u <= (uint32_t)a.a_bytes, vo);  // valid taps never rely on zero fill
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0, 0);
       }
     }
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
       const uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
       if (m < a.M && n < a.N) {
         const size_t off = (size_t)m * a.ldc + n;
+        MI_ASSERT(n + 8 <= a.N, n);
         uint4 o = v;
         if (a.epi >= 4) {
           float f[8];

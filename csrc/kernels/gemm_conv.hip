@@ -347,6 +347,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     const uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
     if (n < a.N) {
       const size_t off = row_off(m) + n;
+      MI_ASSERT(off + 8 <= (size_t)(a.mode == 3 ? a.M : Mrows) * a.ldc, (long long)off);
       uint4 o = v;
       if (a.epi >= 4) {
         // BN backward: dz = dy * relu mask; stats (sum dz, sum dz * (x - mean)) of the rounded dz

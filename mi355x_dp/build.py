@@ -43,12 +43,15 @@ def _digest(paths, extra=""):
     return h.hexdigest()
 
 
-def build_kernels(force=False, verbose=True):
+def build_kernels(force=False, verbose=True, debug=False):
+    """debug=True: libmi355x_kernels_debug.so with -DMI_DEBUG (device-side bounds asserts that
+    printf the failing index and trap), selected at run time by MI355X_DP_DEBUG_KERNELS=1."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    out = os.path.join(NATIVE, "libmi355x_kernels.so")
+    flags = HIP_FLAGS + (["-DMI_DEBUG", "-g"] if debug else [])
+    out = os.path.join(NATIVE, "libmi355x_kernels_debug.so" if debug else "libmi355x_kernels.so")
     stamp = out + ".sha256"
-    dig = _digest(srcs + hdrs, " ".join(HIP_FLAGS))
+    dig = _digest(srcs + hdrs, " ".join(flags))
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == dig:
         if verbose:
             print(f"[build] {os.path.relpath(out, ROOT)} up to date")
@@ -58,8 +61,8 @@ def build_kernels(force=False, verbose=True):
     objs = []
 
     def one(src):
-        obj = os.path.join(BUILD, "kernels", os.path.basename(src) + ".o")
-        _run([HIPCC, *HIP_FLAGS, "-c", src, "-o", obj])
+        obj = os.path.join(BUILD, "kernels", os.path.basename(src) + (".dbg.o" if debug else ".o"))
+        _run([HIPCC, *flags, "-c", src, "-o", obj])
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
@@ -125,7 +128,7 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     force = "--force" in sys.argv
     if what == "kernels":
-        build_kernels(force)
+        build_kernels(force, debug="--debug" in sys.argv)
     elif what == "launcher":
         build_launcher(force)
     elif what == "comm":

@@ -21,6 +21,12 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 NATIVE_DIR = os.path.normpath(os.path.join(_HERE, "..", "_native"))
 KERNEL_LIB = os.path.join(NATIVE_DIR, "libmi355x_kernels.so")
+# MI355X_DP_DEBUG_KERNELS=1: the -DMI_DEBUG build (device bounds asserts; `python -m mi355x_dp.build
+# kernels --debug`).  MI355X_DP_SYNC_CHECK=1: synchronise after every native call so an
+# asynchronous device fault is reported against the kernel that caused it.
+if os.environ.get("MI355X_DP_DEBUG_KERNELS") == "1":
+    KERNEL_LIB = os.path.join(NATIVE_DIR, "libmi355x_kernels_debug.so")
+SYNC_CHECK = os.environ.get("MI355X_DP_SYNC_CHECK") == "1"
 
 _lock = threading.Lock()
 _lib = None
@@ -95,3 +101,9 @@ def call(name, *args):
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
+    if SYNC_CHECK:
+        import torch
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError(f"{name}: device error after launch ({e})") from e

@@ -122,6 +122,10 @@ class TrainingJob:
         env = env_vars(tenv)
         env.update(self.environment)
         env["PYTHONUNBUFFERED"] = "1"
+        if str(self.environment.get("MI355X_DP_DEBUGGER", "1")) not in ("0", "false", "False"):
+            # SageMaker attaches its Debugger hook inside the container; ours records the same
+            # parameter inventory and "losses" collection under output/tensors
+            env["MI355X_DP_DEBUGGER"] = os.path.join(self.output_dir, "tensors")
         print("Training Env:\n" + json.dumps(tenv, indent=4, sort_keys=True), flush=True)
         print("Environment variables:\n" + "\n".join(f"{k}={v}" for k, v in sorted(env.items())
                                                        if k.startswith("SM_")), flush=True)

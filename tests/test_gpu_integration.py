@@ -166,3 +166,28 @@ def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path):
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("IPC_OK") == 2
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "mi355x_dp", "_native", "libmi355x_kernels_debug.so")),
+                    reason="debug kernel library not built (python -m mi355x_dp.build kernels --debug)")
+def test_debug_kernels_training_step_clean(tmp_path):
+    """the -DMI_DEBUG kernel build (device bounds asserts) with per-call synchronous
+    error checking runs a fused ResNet training step + ViT layer without tripping an assert."""
+    code = (
+        f"import sys; sys.path.insert(0, {ROOT!r})\n"
+        "import torch\n"
+        "from mi355x_dp.models import get_model\n"
+        "from mi355x_dp.ops import cross_entropy, _lib\n"
+        "assert _lib.KERNEL_LIB.endswith('_debug.so') and _lib.SYNC_CHECK\n"
+        "for name, size in (('resnet50', 64), ('resnet18', 32)):\n"
+        "    m = get_model(name, num_classes=10).cuda()\n"
+        "    x = torch.randn(4, 3, size, size, device='cuda'); y = torch.randint(0, 10, (4,), device='cuda')\n"
+        "    cross_entropy(m(x), y).backward()\n"
+        "from mi355x_dp.models.vit import VisionTransformer\n"
+        "v = VisionTransformer(image_size=32, patch_size=16, num_layers=1, num_heads=2, hidden_dim=128, mlp_dim=256,\n"
+        "                      num_classes=10).cuda()\n"
+        "v(torch.randn(2, 3, 32, 32, device='cuda')).float().sum().backward()\n"
+        "torch.cuda.synchronize(); print('DEBUG_OK')\n")
+    env = {**os.environ, "MI355X_DP_DEBUG_KERNELS": "1", "MI355X_DP_SYNC_CHECK": "1"}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "DEBUG_OK" in r.stdout, (r.stdout + r.stderr)[-3000:]

@@ -101,6 +101,12 @@ print('MODEL_DATA', est.model_data)
     assert "[1,mpirank:1,algo-1]<stdout>:" in out
     assert "Training seconds:" in out and "Completed - Training job completed" in out
     assert "SHAPES (4, 10) (4, 10)" in out
+    # observability hook auto-attached by the job: inventory + losses collection
+    assert "[mi355x_dp.debugger] Total Trainable Params: 62006" in out
+    assert "name:module.conv1.weight count_params:450" in out
+    import glob
+    losses = glob.glob(str(tmp_path / "jobs" / "**" / "collections" / "losses.jsonl"), recursive=True)
+    assert losses and all(json.loads(l)["loss"] > 0 for l in open(losses[0]))
     from mi355x_dp.sagemaker_local.session import s3_to_local
     os.environ["MI355X_DP_S3_ROOT"] = str(tmp_path / "s3")
     tar = s3_to_local([l.split()[1] for l in r.stdout.splitlines() if l.startswith("MODEL_DATA")][0])
