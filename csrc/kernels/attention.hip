@@ -56,13 +56,31 @@ __device__ __forceinline__ void store4bf(bf16_t* p, f32x4 v, float s) {
   *(uint2*)p = make_uint2(pack2bf(v[0] * s, v[1] * s), pack2bf(v[2] * s, v[3] * s));
 }
 
-// rows [0, TP) of a [T][ld] bf16 matrix (64 columns at col0) -> LDS [TP][KSTR], zero rows >= T
-__device__ __forceinline__ void stage_rows(bf16_t* dst, const bf16_t* src, int ld, int T, int TP) {
-  for (int c = threadIdx.x; c < TP * 8; c += 256) {
-    const int row = c >> 3, part = c & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row < T) v = *(const uint4*)(src + (size_t)row * ld + part * 8);
-    *(uint4*)&dst[row * KSTR + part * 8] = v;
+// rows [0, TP) of two [T][ld] bf16 matrices (64 columns each) -> LDS [TP][KSTR], zero rows >= T.
+// All of a thread's global loads are issued before any LDS store (fully unrolled, fixed trip
+// count), so the staging costs one memory latency instead of one per 16-byte chunk.
+template <int TP>
+__device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, int ld0, bf16_t* dst1,
+                                            const bf16_t* src1, int ld1, int T) {
+  constexpr int PER = (TP * 8 + 255) / 256;
+  uint4 v0[PER], v1[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + 256 * i, row = c >> 3, part = c & 7;
+    v0[i] = make_uint4(0, 0, 0, 0);
+    v1[i] = make_uint4(0, 0, 0, 0);
+    if (c < TP * 8 && row < T) {
+      v0[i] = *(const uint4*)(src0 + (size_t)row * ld0 + part * 8);
+      v1[i] = *(const uint4*)(src1 + (size_t)row * ld1 + part * 8);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + 256 * i, row = c >> 3, part = c & 7;
+    if (c < TP * 8) {
+      *(uint4*)&dst0[row * KSTR + part * 8] = v0[i];
+      *(uint4*)&dst1[row * KSTR + part * 8] = v1[i];
+    }
   }
 }
 
@@ -75,8 +93,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
-  stage_rows(Ks, base + D, ld, T, TP);
-  stage_rows(Vs, base + 2 * D, ld, T, TP);
+  stage_rows2<TP>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
@@ -148,8 +165,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
-  stage_rows(Ks, base + D, ld, T, TP);
-  stage_rows(Vs, base + 2 * D, ld, T, TP);
+  stage_rows2<TP>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
@@ -222,8 +238,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const bf16_t* __re
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
-  stage_rows(Qs, base, ld, T, TP);
-  stage_rows(Ds, dout + (size_t)b * T * D + h * HD, D, T, TP);
+  stage_rows2<TP>(Qs, base, ld, Ds, dout + (size_t)b * T * D + h * HD, D, T);
   for (int i = threadIdx.x; i < TP; i += 256) {
     Ls[i] = i < T ? lse[(size_t)bh * T + i] * LOG2E : INFINITY;  // padded queries: P = 0
     Dv[i] = i < T ? dvec[(size_t)bh * T + i] : 0.f;

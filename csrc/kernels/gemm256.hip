@@ -28,6 +28,8 @@
 //  * XCD-aware, M-grouped tile order (GROUP_M 8) for L2 reuse of the B panel.
 #include "common.h"
 #include "epilogue.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -56,6 +58,12 @@ struct G256Args {
   const bf16_t* aux2;   // epi 4: BN input x
   const float* mean;    // epi 4: BN batch mean
   int bn_relu;
+  // tail split-K (wave quantization): blocks [0, full_blocks) own whole tiles; the tiles of the
+  // last, partial wave are split `tail_split` ways along K; the last-arriving split of a tile adds
+  // the others' fp32 partials (workspace `ws`, per-tile arrival `counters`) and runs the epilogue
+  int full_blocks, tail_split;
+  float* ws;
+  int* counters;
 };
 
 __device__ __forceinline__ void vm_wait6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
@@ -72,15 +80,27 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   const int wm = wid >> 2, wn = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
 
-  // tile order: XCD remap, then GROUP_M-row groups sweeping N
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // tile order: XCD remap, then GROUP_M-row groups sweeping N; tail tiles split along K
+  const int nk = (a.K + G_BK - 1) / G_BK;
+  int bid, kt0 = 0, kt1 = nk, split = 0, tail_tile = -1;
+  if ((int)blockIdx.x < a.full_blocks) {
+    bid = xcd_remap(blockIdx.x, a.full_blocks);
+  } else {
+    const int nunits = gridDim.x - a.full_blocks;
+    const int u = xcd_remap(blockIdx.x - a.full_blocks, nunits);
+    tail_tile = u / a.tail_split;
+    split = u - tail_tile * a.tail_split;
+    bid = a.full_blocks + tail_tile;
+    kt0 = split * nk / a.tail_split;
+    kt1 = (split + 1) * nk / a.tail_split;
+  }
   const int group = bid / (GROUP_M * a.tiles_n);
   const int first_m = group * GROUP_M;
   const int gsz = min(a.tiles_m - first_m, GROUP_M);
   const int tm = first_m + (bid % (GROUP_M * a.tiles_n)) % gsz;
   const int tn = (bid % (GROUP_M * a.tiles_n)) / gsz;
   const int m0 = tm * G_BM, n0 = tn * G_BN;
-  const int nk = (a.K + G_BK - 1) / G_BK;
+  const int nkl = kt1 - kt0;  // this block's k-tiles
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
@@ -122,19 +142,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   }
 
   // issue part `part` of operand `which` (0 = A, 1 = B) for k-tile t (zero-fill past the end)
-  auto issue = [&](int t, int which, int part) {
+  auto issue = [&](int t, int which, int part) {  // t: local k-tile (buffer parity), ta: absolute
     uint4* dst = smem + ((t & 1) * 4 + which * 2 + part) * PART_U4;
-    const uint32_t kb = (uint32_t)t * (G_BK * 2);
+    const int ta = kt0 + t;
+    const uint32_t kb = (uint32_t)ta * (G_BK * 2);
     if (which == 1 || MODE == 0) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const uint32_t vo = t < klim[i] ? (which == 0 ? a_vo[part][i] : b_vo[part][i]) + kb : OOB;
+        const uint32_t vo = (ta < kt1 && ta < klim[i]) ? (which == 0 ? a_vo[part][i] : b_vo[part][i]) + kb : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(which == 0 ? rsA : rsB, LDS_PTR(void, dst + i * 512 + wid * 64),
                                                  16, vo, 0, 0, 0);
       }
     } else {
       // wave-uniform tap / channel block of k-tile t
-      const int tt = t < nk ? t : 0;
+      const int tt = ta < kt1 ? ta : 0;
       const int tap = (int)fdiv((uint32_t)tt, a.fCpt);
       const int c0 = (tt - tap * (int)a.fCpt.d) * 64;
       const int r = (int)fdiv((uint32_t)tap, a.fS);
@@ -145,7 +166,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
       for (int i = 0; i < 2; ++i) {
         const int hw = a_hw[part][i];
         const int h = (hw >> 16) + dh, w = ((int)(short)(hw & 0xffff)) + dw;
-        const bool ok = t < nk && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const bool ok = ta < kt1 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
         const uint32_t vo = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
         MI_ASSERT(vo == OOB || vo + 16u <= (uint32_t)a.a_bytes, vo);  // valid taps never rely on zero fill
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0, 0);
@@ -212,7 +233,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     vm_wait4();
     phase_barrier();
     issue(t + 2, 1, 1);
-    const bool more = t + 1 < nk;
+    const bool more = t + 1 < nkl;
     if (more) read_b(bn, t + 1, 0);
     mma(af, bc, 1, 0);
     if (more) read_a(af, t + 1, 0);
@@ -227,13 +248,45 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   // static priority for the second-dispatched half: the two waves sharing a SIMD stop running in
   // lockstep, so one's MFMAs overlap the other's LDS reads / barrier waits
   if (wid >= 4) __builtin_amdgcn_s_setprio(1);
-  for (int t = 0; t < nk; t += 2) {
+  for (int t = 0; t < nkl; t += 2) {
     ktile(t, bx, by);
-    if (t + 1 < nk) ktile(t + 1, by, bx);
+    if (t + 1 < nkl) ktile(t + 1, by, bx);
   }
   __builtin_amdgcn_s_setprio(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy loads of the tail still target LDS
   __syncthreads();
+
+  // ---- tail split-K: publish this split's partial; the last arriver of the tile reduces
+  if (tail_tile >= 0) {
+    // partial layout [acc index][thread] (16 B per thread): every store / load wave-instruction
+    // covers 1 KB contiguous.  One thread fences (device-scope release after the barrier, cumulative
+    // over the workgroup's stores) and counts arrivals; the last arriver acquires and reduces.
+    const size_t tile_f = (size_t)G_BM * G_BN;
+    f32x4* mine = (f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + split) * tile_f) + tid;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mine[(i * 4 + j) * 512] = acc[i][j];
+    __syncthreads();
+    int* flag = (int*)smem;  // LDS is free after the loop (no second __shared__ object)
+    if (tid == 0) {
+      __threadfence();
+      flag[0] = atomicAdd(a.counters + tail_tile, 1) == a.tail_split - 1;
+      if (flag[0]) __threadfence();
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    for (int q = 0; q < a.tail_split; ++q) {
+      if (q == split) continue;
+      const f32x4* other = (const f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + q) * tile_f) + tid;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += __builtin_nontemporal_load(other + (i * 4 + j) * 512);
+    }
+    if (tid == 0) a.counters[tail_tile] = 0;  // ready for the next launch (stream order)
+    __syncthreads();
+  }
 
   // ------------------------------------------------------------------ epilogue
   // lane holds D[n = 16j + 4fq + r][m = 16i + fr] of each 16x16 tile (weights-first MFMA)
@@ -527,6 +580,71 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
 
 }  // namespace
 
+// Tail split-K planning: with 1 block per CU, a grid of `tiles` runs in ceil(tiles / CUs) waves;
+// when the last wave is at most 3/4 full its tiles are split along K so it fills the chip.
+struct TailWs {
+  float* ws = nullptr;
+  size_t ws_floats = 0;
+  int* cnt = nullptr;
+  int cnt_n = 0;
+};
+static TailWs g_tail_ws[16];
+static int g_num_cus = 0;
+static int g_tail_split_env = -1;
+static int g_tail_min_kt = 12;
+
+MI_API void mi_set_tail_split(int on) { g_tail_split_env = on ? 1 : 0; }
+
+static hipError_t plan_tail(G256Args& a, int nk) {
+  if (g_num_cus == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+      g_num_cus = 256;
+    const char* e = std::getenv("MI355X_DP_TAIL_SPLIT");
+    g_tail_split_env = (e && e[0] == '0') ? 0 : 1;
+    if (const char* m = std::getenv("MI355X_DP_TAIL_MIN_KT")) g_tail_min_kt = std::max(1, std::atoi(m));
+  }
+  const int tiles = a.tiles_m * a.tiles_n;
+  const int full = (tiles / g_num_cus) * g_num_cus, tail = tiles - full;
+  int split = 1;
+  if (g_tail_split_env && tail > 0 && tail * 4 <= g_num_cus * 3) {
+    split = std::min(4, g_num_cus / tail);
+    // a split pays ~2 x 256 KB of fp32 partial traffic per tail tile: only worth it when every
+    // split still runs >= g_tail_min_kt k-tiles (ViT K=768 GEMMs measured slower when split)
+    while (split > 1 && nk / split < g_tail_min_kt) --split;
+  }
+  a.full_blocks = split > 1 ? full : tiles;
+  a.tail_split = split;
+  if (split <= 1) return hipSuccess;
+  int dev = 0;
+  hipGetDevice(&dev);
+  TailWs& w = g_tail_ws[dev & 15];
+  const size_t need = (size_t)tail * split * G_BM * G_BN;
+  if (w.ws_floats < need) {
+    if (w.ws) hipFree(w.ws);
+    hipError_t e = hipMalloc(&w.ws, need * sizeof(float));
+    if (e != hipSuccess) { w.ws = nullptr; w.ws_floats = 0; return e; }
+    w.ws_floats = need;
+  }
+  if (w.cnt_n < tail) {
+    if (w.cnt) hipFree(w.cnt);
+    hipError_t e = hipMalloc(&w.cnt, sizeof(int) * tail);
+    if (e != hipSuccess) { w.cnt = nullptr; w.cnt_n = 0; return e; }
+    hipMemset(w.cnt, 0, sizeof(int) * tail);
+    hipDeviceSynchronize();
+    w.cnt_n = tail;
+  }
+  a.ws = w.ws;
+  a.counters = w.cnt;
+  return hipSuccess;
+}
+
+static int grid_of(const G256Args& a) {
+  const int tiles = a.tiles_m * a.tiles_n;
+  return a.tail_split > 1 ? a.full_blocks + (tiles - a.full_blocks) * a.tail_split : tiles;
+}
+
 // Returns hipErrorInvalidValue when the shape is outside this kernel's contract (caller falls
 // back to the 128x128 kernel).
 MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bias, void* aux, int epi, int M, int N,
@@ -541,7 +659,8 @@ MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bia
   a.a_bytes = rsrc_bytes256((int64_t)M * lda);
   a.b_bytes = rsrc_bytes256((int64_t)N * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm256_nt_kernel<0>, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+  if (hipError_t e = plan_tail(a, cdiv(K, G_BK)); e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gemm256_nt_kernel<0>, dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -591,9 +710,10 @@ MI_API int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, floa
   a.a_bytes = rsrc_bytes256((int64_t)Nb * H * W * Cs);
   a.b_bytes = rsrc_bytes256((int64_t)N * a.K);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  if (hipError_t e = plan_tail(a, cdiv(a.K, G_BK)); e != hipSuccess) return (int)e;
   if (mode == 1)
-    hipLaunchKernelGGL(gemm256_nt_kernel<1>, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+    hipLaunchKernelGGL(gemm256_nt_kernel<1>, dim3(grid_of(a)), dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL(gemm256_nt_kernel<2>, dim3(a.tiles_m * a.tiles_n), dim3(512), 0, st, a);
+    hipLaunchKernelGGL(gemm256_nt_kernel<2>, dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
