@@ -22,7 +22,8 @@
 //     chunks queued back to back (MI355X_DP_SMDDP_CHUNK_MB) so a long bucket does not
 //     hold the comm stream in one monolithic kernel;
 //   * MI355X_DP_SMDDP_IPC=1: fp32 SUM/AVG all-reduces up to MI355X_DP_SMDDP_IPC_MB (default 4)
-//     take a one-shot path over IPC peer pointers instead of RCCL (latency-bound buckets,
+//     take a one-shot (<= MI355X_DP_SMDDP_IPC_ONESHOT_KB, default 256) or two-shot
+//     (reduce-scatter + all-gather) path over IPC peer pointers instead of RCCL (latency-bound buckets,
 //     SURVEY.md §2.3 N4): every rank exports one buffer (2 data slots + flags) through
 //     hipIpcGetMemHandle, handles travel through the c10d store, and the kernel
 //     (csrc/kernels/ipc_allreduce.hip, resolved from the kernel library) signals / waits on
@@ -186,13 +187,16 @@ class SmddpBackend : public c10d::Backend {
     const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
     void* h = lib ? dlopen(lib, RTLD_NOW | RTLD_GLOBAL) : nullptr;
     ipc_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce_f32") : nullptr;
-    if (!ipc_fn_ || size_ > 8) {
+    ipc2_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce2_f32") : nullptr;
+    auto flag_bytes = h ? (int64_t (*)())dlsym(h, "mi_ipc_flag_bytes") : nullptr;
+    if (!ipc_fn_ || !ipc2_fn_ || !flag_bytes || size_ > 8) {
       fprintf(stderr, "smddp: IPC all-reduce unavailable (kernel library %s); using RCCL only\n", lib ? lib : "unset");
       return;
     }
     if (const char* c = std::getenv("MI355X_DP_SMDDP_IPC_MB")) ipc_cap_ = (size_t)(atof(c) * (1 << 20));
     ipc_cap_ = (ipc_cap_ + 255) & ~(size_t)255;
-    const size_t bytes = 2 * ipc_cap_ + 4096;
+    if (const char* c = std::getenv("MI355X_DP_SMDDP_IPC_ONESHOT_KB")) ipc_oneshot_bytes_ = (size_t)(atof(c) * 1024);
+    const size_t bytes = 2 * ipc_cap_ + (size_t)flag_bytes();
     void* mine = nullptr;
     HIPCHECK(hipMalloc(&mine, bytes));
     HIPCHECK(hipMemset(mine, 0, bytes));
@@ -234,8 +238,11 @@ class SmddpBackend : public c10d::Backend {
       flags[q] = (uint32_t*)((char*)ipc_base_[q] + 2 * ipc_cap_);
     }
     HIPCHECK(hipMemcpyAsync((char*)ipc_base_[rank_] + slot, t.data_ptr(), t.numel() * 4, hipMemcpyDeviceToDevice, s));
-    const int rc = ipc_fn_(data, flags, rank_, size_, (float*)t.data_ptr(), t.numel(), epoch,
-                           avg ? 1.f / size_ : 1.f, ipc_err_dev_, ipc_spin_limit_, s);
+    // one-shot (one flag round, every peer's whole bucket read) for latency-bound sizes, two-shot
+    // (reduce-scatter + all-gather, 2/world of the bucket per link) above the threshold
+    IpcFn fn = (size_t)t.numel() * 4 <= ipc_oneshot_bytes_ ? ipc_fn_ : ipc2_fn_;
+    const int rc = fn(data, flags, rank_, size_, (float*)t.data_ptr(), t.numel(), epoch,
+                      avg ? 1.f / size_ : 1.f, ipc_err_dev_, ipc_spin_limit_, s);
     TORCH_CHECK(rc == 0, "smddp: IPC all-reduce launch failed with hipError ", rc);
   }
 
@@ -439,7 +446,9 @@ class SmddpBackend : public c10d::Backend {
   std::mutex init_mu_;
   bool ipc_on_ = false;
   IpcFn ipc_fn_ = nullptr;
+  IpcFn ipc2_fn_ = nullptr;
   size_t ipc_cap_ = 4u << 20;
+  size_t ipc_oneshot_bytes_ = 256u << 10;  // MI355X_DP_SMDDP_IPC_ONESHOT_KB
   std::vector<void*> ipc_base_;
   int* ipc_err_ = nullptr;      // host-mapped: the watchdog reads it without a device sync
   int* ipc_err_dev_ = nullptr;

@@ -896,9 +896,14 @@ MI_API void mi_set_gemm256(int on) { g_gemm256 = on ? 1 : 0; }
 // shapes with few output tiles (ViT: 9-36) stay on the 128x128 split-K kernel (L2 locality).
 extern "C" int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
                              hipStream_t st);
+static int g_tn256_min_tiles = -1;
 static bool use_gemm256_tn(int M, int N, int K) {
   use_gemm256(0, 0, 0);  // env init
-  return g_gemm256 && K >= 1024 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= 128;
+  if (g_tn256_min_tiles < 0) {
+    const char* e = std::getenv("MI355X_DP_TN256_MIN_TILES");
+    g_tn256_min_tiles = e ? std::max(1, std::atoi(e)) : 128;
+  }
+  return g_gemm256 && K >= 1024 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_tn256_min_tiles;
 }
 
 // Plain GEMM, "NT": C[M][N] = A[M][K] * B[N][K]^T (+bias[N]); A, B bf16; C bf16 or fp32.

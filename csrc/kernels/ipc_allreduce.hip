@@ -1,4 +1,4 @@
-// One-shot all-reduce over IPC peer pointers for latency-bound buckets (SURVEY.md §2.3 N4,
+// One-shot and two-shot all-reduce over IPC peer pointers (SURVEY.md §2.3 N4,
 // §5.8: "a one-shot IPC all-reduce kernel (peer-pointer loads) to cut latency").  Used by the
 // native smddp backend (csrc/comm/smddp_backend.cpp) for small fp32 all-reduces when
 // MI355X_DP_SMDDP_IPC=1; RCCL stays the path for everything else.
@@ -59,9 +59,146 @@ __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcPeers p, int rank
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two-shot (reduce-scatter + all-gather) variant for bandwidth-bound buckets: every rank reads
+// (world-1)/world of the data from peers twice instead of (world-1) x all of it once, so over 7
+// point-to-point xGMI links each link carries 2/world of the bucket instead of all of it.
+//   phase 1: wait for every peer's input flag (as above); block b sums chunk b of this rank's
+//            shard over all peers' slots and writes the scaled sum into its OWN slot (peers read
+//            this rank's slot only at their own shard range in phase 1, never at this one) and
+//            into `out`; then a system-scope release and flag2[rank][b] = epoch on every peer;
+//   phase 2: block b waits for flag2[q][b] from every peer and copies chunk b of shard q from
+//            peer q's slot into `out`.
+// Only blocks with the same index talk to each other (no grid barrier, no co-residency
+// assumption).  Reads of peer slots follow a system-scope acquire by thread 0 (L1/L2
+// invalidation for the CU / XCD) and use non-temporal loads.
+// Flag region per rank: [0, IPC_MAX_PEERS) input flags, then IPC_FLAG2_OFF + src * IPC_MAX_BLOCKS2 + b.
+constexpr int IPC_MAX_BLOCKS2 = 256;
+constexpr int IPC_FLAG2_OFF = 256;
+
+__device__ __forceinline__ bool ipc_wait_ge(uint32_t* f, uint32_t epoch, uint32_t spin_limit, uint32_t& spins) {
+  while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+    if (++spins > spin_limit) return false;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return true;
+}
+
+template <bool VEC>
+__device__ __forceinline__ void ipc_sum_chunk(const IpcPeers& p, int world, float* mine, float* out, int64_t lo,
+                                              int64_t hi, float scale) {
+  if constexpr (VEC) {
+    for (int64_t i = lo + 4 * (int64_t)threadIdx.x; i < hi; i += 4 * (int64_t)blockDim.x) {
+      f32x4 s = __builtin_nontemporal_load((const f32x4*)(p.data[0] + i));
+#pragma unroll 1
+      for (int q = 1; q < world; ++q) s += __builtin_nontemporal_load((const f32x4*)(p.data[q] + i));
+      s *= scale;
+      *(f32x4*)(mine + i) = s;
+      *(f32x4*)(out + i) = s;
+    }
+  } else {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      float s = 0.f;
+#pragma unroll 1
+      for (int q = 0; q < world; ++q) s += __builtin_nontemporal_load(p.data[q] + i);
+      mine[i] = s * scale;
+      out[i] = s * scale;
+    }
+  }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void ipc_copy_chunk(const float* src, float* out, int64_t lo, int64_t hi) {
+  if constexpr (VEC) {
+    for (int64_t i = lo + 4 * (int64_t)threadIdx.x; i < hi; i += 4 * (int64_t)blockDim.x)
+      *(f32x4*)(out + i) = __builtin_nontemporal_load((const f32x4*)(src + i));
+  } else {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = __builtin_nontemporal_load(src + i);
+  }
+}
+
+// shard = ceil(n / world) rounded up to 4 elements; chunk = ceil(shard / gridDim.x) rounded to 4
+template <bool VEC>
+__global__ __launch_bounds__(256) void ipc_allreduce2_kernel(IpcPeers p, int rank, int world, float* __restrict__ out,
+                                                             int64_t n, int64_t shard, int64_t chunk, uint32_t epoch,
+                                                             float scale, int* err, uint32_t spin_limit) {
+  __shared__ int ok;
+  const int b = blockIdx.x;
+  if (b == 0 && threadIdx.x < (unsigned)world) {
+    __threadfence_system();
+    __hip_atomic_store(p.flags[threadIdx.x] + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    bool good = true;
+    for (int q = 0; q < world && good; ++q) good = ipc_wait_ge(p.flags[rank] + q, epoch, spin_limit, spins);
+    if (!good) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ok = good;
+  }
+  __syncthreads();
+  if (!ok) return;
+  // phase 1: reduce chunk b of this rank's shard
+  {
+    const int64_t lo = min(n, rank * shard + b * chunk);
+    const int64_t hi = min(min(n, (rank + 1) * shard), lo + chunk);
+    ipc_sum_chunk<VEC>(p, world, (float*)p.data[rank], out, lo, hi, scale);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();  // this block's sums (in this XCD's L2) reach memory before the flags
+    for (int q = 0; q < world; ++q)
+      if (q != rank)
+        __hip_atomic_store(p.flags[q] + IPC_FLAG2_OFF + rank * IPC_MAX_BLOCKS2 + b, epoch, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t spins = 0;
+    bool good = true;
+    for (int q = 0; q < world && good; ++q)
+      if (q != rank) good = ipc_wait_ge(p.flags[rank] + IPC_FLAG2_OFF + q * IPC_MAX_BLOCKS2 + b, epoch, spin_limit, spins);
+    if (!good) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ok = good;
+  }
+  __syncthreads();
+  if (!ok) return;
+  // phase 2: gather chunk b of every other shard
+  for (int q = 0; q < world; ++q) {
+    if (q == rank) continue;
+    const int64_t lo = min(n, q * shard + b * chunk);
+    const int64_t hi = min(min(n, (q + 1) * shard), lo + chunk);
+    ipc_copy_chunk<VEC>(p.data[q], out, lo, hi);
+  }
+}
+
 }  // namespace
 
 MI_API int mi_ipc_max_peers() { return IPC_MAX_PEERS; }
+
+// bytes of flag words every rank's IPC buffer must provide after its two data slots
+MI_API int64_t mi_ipc_flag_bytes() { return (int64_t)(IPC_FLAG2_OFF + IPC_MAX_PEERS * IPC_MAX_BLOCKS2) * 4; }
+
+// Two-shot all-reduce; same arguments and slot / flag protocol as mi_ipc_allreduce_f32 (the
+// input flags are shared: a call is either one-shot or two-shot on every rank, by size).
+MI_API int mi_ipc_allreduce2_f32(const float* const* data, uint32_t* const* flags, int rank, int world, float* out,
+                                 int64_t n, uint32_t epoch, float scale, int* err, uint32_t spin_limit,
+                                 hipStream_t st) {
+  if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || n < 0) return (int)hipErrorInvalidValue;
+  IpcPeers p{};
+  bool vec = n % 4 == 0 && ((uintptr_t)out & 15) == 0;
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = data[q];
+    p.flags[q] = flags[q];
+    vec = vec && ((uintptr_t)data[q] & 15) == 0;
+  }
+  const int64_t shard = ((n + world - 1) / world + 3) & ~(int64_t)3;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(IPC_MAX_BLOCKS2, (shard + 2047) / 2048));
+  const int64_t chunk = ((shard + blocks - 1) / blocks + 3) & ~(int64_t)3;
+  if (vec)
+    hipLaunchKernelGGL(ipc_allreduce2_kernel<true>, dim3(blocks), dim3(256), 0, st, p, rank, world, out, n, shard,
+                       chunk, epoch, scale, err, spin_limit);
+  else
+    hipLaunchKernelGGL(ipc_allreduce2_kernel<false>, dim3(blocks), dim3(256), 0, st, p, rank, world, out, n, shard,
+                       chunk, epoch, scale, err, spin_limit);
+  return (int)hipGetLastError();
+}
 
 // data: per-rank pointer to THIS call's slot; flags: per-rank flag arrays; err: host-mapped int.
 MI_API int mi_ipc_allreduce_f32(const float* const* data, uint32_t* const* flags, int rank, int world, float* out,

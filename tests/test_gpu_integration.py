@@ -139,10 +139,12 @@ def test_notebook2_flow_example(tmp_path):
     assert next(iter(sd)) == "module.conv1.weight" and sd["module.fc.weight"].shape == (1000, 512)
 
 
-def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path):
-    """SURVEY N4 one-shot IPC all-reduce in the native smddp backend: 2 ranks sharing cuda:0
-    (IPC handles opened by the peer process), many back-to-back calls (slot parity reuse),
-    SUM and AVG, sizes up to the cap; RCCL is never initialised on this path."""
+@pytest.mark.parametrize("oneshot_kb", ["256", "0"])
+def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path, oneshot_kb):
+    """SURVEY N4 one-shot / two-shot IPC all-reduce in the native smddp backend: 2 ranks sharing
+    cuda:0 (IPC handles opened by the peer process), many back-to-back calls (slot parity reuse),
+    SUM and AVG, sizes up to the cap (vectorised and scalar two-shot paths); RCCL is never
+    initialised on this path.  oneshot_kb=256: small sizes one-shot, 4 MB two-shot; 0: all two-shot."""
     script = tmp_path / "ipc.py"
     script.write_text(
         "import os, sys, torch, torch.distributed as dist\n"
@@ -151,7 +153,7 @@ def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path):
         "dist.init_process_group(backend='smddp')\n"
         "r, w = dist.get_rank(), dist.get_world_size()\n"
         "for it in range(40):\n"
-        "    n = [1, 7, 1000, 65536, 1 << 20][it % 5]\n"
+        "    n = [1, 7, 1000, 65536, 1 << 20, 999999][it % 6]\n"
         "    t = torch.arange(n, device='cuda', dtype=torch.float32) * (r + 1) + it\n"
         "    op = dist.ReduceOp.AVG if it % 2 else dist.ReduceOp.SUM\n"
         "    dist.all_reduce(t, op=op)\n"
@@ -161,7 +163,8 @@ def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path):
         "    assert torch.allclose(t, ref, rtol=1e-6, atol=1e-3), (it, (t - ref).abs().max().item())\n"
         "torch.cuda.synchronize()\n"
         "print('IPC_OK', r, flush=True)\n")
-    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC": "1", "MI355X_DP_SMDDP_DEVICE": "0"}
+    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC": "1", "MI355X_DP_SMDDP_DEVICE": "0",
+           "MI355X_DP_SMDDP_IPC_ONESHOT_KB": oneshot_kb}
     r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2", str(script)], cwd=ROOT,
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
