@@ -46,9 +46,14 @@
 #include <chrono>
 #include <cstdlib>
 #include <deque>
+#include <memory>
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <exception>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
+#include <vector>
 
 namespace smddp {
 
@@ -91,36 +96,46 @@ static ncclRedOp_t to_nccl(const c10d::ReduceOp& op) {
   }
 }
 
+// Completion event of one collective, shared by the Work (user side) and the watchdog's pending
+// queue.  The watchdog only ever holds these -- never the Work -- so it never drops the last
+// reference to a Work's output tensors: releasing a tensor that has a Python object needs the GIL,
+// which a C++ thread cannot take while the interpreter is finalising (std::terminate at exit).
+struct DoneEvent {
+  hipEvent_t ev = nullptr;
+  std::chrono::steady_clock::time_point start;
+  explicit DoneEvent(hipStream_t s) {
+    HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHECK(hipEventRecord(ev, s));
+    start = std::chrono::steady_clock::now();
+  }
+  ~DoneEvent() { hipEventDestroy(ev); }
+};
+
 class SmddpWork : public c10d::Work {
  public:
   SmddpWork(int rank, c10d::OpType op, int device, HIPStreamMasqueradingAsCUDA comm, std::vector<at::Tensor> outputs,
             bool blocking)
       : c10d::Work(rank, op), device_(device), comm_(comm), outputs_(std::move(outputs)), blocking_(blocking) {
-    HIPCHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
-    HIPCHECK(hipEventRecord(done_, comm_.stream()));
-    start_ = std::chrono::steady_clock::now();
+    done_ = std::make_shared<DoneEvent>(comm_.stream());
     std::vector<c10::Device> devs{c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device)};
     future_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()), devs);
     c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_);
     future_->markCompleted(c10::IValue(outputs_));
   }
-  ~SmddpWork() override { hipEventDestroy(done_); }
-
-  bool isCompleted() override { return hipEventQuery(done_) == hipSuccess; }
+  bool isCompleted() override { return hipEventQuery(done_->ev) == hipSuccess; }
   bool isSuccess() const override { return true; }
 
   bool wait(std::chrono::milliseconds timeout) override {
     auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_);
-    HIPCHECK(hipStreamWaitEvent(cur.stream(), done_, 0));
-    if (blocking_) HIPCHECK(hipEventSynchronize(done_));
+    HIPCHECK(hipStreamWaitEvent(cur.stream(), done_->ev, 0));
+    if (blocking_) HIPCHECK(hipEventSynchronize(done_->ev));
     return true;
   }
   void synchronize() override { wait(kNoTimeout); }
   c10::intrusive_ptr<c10::ivalue::Future> getFuture() override { return future_; }
   std::vector<at::Tensor> result() override { return outputs_; }
 
-  std::chrono::steady_clock::time_point start_;
-  hipEvent_t done_;
+  std::shared_ptr<DoneEvent> done_;
 
  private:
   int device_;
@@ -129,6 +144,14 @@ class SmddpWork : public c10d::Work {
   bool blocking_;
   c10::intrusive_ptr<c10::ivalue::Future> future_;
 };
+
+class SmddpBackend;
+// Live backends: an atexit hook (registered after the HIP runtime initialised, so it runs before
+// the runtime's own static teardown) stops every watchdog thread of a process group the user never
+// destroyed, so no thread polls HIP events while the runtime is being torn down.
+static std::mutex g_live_mu;
+static std::vector<SmddpBackend*> g_live;
+static void stop_all_watchdogs();
 
 class SmddpBackend : public c10d::Backend {
  public:
@@ -153,11 +176,17 @@ class SmddpBackend : public c10d::Backend {
     if (ipc && ipc[0] == '1' && size > 1) setup_ipc();
     if (!ipc_on_) comm();  // eager RCCL bootstrap unless the IPC path may serve the first collectives
     watchdog_ = std::thread([this] { watchdog_loop(); });
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.push_back(this);
   }
 
   ~SmddpBackend() override {
-    stop_ = true;
-    if (watchdog_.joinable()) watchdog_.join();
+    {
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      for (auto& b : g_live)
+        if (b == this) b = nullptr;
+    }
+    stop_watchdog();
     hipEventDestroy(ready_);
     if (comm_) ncclCommDestroy(comm_);
     if (ipc_on_) {
@@ -178,6 +207,18 @@ class SmddpBackend : public c10d::Backend {
   }
 
   bool ipc_enabled() const { return ipc_on_; }
+
+  void stop_watchdog() {
+    stop_ = true;
+    if (watchdog_.joinable() && watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();
+  }
+
+  // dist.destroy_process_group(): drain this backend's work, stop the watchdog
+  void shutdown() override {
+    c10::hip::HIPGuardMasqueradingAsCUDA dg((c10::DeviceIndex)device_);
+    hipStreamSynchronize(comm_stream_.stream());
+    stop_watchdog();
+  }
 
  private:
   using IpcFn = int (*)(const float* const*, uint32_t* const*, int, int, float*, int64_t, uint32_t, float, int*,
@@ -266,7 +307,7 @@ class SmddpBackend : public c10d::Backend {
     auto w = c10::make_intrusive<SmddpWork>(rank_, op, device_, comm_stream_, std::move(outputs), blocking);
     {
       std::lock_guard<std::mutex> lk(mu_);
-      pending_.push_back(w);
+      pending_.push_back(w->done_);
     }
     return w;
   }
@@ -420,11 +461,11 @@ class SmddpBackend : public c10d::Backend {
       std::lock_guard<std::mutex> lk(mu_);
       while (!pending_.empty()) {
         auto& w = pending_.front();
-        if (hipEventQuery(w->done_) == hipSuccess) {
+        if (hipEventQuery(w->ev) == hipSuccess) {
           pending_.pop_front();
           continue;
         }
-        if (std::chrono::steady_clock::now() - w->start_ > timeout_) {
+        if (std::chrono::steady_clock::now() - w->start > timeout_) {
           fprintf(stderr, "smddp watchdog: rank %d collective did not complete within %lld ms; aborting\n", rank_,
                   (long long)timeout_.count());
           fflush(stderr);
@@ -457,14 +498,38 @@ class SmddpBackend : public c10d::Backend {
   hipEvent_t ready_;
   size_t chunk_bytes_ = 0;
   std::mutex mu_;
-  std::deque<c10::intrusive_ptr<SmddpWork>> pending_;
+  std::deque<std::shared_ptr<DoneEvent>> pending_;
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
 };
 
+static void stop_all_watchdogs() {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  for (auto* b : g_live)
+    if (b) b->stop_watchdog();
+}
+
+// Print where std::terminate came from (the process then aborts as before): the launcher's
+// abort-all report names the rank, this names the call site.
+static void terminate_with_backtrace() {
+  void* frames[48];
+  const int n = backtrace(frames, 48);
+  static const char msg[] = "smddp: std::terminate called; backtrace:\n";
+  ssize_t w = write(2, msg, sizeof(msg) - 1);
+  (void)w;
+  backtrace_symbols_fd(frames, n, 2);
+  std::abort();
+}
+
 c10::intrusive_ptr<c10d::Backend> create_backend(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size,
                                                  int device, double timeout_s) {
-  return c10::make_intrusive<SmddpBackend>(store, rank, size, device, timeout_s);
+  static std::once_flag once;
+  auto b = c10::make_intrusive<SmddpBackend>(store, rank, size, device, timeout_s);
+  std::call_once(once, [] {
+    std::atexit(stop_all_watchdogs);
+    if (std::getenv("MI355X_DP_SMDDP_TERMINATE_TRACE")) std::set_terminate(terminate_with_backtrace);
+  });
+  return b;
 }
 
 int rccl_version() {

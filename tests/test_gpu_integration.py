@@ -164,7 +164,7 @@ def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path, oneshot_kb):
         "torch.cuda.synchronize()\n"
         "print('IPC_OK', r, flush=True)\n")
     env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC": "1", "MI355X_DP_SMDDP_DEVICE": "0",
-           "MI355X_DP_SMDDP_IPC_ONESHOT_KB": oneshot_kb}
+           "MI355X_DP_SMDDP_IPC_ONESHOT_KB": oneshot_kb, "MI355X_DP_SMDDP_TERMINATE_TRACE": "1"}
     r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2", str(script)], cwd=ROOT,
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
