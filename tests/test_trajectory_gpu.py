@@ -1,0 +1,19 @@
+"""Training-trajectory parity: the engine's loss curve (native bf16 kernels, flat-buffer DP,
+fused FlatSGD) tracks stock PyTorch fp32 training from the same init on the same batch
+(tools/loss_parity.py; the ResNet-50 curves are in profiles/loss_parity_rn50.md)."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def test_training_trajectory_matches_stock_fp32():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import loss_parity
+    ours, ref, _ = loss_parity.run("resnet18", batch=32, size=64, classes=10, steps=12, lr=0.02)
+    for i, (o, r) in enumerate(zip(ours, ref)):
+        assert abs(o - r) <= 0.05 * abs(r) + 0.02, (i, ours, ref)
+    assert ours[-1] < 0.7 * ours[0], ours  # it learns the batch
