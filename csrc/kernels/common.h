@@ -59,6 +59,12 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// streaming 16-byte load (nontemporal: read once, do not keep in the caches)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const void* base, int64_t v) {
+  return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)base + v));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -66,6 +66,26 @@ struct G256Args {
   int* counters;
 };
 
+// Wave priority (A/B knob, MI_G256_PRIO): 0 none; 1 static s_setprio 1 for the second-dispatched
+// half (waves 4-7) before the main loop -- the guard must be provably wave-uniform
+// (readfirstlane), a plain `if (wid >= 4)` lowers to s_and_saveexec + an UNCONDITIONAL
+// s_setprio, i.e. every wave at priority 1; 2 per-MFMA-cluster setprio(1)/(0) flips (keeps hipcc
+// from moving the cluster's MFMAs across the phase's loads / barriers).
+#ifndef MI_G256_PRIO
+#define MI_G256_PRIO 1
+#endif
+__device__ __forceinline__ void static_prio() {
+#if MI_G256_PRIO == 1
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+}
+template <int P>
+__device__ __forceinline__ void cluster_prio() {
+#if MI_G256_PRIO == 2
+  __builtin_amdgcn_s_setprio(P);
+#endif
+}
+
 __device__ __forceinline__ void vm_wait6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
 __device__ __forceinline__ void vm_wait4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -201,6 +221,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         f[j][kk] = __builtin_bit_cast(bf16x8, src[(wn * 32 + j * 16 + fr) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
   };
   auto mma = [&](const bf16x8 (&af_)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
+    cluster_prio<1>();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -209,6 +230,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af_[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
+    cluster_prio<0>();
   };
 
   // One k-tile = 4 quadrant phases:
@@ -247,7 +269,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   read_b(bx, 0, 0);
   // static priority for the second-dispatched half: the two waves sharing a SIMD stop running in
   // lockstep, so one's MFMAs overlap the other's LDS reads / barrier waits
-  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  static_prio();
   for (int t = 0; t < nkl; t += 2) {
     ktile(t, bx, by);
     if (t + 1 < nkl) ktile(t + 1, by, bx);
@@ -512,6 +534,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
       for (int kk = 0; kk < 2; ++kk) f[j][kk] = tr_frag(src, (wn >> 1) * 64 + (wn & 1) * 32 + j * 16, kk);
   };
   auto mma = [&](const bf16x8 (&af_)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
+    cluster_prio<1>();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -520,6 +543,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af_[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
+    cluster_prio<0>();
   };
   auto ktile = [&](int t, bf16x8 (&bc)[2][2], bf16x8 (&bn)[2][2]) {
     issue(t + 1, 1, 0);
@@ -546,7 +570,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
   phase_barrier();
   read_a(af, 0, 0);
   read_b(bx, 0, 0);
-  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  static_prio();
   for (int t = 0; t < nk; t += 2) {
     ktile(t, bx, by);
     if (t + 1 < nk) ktile(t + 1, by, bx);

@@ -602,6 +602,44 @@ __global__ void wtrans_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__
   }
 }
 
+// All conv weights of a flat bf16 parameter buffer in ONE launch (after the optimizer step):
+// desc[t] = {src element offset, dst element offset, K, RS, C, first block}; every 64x64 (k, c)
+// tile of every tap is one block; a block finds its tensor by binary search over first-block.
+// Replaces one mi_conv_wtrans launch per conv per backward (52 for ResNet-50).
+struct WtDesc {
+  int src, dst, K, RS, C, blk0;
+};
+__global__ void wtrans_multi_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                    const WtDesc* __restrict__ desc, int ntens) {
+  __shared__ bf16_t t[64][65];
+  const int b = blockIdx.x;
+  int lo = 0, hi = ntens - 1;
+  while (lo < hi) {  // last tensor with blk0 <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WtDesc d = desc[lo];
+  const int nc = (d.C + 63) >> 6, nkb = (d.K + 63) >> 6;
+  int r0 = b - d.blk0;
+  const int cx = r0 % nc;
+  r0 /= nc;
+  const int ky = r0 % nkb;
+  const int tap = r0 / nkb;
+  const int k0 = ky * 64, c0 = cx * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const bf16_t* src = w + d.src;
+  bf16_t* dst = wt + d.dst;
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + tx;
+    t[r][tx] = (k < d.K && c < d.C) ? src[((size_t)k * d.RS + tap) * d.C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + tx;
+    if (c < d.C && k < d.K) dst[((size_t)c * d.RS + tap) * d.K + k] = t[tx][r];
+  }
+}
+
 // byte extent for a buffer resource; 0 (= use the register-staged path) beyond 2 GiB
 static int rsrc_bytes(int64_t elems) {
   const int64_t b = elems * 2;
@@ -874,6 +912,14 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
 MI_API int mi_conv_wtrans(const void* w, void* wt, int K, int RS, int C, hipStream_t st) {
   dim3 grid(cdiv(C, 64), cdiv(K, 64), RS);
   hipLaunchKernelGGL(wtrans_kernel, grid, dim3(256), 0, st, (const bf16_t*)w, (bf16_t*)wt, K, RS, C);
+  return (int)hipGetLastError();
+}
+
+// desc: device int32 [ntens][6] (WtDesc); nblocks = sum over tensors of RS * cdiv(K,64) * cdiv(C,64)
+MI_API int mi_conv_wtrans_multi(const void* w, void* wt, const void* desc, int ntens, int nblocks, hipStream_t st) {
+  if (ntens <= 0 || nblocks <= 0) return 0;
+  hipLaunchKernelGGL(wtrans_multi_kernel, dim3(nblocks), dim3(256), 0, st, (const bf16_t*)w, (bf16_t*)wt,
+                     (const WtDesc*)desc, ntens);
   return (int)hipGetLastError();
 }
 

@@ -157,29 +157,66 @@ __global__ void bn_eval_coeffs_kernel(int C, float eps, const float* __restrict_
   shift[c] = bt - rmean[c] * gm * invstd;
 }
 
+// Elementwise passes are HBM-bound: each thread keeps EW_U 16-byte vectors (EW_U x grid stride
+// apart, so every wave-instruction stays 1 KB contiguous) in flight before using any, instead of
+// one load -> use -> store chain per iteration.  Channel of vector v: (8 v) mod C, advanced
+// incrementally by the (uniform) stride's channel step.
+constexpr int EW_U = 4;
+
+struct EwIter {
+  int64_t v0, stride;
+  int c0, cstep;
+  __device__ EwIter(int64_t nvec, int C) {
+    stride = (int64_t)gridDim.x * NT;
+    v0 = blockIdx.x * (int64_t)NT + threadIdx.x;
+    cstep = (int)((stride * 8) % C);
+    c0 = (int)((v0 * 8) % C);
+  }
+  __device__ __forceinline__ int chan(int c, int C) const { return c + cstep >= C ? c + cstep - C : c + cstep; }
+  __device__ __forceinline__ void next(int C) {
+    v0 += stride * EW_U;
+    c0 = (int)((v0 * 8) % C);
+  }
+};
+
 // y = act(x*scale + shift (+ res)); grid-stride over 8-element vectors
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       bf16_t* __restrict__ y, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, int64_t nvec, int C, int relu) {
-  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
-    const int c = (int)((v * 8) % C);
-    float f[8];
-    unpack8(((const uint4*)x)[v], f);
-    const float4 a0 = *(const float4*)(scale + c), a1 = *(const float4*)(scale + c + 4);
-    const float4 b0 = *(const float4*)(shift + c), b1 = *(const float4*)(shift + c + 4);
-    f[0] = f[0] * a0.x + b0.x; f[1] = f[1] * a0.y + b0.y; f[2] = f[2] * a0.z + b0.z; f[3] = f[3] * a0.w + b0.w;
-    f[4] = f[4] * a1.x + b1.x; f[5] = f[5] * a1.y + b1.y; f[6] = f[6] * a1.z + b1.z; f[7] = f[7] * a1.w + b1.w;
-    if (res) {
-      float r[8];
-      unpack8(((const uint4*)res)[v], r);
+  for (EwIter it(nvec, C); it.v0 < nvec; it.next(C)) {
+    uint4 xv[EW_U], rv[EW_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += r[j];
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = it.v0 + u * it.stride;
+      if (v < nvec) {
+        xv[u] = ld_nt16(x, v);
+        if (res) rv[u] = ld_nt16(res, v);
+      }
     }
-    if (relu) {
+    int c = it.c0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = it.v0 + u * it.stride;
+      if (v >= nvec) break;
+      float f[8];
+      unpack8(xv[u], f);
+      const float4 a0 = *(const float4*)(scale + c), a1 = *(const float4*)(scale + c + 4);
+      const float4 b0 = *(const float4*)(shift + c), b1 = *(const float4*)(shift + c + 4);
+      f[0] = f[0] * a0.x + b0.x; f[1] = f[1] * a0.y + b0.y; f[2] = f[2] * a0.z + b0.z; f[3] = f[3] * a0.w + b0.w;
+      f[4] = f[4] * a1.x + b1.x; f[5] = f[5] * a1.y + b1.y; f[6] = f[6] * a1.z + b1.z; f[7] = f[7] * a1.w + b1.w;
+      if (res) {
+        float r[8];
+        unpack8(rv[u], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += r[j];
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      }
+      ((uint4*)y)[v] = pack8(f);
+      c = it.chan(c, C);
     }
-    ((uint4*)y)[v] = pack8(f);
   }
 }
 
@@ -242,25 +279,41 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
                                                           int64_t nvec, int C, int relu) {
-  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
-    const int c = (int)((v * 8) % C);
-    float d[8], xv[8];
-    unpack8(((const uint4*)dy)[v], d);
-    unpack8(((const uint4*)x)[v], xv);
-    if (relu) {
-      float yv[8];
-      unpack8(((const uint4*)y)[v], yv);
+  for (EwIter it(nvec, C); it.v0 < nvec; it.next(C)) {
+    uint4 dv[EW_U], xq[EW_U], yq[EW_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = it.v0 + u * it.stride;
+      if (v < nvec) {
+        dv[u] = ld_nt16(dy, v);
+        xq[u] = ld_nt16(x, v);
+        if (relu) yq[u] = ld_nt16(y, v);
+      }
     }
-    if (dres) ((uint4*)dres)[v] = pack8(d);
-    float k0[8], k1[8], k2[8], o[8];
-    *(float4*)&k0[0] = *(const float4*)(coef + c); *(float4*)&k0[4] = *(const float4*)(coef + c + 4);
-    *(float4*)&k1[0] = *(const float4*)(coef + C + c); *(float4*)&k1[4] = *(const float4*)(coef + C + c + 4);
-    *(float4*)&k2[0] = *(const float4*)(coef + 2 * C + c); *(float4*)&k2[4] = *(const float4*)(coef + 2 * C + c + 4);
+    int c = it.c0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = k0[j] * d[j] + k1[j] * xv[j] + k2[j];
-    ((uint4*)dx)[v] = pack8(o);
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = it.v0 + u * it.stride;
+      if (v >= nvec) break;
+      float d[8], xv[8];
+      unpack8(dv[u], d);
+      unpack8(xq[u], xv);
+      if (relu) {
+        float yv[8];
+        unpack8(yq[u], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      }
+      if (dres) ((uint4*)dres)[v] = pack8(d);
+      float k0[8], k1[8], k2[8], o[8];
+      *(float4*)&k0[0] = *(const float4*)(coef + c); *(float4*)&k0[4] = *(const float4*)(coef + c + 4);
+      *(float4*)&k1[0] = *(const float4*)(coef + C + c); *(float4*)&k1[4] = *(const float4*)(coef + C + c + 4);
+      *(float4*)&k2[0] = *(const float4*)(coef + 2 * C + c); *(float4*)&k2[4] = *(const float4*)(coef + 2 * C + c + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = k0[j] * d[j] + k1[j] * xv[j] + k2[j];
+      ((uint4*)dx)[v] = pack8(o);
+      c = it.chan(c, C);
+    }
   }
 }
 
@@ -288,7 +341,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const bf16_t* __restric
 }
 
 inline int ew_grid(int64_t nvec) {
-  int64_t g = (nvec + NT - 1) / NT;
+  int64_t g = (nvec + NT * EW_U - 1) / (NT * EW_U);
   return (int)(g < 4096 ? g : 4096);
 }
 

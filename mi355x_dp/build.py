@@ -43,13 +43,16 @@ def _digest(paths, extra=""):
     return h.hexdigest()
 
 
-def build_kernels(force=False, verbose=True, debug=False):
+def build_kernels(force=False, verbose=True, debug=False, variant=None, defines=()):
     """debug=True: libmi355x_kernels_debug.so with -DMI_DEBUG (device-side bounds asserts that
-    printf the failing index and trap), selected at run time by MI355X_DP_DEBUG_KERNELS=1."""
+    printf the failing index and trap), selected at run time by MI355X_DP_DEBUG_KERNELS=1.
+    variant="x", defines=("MI_FOO=1",): an A/B build libmi355x_kernels_x.so with extra -D flags,
+    selected at run time by MI355X_DP_KERNEL_VARIANT=x (same process, same shapes, one knob)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    flags = HIP_FLAGS + (["-DMI_DEBUG", "-g"] if debug else [])
-    out = os.path.join(NATIVE, "libmi355x_kernels_debug.so" if debug else "libmi355x_kernels.so")
+    flags = HIP_FLAGS + (["-DMI_DEBUG", "-g"] if debug else []) + [f"-D{d}" for d in defines]
+    tag = "debug" if debug else variant
+    out = os.path.join(NATIVE, f"libmi355x_kernels_{tag}.so" if tag else "libmi355x_kernels.so")
     stamp = out + ".sha256"
     dig = _digest(srcs + hdrs, " ".join(flags))
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == dig:
@@ -61,7 +64,7 @@ def build_kernels(force=False, verbose=True, debug=False):
     objs = []
 
     def one(src):
-        obj = os.path.join(BUILD, "kernels", os.path.basename(src) + (".dbg.o" if debug else ".o"))
+        obj = os.path.join(BUILD, "kernels", os.path.basename(src) + (f".{tag}.o" if tag else ".o"))
         _run([HIPCC, *flags, "-c", src, "-o", obj])
         return obj
 

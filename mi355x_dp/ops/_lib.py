@@ -26,6 +26,8 @@ KERNEL_LIB = os.path.join(NATIVE_DIR, "libmi355x_kernels.so")
 # asynchronous device fault is reported against the kernel that caused it.
 if os.environ.get("MI355X_DP_DEBUG_KERNELS") == "1":
     KERNEL_LIB = os.path.join(NATIVE_DIR, "libmi355x_kernels_debug.so")
+elif os.environ.get("MI355X_DP_KERNEL_VARIANT"):  # A/B builds: mi355x_dp.build.build_kernels(variant=...)
+    KERNEL_LIB = os.path.join(NATIVE_DIR, f"libmi355x_kernels_{os.environ['MI355X_DP_KERNEL_VARIANT']}.so")
 SYNC_CHECK = os.environ.get("MI355X_DP_SYNC_CHECK") == "1"
 
 _lock = threading.Lock()

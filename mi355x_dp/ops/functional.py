@@ -48,6 +48,19 @@ def weight_bf16(w: torch.Tensor) -> torch.Tensor:
         return w.detach().to(BF16).contiguous()
 
 
+def weight_bf16_t(w: torch.Tensor) -> torch.Tensor:
+    """Conv-dgrad operand [C][R][S][K] (bf16) of a [K, C, R, S] conv weight: the flat engine's
+    transposed copy (refreshed once per optimizer step for every conv) or a fresh transpose."""
+    wt = getattr(w, "_mi_bf16_t", None)
+    if wt is not None:
+        return wt
+    K, C, R, S = w.shape
+    w16 = weight_bf16(w)
+    wt = torch.empty((C, R, S, K), dtype=BF16, device=w.device)
+    _lib.call("mi_conv_wtrans", ptr(w16), ptr(wt), K, R * S, C, stream_of(w16))
+    return wt
+
+
 def _flat(p) -> bool:
     return p is not None and getattr(p, "_mi_flat", False) and p.grad is not None
 
@@ -149,8 +162,7 @@ class _Conv2d(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if ctx.mode != "direct":
                 raise NotImplementedError("input gradient of a small-channel (stem) convolution")
-            wt = torch.empty((C, R, S, K), dtype=BF16, device=dy.device)
-            _lib.call("mi_conv_wtrans", ptr(w16), ptr(wt), K, R * S, C, st)
+            wt = weight_bf16_t(weight)
             dx = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
             _lib.call("mi_conv2d_dgrad", ptr(dy), ptr(wt), ptr(dx), N, H, W, C, K, R, S, stride, padding, P, Q, st)
         if ctx.needs_input_grad[1]:

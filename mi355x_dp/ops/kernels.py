@@ -15,6 +15,7 @@ signature("mi_set_nt_stages", I)
 signature("mi_conv2d_dgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_wgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv_wtrans", P, P, I, I, I, P)
+signature("mi_conv_wtrans_multi", P, P, P, I, I, P)
 signature("mi_gemm_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, P)
 signature("mi_gemm_tn", P, P, P, I, I, I, I, I, I, P)
 

@@ -33,7 +33,7 @@ import torch
 from . import _lib
 from . import kernels as _k  # noqa: F401
 from ._lib import ptr, stream_of
-from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, weight_bf16
+from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, weight_bf16, weight_bf16_t
 
 F32 = torch.float32
 EPI_ACCUM, EPI_BN_BWD, EPI_ACCUM_BN_BWD = 3, 4, 5
@@ -114,10 +114,8 @@ def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0
     N, C, H, W = x_shape
     K, _, R, S = spec.w.shape
     P, Q = dy.shape[2], dy.shape[3]
-    w16 = weight_bf16(spec.w)
-    wt = torch.empty((C, R, S, K), dtype=BF16, device=dy.device)
     st = stream_of(dy)
-    _lib.call("mi_conv_wtrans", ptr(w16), ptr(wt), K, R * S, C, st)
+    wt = weight_bf16_t(spec.w)
     _lib.call("mi_conv2d_dgrad_ex", ptr(dy), ptr(wt), ptr(out), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
               int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), st)
     return out

@@ -135,6 +135,9 @@ class DataParallel(nn.Module):
             if self.buffers.buffers:
                 dist.broadcast(self.buffers.data, 0, group=process_group)
             self.flat.refresh_bf16()
+        # a state_dict loaded into the wrapped model (checkpoint resume) writes the fp32 masters in
+        # place; the bf16 compute copy and the transposed dgrad copies follow it
+        module.register_load_state_dict_post_hook(lambda _m, _keys: self.flat.refresh_bf16())
         self._reset()
 
     @property
@@ -250,6 +253,7 @@ class FlatSGD:
         f = self.engine.flat
         sgd_flat_(f.data, f.grad, self.momentum_buf, f.bf16, g["lr"], g["momentum"], g["dampening"],
                   g["weight_decay"], g["nesterov"], first_step=(self.steps == 0), grad_scale=self.engine.grad_scale)
+        f.refresh_transposed()  # dgrad operands of every conv, one launch
         self.steps += 1
 
     def state_dict(self):

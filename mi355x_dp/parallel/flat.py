@@ -74,6 +74,43 @@ class FlatParams:
             if self.bf16 is not None:
                 from mi355x_dp.ops.functional import cast_bf16_
                 cast_bf16_(self.data, self.bf16)
+        self._init_transposed()
+
+    def _init_transposed(self):
+        """Conv-dgrad operands: every kernel-layout conv weight [K][R][S][C] also kept transposed as
+        [C][R][S][K] in a second bf16 buffer (same offsets), rebuilt for ALL convs by ONE kernel
+        launch whenever the bf16 copy changes (``refresh_transposed``), instead of one transpose
+        per conv per backward.  Attached as ``p._mi_bf16_t``; GPU + native kernels only."""
+        self.bf16_t = None
+        if self.bf16 is None or self.device.type != "cuda":
+            return
+        from mi355x_dp.ops import _lib
+        if _lib.load(required=False) is None:
+            return
+        desc, blk = [], 0
+        for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
+            if p.dim() != 4 or not kl:
+                continue
+            K, C, R, S = p.shape
+            desc.append([o, o, K, R * S, C, blk])
+            blk += R * S * ((K + 63) // 64) * ((C + 63) // 64)
+        if not desc:
+            return
+        self.bf16_t = torch.zeros_like(self.bf16)
+        self._wt_desc = torch.tensor(desc, dtype=torch.int32, device=self.device)
+        self._wt_blocks = blk
+        for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
+            if p.dim() == 4 and kl:
+                K, C, R, S = p.shape
+                p._mi_bf16_t = self.bf16_t[o:o + p.numel()].view(C, R, S, K)
+        self.refresh_transposed()
+
+    def refresh_transposed(self):
+        if getattr(self, "bf16_t", None) is None:
+            return
+        from mi355x_dp.ops._lib import call, ptr, stream_of
+        call("mi_conv_wtrans_multi", ptr(self.bf16), ptr(self.bf16_t), ptr(self._wt_desc), len(self._wt_desc),
+             self._wt_blocks, stream_of(self.bf16))
 
     def param_range(self, i: int):
         p = self.params[i]
@@ -86,6 +123,7 @@ class FlatParams:
         if self.bf16 is not None:
             from mi355x_dp.ops.functional import cast_bf16_
             cast_bf16_(self.data, self.bf16)
+            self.refresh_transposed()
 
     def reattach_grads(self):
         """Re-point .grad at the flat views (after user code set them to None)."""

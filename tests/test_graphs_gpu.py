@@ -31,6 +31,8 @@ def test_graphed_step_matches_eager():
     core()                                   # eager first step (optimizer first-step semantics)
     gs = GraphedStep(core, warmup=1)         # one more eager step on a side stream, then capture
     state = [eng.flat.data, eng.flat.bf16, opt.momentum_buf, eng.buffers.data]
+    if eng.flat.bf16_t is not None:  # transposed dgrad copies of the conv weights
+        state.append(eng.flat.bf16_t)
     snap = [t.clone() for t in state]
 
     augment(imgs, 8, mean, std, pad=4, flip=True, seed=7, out=x)

@@ -265,3 +265,32 @@ def test_checksum_deterministic():
     assert len(set(a)) == 1, a                      # bit-identical run to run (replica checks rely on it)
     ref = float((x.double().cpu() * ((torch.arange(x.numel(), dtype=torch.float64) % 7) + 1)).sum())
     assert a[0] == pytest.approx(ref, rel=1e-9, abs=1e-6)
+
+
+def test_flat_transposed_conv_weights_follow_sgd():
+    """The engine's [C][R][S][K] dgrad copies (one wtrans_multi launch for every conv) equal a
+    transpose of the bf16 compute copy after construction, after an optimizer step and after a
+    state_dict load."""
+    from mi355x_dp.models import get_model
+    from mi355x_dp.parallel import DataParallel, FlatSGD
+    eng = DataParallel(get_model("resnet50", num_classes=10).cuda())
+    opt = FlatSGD(eng, lr=0.5, momentum=0.9)
+
+    def check():
+        n = 0
+        for p in eng.flat.params:
+            wt = getattr(p, "_mi_bf16_t", None)
+            if wt is None:
+                continue
+            ref = p._mi_bf16.permute(1, 2, 3, 0)  # [K,C,R,S] view of [K][R][S][C] -> [C,R,S,K]
+            assert torch.equal(wt, ref.contiguous()), tuple(p.shape)
+            n += 1
+        assert n == 53  # every ResNet-50 conv
+    check()
+    eng.flat.grad.normal_()
+    opt.step()
+    torch.cuda.synchronize()
+    check()
+    sd = {k: v.clone() * 0.5 for k, v in eng.module.state_dict().items()}
+    eng.module.load_state_dict(sd)
+    check()
