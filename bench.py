@@ -58,8 +58,11 @@ def main():
     if world != args.gpus:
         if rank == 0:
             print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one rank per GPU; more ranks than GPUs share them (gloo rehearsal of the multi-rank path on a
+    # 1-GPU box -- RCCL itself refuses two ranks on one device)
+    gpu = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         if args.backend == "smddp":
             import smdistributed.dataparallel.torch.torch_smddp  # noqa: F401  (registers 'smddp')

@@ -8,8 +8,9 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return 0.5f * (1.f + erff(x * 0.70710678f)) + x * 0.39894228f * __expf(-0.5f * x * x);
 }
 
-// elementwise op on one 16-byte chunk (8 bf16) of the bf16 epilogue; aux has C's layout
-__device__ __forceinline__ uint4 epilogue_op(int epi, uint4 v, bf16_t* aux) {
+// elementwise op on one 16-byte chunk (8 bf16) of the bf16 epilogue; aux has C's layout.
+// epi 2 / 3 read aux: callers that batch their loads pass the chunk already loaded (aux_v).
+__device__ __forceinline__ uint4 epilogue_op_v(int epi, uint4 v, bf16_t* aux, uint4 aux_v) {
   float f[8];
   unpack8(v, f);
   if (epi == 1) {
@@ -18,7 +19,7 @@ __device__ __forceinline__ uint4 epilogue_op(int epi, uint4 v, bf16_t* aux) {
     for (int q = 0; q < 8; ++q) f[q] = gelu_f(f[q]);
   } else {
     float g[8];
-    unpack8(*(const uint4*)aux, g);
+    unpack8(aux_v, g);
     if (epi == 2) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) f[q] *= gelu_grad_f(g[q]);
@@ -28,4 +29,8 @@ __device__ __forceinline__ uint4 epilogue_op(int epi, uint4 v, bf16_t* aux) {
     }
   }
   return pack8(f);
+}
+
+__device__ __forceinline__ uint4 epilogue_op(int epi, uint4 v, bf16_t* aux) {
+  return epilogue_op_v(epi, v, aux, epi == 1 ? v : *(const uint4*)aux);
 }

@@ -360,13 +360,35 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
             make_uint2(pack2bf(v[0] + bv[j][0], v[1] + bv[j][1]), pack2bf(v[2] + bv[j][2], v[3] + bv[j][3]));
       }
     lgkm_wait0();
+    // 8 row steps in 2 groups of EPI_U: a group's global operand loads (residual C, relu source,
+    // BN input) are all issued before its first store, so their HBM latency overlaps instead of
+    // serialising behind each step's store (the compiler cannot move a load across a store to C)
+    constexpr int EPI_U = 4;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int rl = s * 8 + (lane >> 3);
-      const int m = m0 + wm * 128 + mq * 64 + rl;
-      const uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
-      if (m < a.M && n < a.N) {
-        const size_t off = (size_t)m * a.ldc + n;
+    for (int s0 = 0; s0 < 8; s0 += EPI_U) {
+      uint4 cv[EPI_U], yq[EPI_U], xq[EPI_U];
+      size_t offs[EPI_U];
+      bool ok[EPI_U];
+#pragma unroll
+      for (int u = 0; u < EPI_U; ++u) {
+        const int rl = (s0 + u) * 8 + (lane >> 3);
+        const int m = m0 + wm * 128 + mq * 64 + rl;
+        ok[u] = m < a.M && n < a.N;
+        offs[u] = ok[u] ? (size_t)m * a.ldc + n : 0;
+        if (ok[u] && a.epi >= 4) {
+          if (a.epi == 5) cv[u] = *(const uint4*)((const bf16_t*)a.C + offs[u]);
+          if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
+          if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
+        } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
+          yq[u] = *(const uint4*)(a.aux + offs[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EPI_U; ++u) {
+        const int rl = (s0 + u) * 8 + (lane >> 3);
+        const uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
+        if (!ok[u]) continue;
+        const size_t off = offs[u];
         MI_ASSERT(n + 8 <= a.N, n);
         uint4 o = v;
         if (a.epi >= 4) {
@@ -374,25 +396,25 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
           unpack8(v, f);
           if (a.epi == 5) {  // dy = this dgrad + the gradient already in C (residual sum)
             float c0[8];
-            unpack8(*(const uint4*)((const bf16_t*)a.C + off), c0);
+            unpack8(cv[u], c0);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] += c0[q];
           }
           if (a.bn_relu) {
             float yv[8];
-            unpack8(*(const uint4*)(a.aux + off), yv);
+            unpack8(yq[u], yv);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] = yv[q] > 0.f ? f[q] : 0.f;
           }
           o = pack8(f);
           if (a.stats) {
             float xv[8];
-            unpack8(*(const uint4*)(a.aux2 + off), xv);
+            unpack8(xq[u], xv);
 #pragma unroll
             for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * (xv[q] - mu[q]); }
           }
         } else {
-          if (a.epi) o = epilogue_op(a.epi, v, a.aux + off);
+          if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[u]);
           if (a.stats) {
             float f[8];
             unpack8(v, f);

@@ -341,41 +341,68 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
   const int cc = tid % CPR, rr = tid / CPR;
   const int n = n0 + cc * 8;
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int ml = rr; ml < BM; ml += RPP) {
-    const int m = m0 + ml;
-    if (m >= Mrows) break;
-    const uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
-    if (n < a.N) {
-      const size_t off = row_off(m) + n;
+  float mu[8];
+  if (a.epi >= 4 && a.stats && n < a.N) {
+    *(float4*)&mu[0] = *(const float4*)(a.mean + n);
+    *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
+  }
+  // row steps in groups of EU: a group's global operand loads (residual C, relu source, BN input,
+  // epilogue aux) are all issued before its first store, so their latency overlaps instead of
+  // serialising behind each step's store (the compiler cannot move a load across a store to C)
+  constexpr int NSTEP = BM / RPP;
+  constexpr int EU = NSTEP < 4 ? NSTEP : 4;
+#pragma unroll
+  for (int s0 = 0; s0 < NSTEP; s0 += EU) {
+    uint4 cv[EU], yq[EU], xq[EU];
+    size_t offs[EU];
+    bool ok[EU];
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      const int m = m0 + rr + (s0 + u) * RPP;
+      ok[u] = m < Mrows && n < a.N;
+      offs[u] = ok[u] ? row_off(m) + n : 0;
+      if (ok[u] && a.epi >= 4) {
+        if (a.epi == 5) cv[u] = *(const uint4*)((const bf16_t*)a.C + offs[u]);
+        if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
+        if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
+      } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
+        yq[u] = *(const uint4*)(a.aux + offs[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      if (!ok[u]) continue;
+      const int ml = rr + (s0 + u) * RPP;
+      const uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
+      const size_t off = offs[u];
       MI_ASSERT(off + 8 <= (size_t)(a.mode == 3 ? a.M : Mrows) * a.ldc, (long long)off);
       uint4 o = v;
       if (a.epi >= 4) {
         // BN backward: dz = dy * relu mask; stats (sum dz, sum dz * (x - mean)) of the rounded dz
         // (epi 5: dy = this dgrad + the gradient already in C -- a block input's residual sum)
-        float f[8], xv[8], mu[8];
+        float f[8];
         unpack8(v, f);
         if (a.epi == 5) {
           float c0[8];
-          unpack8(*(const uint4*)((const bf16_t*)a.C + off), c0);
+          unpack8(cv[u], c0);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += c0[q];
         }
         if (a.bn_relu) {
           float yv[8];
-          unpack8(*(const uint4*)(a.aux + off), yv);
+          unpack8(yq[u], yv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] = yv[q] > 0.f ? f[q] : 0.f;
         }
         o = pack8(f);
         if (a.stats) {
-          unpack8(*(const uint4*)(a.aux2 + off), xv);
-          *(float4*)&mu[0] = *(const float4*)(a.mean + n);
-          *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
+          float xv[8];
+          unpack8(xq[u], xv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * (xv[q] - mu[q]); }
         }
       } else {
-        if (a.epi) o = epilogue_op(a.epi, v, a.aux + off);
+        if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[u]);
         if (a.stats) {
           float f[8];
           unpack8(v, f);
@@ -769,26 +796,37 @@ MI_API int mi_set_nt_stages(int stages) {
 extern "C" int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
                                const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs,
                                int P, int Q, int R, int S, int stride, int pad, int N, hipStream_t st);
-static int g_gemm256_env = -1, g_conv256_min_tiles = -1;
-static bool use_gemm256_conv(int M, int N, int Cs) {
+static int g_gemm256_env = -1, g_conv256_min_tiles = -1, g_conv256_min_k = 64;
+static bool use_gemm256_conv(int M, int N, int Cs, int Kt) {
   if (g_gemm256_env < 0) {
     const char* e = std::getenv("MI355X_DP_GEMM256");
     g_gemm256_env = (e && e[0] == '0') ? 0 : 1;
     const char* t = std::getenv("MI355X_DP_CONV256_MIN_TILES");
     g_conv256_min_tiles = t ? std::atoi(t) : 96;
+    // GEMM depth (R*S*Cs) below which a conv stays on the 128-tile kernel: a 1x1 conv over few
+    // channels is one or two k-tiles -- nothing for the 256x256 pipeline to overlap, and its 128 KB
+    // of LDS holds the CU to one block through a load-latency-bound prologue / epilogue
+    const char* c = std::getenv("MI355X_DP_CONV256_MIN_K");
+    g_conv256_min_k = c ? std::atoi(c) : 512;
   }
-  return g_gemm256_env && Cs % 64 == 0 && N % 8 == 0 && N >= 256 &&
+  return g_gemm256_env && Cs % 64 == 0 && Kt >= g_conv256_min_k && N % 8 == 0 && N >= 256 &&
          (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_conv256_min_tiles;
 }
 
 MI_API void mi_set_conv256_min_tiles(int t) {
-  use_gemm256_conv(0, 0, 0);  // env init
+  use_gemm256_conv(0, 0, 0, 0);  // env init
   g_conv256_min_tiles = t;
 }
 
+// minimum GEMM depth R*S*Cs for the 256x256 conv path (tests force small shapes onto it with 0)
+MI_API void mi_set_conv256_min_k(int k) {
+  use_gemm256_conv(0, 0, 0, 0);  // env init
+  g_conv256_min_k = k;
+}
+
 // Statistics-slab rows written by a conv forward (M output pixels, N channels, Cs input channels).
-MI_API int mi_conv_stat_rows(int M, int N, int Cs) {
-  if (use_gemm256_conv(M, N, Cs)) return 2 * cdiv(M, 256);
+MI_API int mi_conv_stat_rows(int M, int N, int Cs, int RS) {
+  if (use_gemm256_conv(M, N, Cs, RS * Cs)) return 2 * cdiv(M, 256);
   const int bm = nt_choice(M, N) == 2 ? 64 : 128;
   return cdiv(M, bm);
 }
@@ -805,7 +843,7 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
                          int Nb, int H, int W, int C, int K, int R, int S,
                          int stride, int pad, int P, int Q, int out_f32, hipStream_t st) {
   if ((C % 64 != 0 && C != 8) || K % 8 != 0) return (int)hipErrorInvalidValue;
-  if (!out_f32 && !bias && use_gemm256_conv(Nb * P * Q, K, C))
+  if (!out_f32 && !bias && use_gemm256_conv(Nb * P * Q, K, C, R * S * C))
     return mi_gemm256_conv(1, x, w, y, stats, 0, nullptr, nullptr, nullptr, 0, Nb, H, W, C, P, Q, R, S, stride, pad,
                            K, st);
   NTArgs a{};
@@ -823,7 +861,7 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
   if (K % 64 != 0 || C % 8 != 0 || stride > 2) return (int)hipErrorInvalidValue;
-  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K))
+  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
     return mi_gemm256_conv(2, dy, wt, dx, nullptr, 0, nullptr, nullptr, nullptr, 0, Nb, P, Q, K, H, W, R, S, 1, pad, C,
                            st);
   NTArgs a{};
@@ -849,9 +887,9 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
 }
 
 // Statistics-slab rows written by mi_conv2d_dgrad_ex with stats (all parity classes).
-MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride, int K) {
+MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride, int K, int RS) {
   const int M = Nb * H * W;
-  if (stride == 1 && use_gemm256_conv(M, C, K)) return 2 * cdiv(M, 256);
+  if (stride == 1 && use_gemm256_conv(M, C, K, RS * K)) return 2 * cdiv(M, 256);
   const int bm = nt_choice(M, C) == 2 ? 64 : 128;
   if (stride == 1) return cdiv(M, bm);
   int mrows = 0;
@@ -869,7 +907,7 @@ MI_API int mi_conv2d_dgrad_ex(const void* dy, const void* wt, void* dx, int Nb, 
   if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4 || epi == 5) ||
       (epi && !aux && bn_relu) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)))
     return (int)hipErrorInvalidValue;
-  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K))
+  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
     return mi_gemm256_conv(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
                            bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, st);
   NTArgs a{};

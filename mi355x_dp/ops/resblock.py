@@ -77,7 +77,7 @@ def _conv_fwd_stats(x, spec):
     K, _, R, S = spec.w.shape
     P, Q = _out_hw(H, R, spec.stride, spec.pad), _out_hw(W, S, spec.stride, spec.pad)
     lib = _lib.load()
-    rows = lib.mi_conv_stat_rows(N * P * Q, K, C)
+    rows = lib.mi_conv_stat_rows(N * P * Q, K, C, R * S)
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=x.device)
     y = torch.empty((N, K, P, Q), dtype=BF16, device=x.device, memory_format=CL)
     _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), ptr(slab), N, H, W, C, K, R, S, spec.stride,
@@ -126,7 +126,8 @@ def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev):
     input: returns (dz, slab, rows)."""
     N, C, H, W = y_prev.shape
     lib = _lib.load()
-    rows = lib.mi_dgrad_stat_rows(N, H, W, C, dy.shape[2], dy.shape[3], spec.stride, spec.w.shape[0])
+    rows = lib.mi_dgrad_stat_rows(N, H, W, C, dy.shape[2], dy.shape[3], spec.stride, spec.w.shape[0],
+                                 spec.w.shape[2] * spec.w.shape[3])
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dy.device)
     dz = torch.empty_like(y_prev, memory_format=CL)
     _dgrad(dy, spec, y_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab)
@@ -245,7 +246,7 @@ class _ResBlock(torch.autograd.Function):
             N, C, H, W = x.shape
             lib = _lib.load()
             rows = lib.mi_dgrad_stat_rows(N, H, W, C, dc.shape[2], dc.shape[3], convs[0].stride,
-                                          convs[0].w.shape[0])
+                                          convs[0].w.shape[0], convs[0].w.shape[2] * convs[0].w.shape[3])
             slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dx.device)
             _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab)
             _HANDOFF[(dx.data_ptr(), dx.device.index)] = (slab, rows, dx._version, c_prev.data_ptr())

@@ -92,8 +92,10 @@ def conv256_forced():
     from mi355x_dp.ops import _lib
     lib = _lib.load()
     lib.mi_set_conv256_min_tiles(1)
+    lib.mi_set_conv256_min_k(0)
     yield lib
     lib.mi_set_conv256_min_tiles(96)
+    lib.mi_set_conv256_min_k(512)
 
 
 @pytest.mark.parametrize("shape", CONV256)
@@ -110,7 +112,7 @@ def test_conv256_fwd_stats_and_dgrad(shape, conv256_forced):
     w = (torch.randn(K, C, R, R, device="cuda") * 0.05).to(BF).contiguous(memory_format=CL)
     st = stream_of(x)
     M = N * P * P
-    rows = lib.mi_conv_stat_rows(M, K, C)
+    rows = lib.mi_conv_stat_rows(M, K, C, R * R)
     assert rows == 2 * ((M + 255) // 256)
     slab = torch.full((rows + 64, 2, K), float("nan"), device="cuda")
     y = torch.empty(N, K, P, P, dtype=BF, device="cuda", memory_format=CL)
@@ -145,7 +147,7 @@ def test_conv256_fwd_stats_and_dgrad(shape, conv256_forced):
     ybn = torch.randn_like(x, dtype=torch.float32).to(BF).contiguous(memory_format=CL)
     xbn = torch.randn_like(x, dtype=torch.float32).to(BF).contiguous(memory_format=CL)
     mean = torch.randn(C, device="cuda") * 0.1
-    r2 = lib.mi_dgrad_stat_rows(N, H, H, C, P, P, 1, K)
+    r2 = lib.mi_dgrad_stat_rows(N, H, H, C, P, P, 1, K, R * R)
     slab2 = torch.full((r2 + 64, 2, C), float("nan"), device="cuda")
     dz = torch.empty_like(x)
     _lib.call("mi_conv2d_dgrad_ex", ptr(dy), ptr(wt), ptr(dz), N, H, H, C, K, R, R, s, p, P, P, 4, ptr(ybn),

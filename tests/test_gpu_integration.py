@@ -194,3 +194,20 @@ def test_debug_kernels_training_step_clean(tmp_path):
     env = {**os.environ, "MI355X_DP_DEBUG_KERNELS": "1", "MI355X_DP_SYNC_CHECK": "1"}
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "DEBUG_OK" in r.stdout, (r.stdout + r.stderr)[-3000:]
+
+
+def test_bench_two_ranks_torchrun_gloo():
+    """bench.py under the driver's exact launcher shape (torch.distributed.run, 127.0.0.1, N=2) on
+    one GPU: 2 gloo ranks share cuda:0; rank 0 prints ONE JSON line with the whole-job value."""
+    import json
+    port = 29500 + (os.getpid() % 2000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--backend", "gloo", "--model", "resnet18", "--image-size", "32", "--batch", "32", "--num-classes", "10"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 64 and out["value"] > 0
