@@ -340,6 +340,151 @@ __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const bf16_t* __restric
   }
 }
 
+// ------------------------------------------------ ResNet stem: BN apply + ReLU + MaxPool, fused
+// The stem's BN/ReLU output is the largest activation of the network (64 x 112 x 112 per image)
+// and its only consumer is the 3x3/2 max pool.  Forward reads the conv output c and pools
+// relu(c*scale + shift) directly (values rounded to bf16 before the compare, so the arg-max and
+// torch's first-max tie rule match the unfused bn -> relu -> maxpool chain); the full-resolution
+// activation is never written.  Backward recomputes the mask from c instead of reading it:
+// pass 1 (STATS) gathers dz = [y > 0] * sum(dpool routed by the arg-max) per input pixel and
+// reduces (sum dz, sum dz*(c - mean)) into the BN backward slab; pass 2 (APPLY) regathers dz and
+// writes dc = k0*dz + k1*c + k2.  Neither pass writes dz.
+__global__ __launch_bounds__(NT) void bnpool_fwd_kernel(const bf16_t* __restrict__ c, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, bf16_t* __restrict__ y,
+                                                        uint8_t* __restrict__ idx, int Nb, int H, int W, int C, int P,
+                                                        int Q, int k, int s, int pad) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)Nb * P * Q * C8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int c8 = (int)(t % C8);
+    int64_t pix = t / C8;
+    const int q = (int)(pix % Q); pix /= Q;
+    const int p = (int)(pix % P);
+    const int n = (int)(pix / P);
+    float a[8], b[8], best[8];
+    uint8_t bi[8];
+    *(float4*)&a[0] = *(const float4*)(scale + c8 * 8); *(float4*)&a[4] = *(const float4*)(scale + c8 * 8 + 4);
+    *(float4*)&b[0] = *(const float4*)(shift + c8 * 8); *(float4*)&b[4] = *(const float4*)(shift + c8 * 8 + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < k; ++r) {
+      const int ih = p * s - pad + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int cc = 0; cc < k; ++cc) {
+        const int iw = q * s - pad + cc;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*(const uint4*)(c + (((size_t)n * H + ih) * W + iw) * C + c8 * 8), f);
+        const uint8_t tap = (uint8_t)(r * k + cc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = bf2f(f2bf(fmaxf(f[j] * a[j] + b[j], 0.f)));
+          if (v > best[j]) { best[j] = v; bi[j] = tap; }
+        }
+      }
+    }
+    const size_t o = (size_t)t * 8;
+    *(uint4*)(y + o) = pack8(best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(uint2*)(idx + o) = packed;
+  }
+}
+
+// dz (8 channels at input pixel (n,h,w), channel base cc) from the pooled gradient, the arg-max
+// taps and the conv output (relu mask recomputed); also returns the 8 conv outputs.
+__device__ __forceinline__ void bnpool_dz(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                          const bf16_t* __restrict__ c, const float* a, const float* b, int n,
+                                          int h, int w, int cc, int H, int W, int C, int P, int Q, int k, int s,
+                                          int pad, float* dz, float* cv) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
+  const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
+  for (int p = p_lo; p <= p_hi; ++p) {
+    const int r = h + pad - p * s;
+    if (r < 0 || r >= k) continue;
+    for (int q = q_lo; q <= q_hi; ++q) {
+      const int t = w + pad - q * s;
+      if (t < 0 || t >= k) continue;
+      const size_t o = (((size_t)n * P + p) * Q + q) * C + cc;
+      const uint2 ii = *(const uint2*)(idx + o);
+      float g[8];
+      unpack8(*(const uint4*)(dy + o), g);
+      const uint32_t tap = (uint32_t)(r * k + t);
+      const uint32_t wds[2] = {ii.x, ii.y};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (((wds[j >> 2] >> (8 * (j & 3))) & 0xffu) == tap) acc[j] += g[j];
+    }
+  }
+  unpack8(*(const uint4*)(c + (((size_t)n * H + h) * W + w) * C + cc), cv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dz[j] = bf2f(f2bf(cv[j] * a[j] + b[j])) > 0.f ? acc[j] : 0.f;
+}
+
+__global__ __launch_bounds__(NT) void bnpool_bwd_stats_kernel(const bf16_t* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx,
+                                                              const bf16_t* __restrict__ c,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              const float* __restrict__ mean,
+                                                              float* __restrict__ part, int Nb, int H, int W, int C,
+                                                              int P, int Q, int k, int s, int pad,
+                                                              int rows_per_block) {
+  const SlabGeom g = slab_geom(C);
+  const int tid = threadIdx.x;
+  const int c8 = tid % g.tpr, r0 = tid / g.tpr;
+  const int cbase = blockIdx.y * g.cw;
+  const int cc = cbase + c8 * 8;
+  const int M = Nb * H * W;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  float a[8], b[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a[j] = scale[cc + j]; b[j] = shift[cc + j]; mu[j] = mean[cc + j]; }
+  float sd[8] = {0}, sq[8] = {0};
+  for (int r = rb + r0; r < re; r += g.rp) {
+    const int w = r % W, nh = r / W;
+    const int h = nh % H, n = nh / H;
+    float dz[8], cv[8];
+    bnpool_dz(dy, idx, c, a, b, n, h, w, cc, H, W, C, P, Q, k, s, pad, dz, cv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sd[j] += dz[j]; sq[j] += dz[j] * (cv[j] - mu[j]); }
+  }
+  block_reduce_store(sd, sq, part, C, cbase, g);
+}
+
+__global__ __launch_bounds__(NT) void bnpool_bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx,
+                                                              const bf16_t* __restrict__ c,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              const float* __restrict__ coef,
+                                                              bf16_t* __restrict__ dc, int Nb, int H, int W, int C,
+                                                              int P, int Q, int k, int s, int pad) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)Nb * H * W * C8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int c8 = (int)(t % C8);
+    int64_t pix = t / C8;
+    const int w = (int)(pix % W); pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    const int cc = c8 * 8;
+    float a[8], b[8], k0[8], k1[8], k2[8];
+    *(float4*)&a[0] = *(const float4*)(scale + cc); *(float4*)&a[4] = *(const float4*)(scale + cc + 4);
+    *(float4*)&b[0] = *(const float4*)(shift + cc); *(float4*)&b[4] = *(const float4*)(shift + cc + 4);
+    float dz[8], cv[8], o[8];
+    bnpool_dz(dy, idx, c, a, b, n, h, w, cc, H, W, C, P, Q, k, s, pad, dz, cv);
+    *(float4*)&k0[0] = *(const float4*)(coef + cc); *(float4*)&k0[4] = *(const float4*)(coef + cc + 4);
+    *(float4*)&k1[0] = *(const float4*)(coef + C + cc); *(float4*)&k1[4] = *(const float4*)(coef + C + cc + 4);
+    *(float4*)&k2[0] = *(const float4*)(coef + 2 * C + cc); *(float4*)&k2[4] = *(const float4*)(coef + 2 * C + cc + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = k0[j] * dz[j] + k1[j] * cv[j] + k2[j];
+    *(uint4*)(dc + (size_t)t * 8) = pack8(o);
+  }
+}
+
 inline int ew_grid(int64_t nvec) {
   int64_t g = (nvec + NT * EW_U - 1) / (NT * EW_U);
   return (int)(g < 4096 ? g : 4096);
@@ -398,6 +543,7 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
   nblk = tall_slab_split(part, nblk, C, st, fin);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, eps, momentum,
                      gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
+  if (!y) return (int)hipGetLastError();  // statistics + coefficients only (the consumer applies them)
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
                      (bf16_t*)y, scale, shift, nvec, C, relu);
@@ -457,5 +603,56 @@ MI_API int mi_bn_bwd_eval(const void* dy, const void* y, const float* scale, voi
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_bwd_eval_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)y, scale, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
+  return (int)hipGetLastError();
+}
+
+// The gather-bound statistics pass wants more blocks in flight than the plain slab geometry gives.
+inline void bnpool_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3& grid) {
+  SlabGeom g = slab_geom(C);
+  const int ncs = C / g.cw;
+  const int target = std::max(1, 4096 / ncs);
+  rows_per_block = std::max(g.rp * 4, cdiv(M, target));
+  rows_per_block = cdiv(rows_per_block, g.rp) * g.rp;
+  nblk = cdiv(M, rows_per_block);
+  grid = dim3(nblk, ncs);
+}
+
+MI_API int mi_bnpool_partial_rows(int M, int C) {
+  int nblk, rpb; dim3 grid;
+  bnpool_launch_dims(M, C, nblk, rpb, grid);
+  return nblk;
+}
+
+// Stem forward tail: pooled = maxpool(relu(c*scale + shift)), idx = arg-max tap (uint8).
+MI_API int mi_bnpool_fwd(const void* c, const float* scale, const float* shift, void* y, void* idx, int Nb, int H,
+                         int W, int C, int P, int Q, int k, int s, int pad, hipStream_t st) {
+  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)Nb * P * Q * (C / 8);
+  const int64_t g = std::min<int64_t>((total + NT - 1) / NT, 16384);
+  hipLaunchKernelGGL(bnpool_fwd_kernel, dim3((int)g), dim3(NT), 0, st, (const bf16_t*)c, scale, shift, (bf16_t*)y,
+                     (uint8_t*)idx, Nb, H, W, C, P, Q, k, s, pad);
+  return (int)hipGetLastError();
+}
+
+// Stem backward: dpool -> dc (BN training backward through ReLU and MaxPool), dgamma/dbeta += .
+// part: [mi_bnpool_partial_rows(Nb*H*W, C) + mi_bn_slab_extra_rows()][2][C] fp32, coef: [3][C] fp32.
+MI_API int mi_bnpool_bwd(const void* dy, const void* idx, const void* c, void* dc, int Nb, int H, int W, int C, int P,
+                         int Q, int k, int s, int pad, const float* scale, const float* shift, const float* gamma,
+                         const float* save_mean, const float* save_invstd, float* dgamma, float* dbeta, float* coef,
+                         float* part, hipStream_t st) {
+  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
+  const int M = Nb * H * W;
+  int nblk, rpb; dim3 grid;
+  bnpool_launch_dims(M, C, nblk, rpb, grid);
+  hipLaunchKernelGGL(bnpool_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,
+                     (const bf16_t*)c, scale, shift, save_mean, part, Nb, H, W, C, P, Q, k, s, pad, rpb);
+  const float* fin = part;
+  nblk = tall_slab_split(part, nblk, C, st, fin);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
+                     save_mean, save_invstd, dgamma, dbeta, coef);
+  const int64_t total = (int64_t)M * (C / 8);
+  const int64_t g = std::min<int64_t>((total + NT - 1) / NT, 16384);
+  hipLaunchKernelGGL(bnpool_bwd_apply_kernel, dim3((int)g), dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,
+                     (const bf16_t*)c, scale, shift, coef, (bf16_t*)dc, Nb, H, W, C, P, Q, k, s, pad);
   return (int)hipGetLastError();
 }

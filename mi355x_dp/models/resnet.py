@@ -19,10 +19,13 @@ import torch.nn as nn
 import os
 
 from mi355x_dp.ops import resblock as _rb
+from mi355x_dp.ops import stem as _stem
 from .layers import BatchNorm2d, Conv2d, GlobalAvgPool2d, Linear, MaxPool2d, ReLU, conv_bn, to_device_input
 
 # one fused autograd node per residual block on the native training path (MI355X_DP_FUSED_BLOCKS=0: per-op)
 FUSED_BLOCKS = os.environ.get("MI355X_DP_FUSED_BLOCKS", "1") != "0"
+# stem conv -> BN -> ReLU -> maxpool as one node (MI355X_DP_FUSED_STEM=0: per-op)
+FUSED_STEM = os.environ.get("MI355X_DP_FUSED_STEM", "1") != "0"
 
 
 def conv3x3(in_planes, out_planes, stride=1):
@@ -127,8 +130,11 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         x = to_device_input(x)
-        x = conv_bn(self.conv1, self.bn1, x, relu=True)
-        x = self.maxpool(x)
+        if FUSED_STEM and _stem.fusable(self.conv1, self.bn1, self.maxpool, x):
+            x = _stem.stem(self.conv1, self.bn1, self.maxpool, x)
+        else:
+            x = conv_bn(self.conv1, self.bn1, x, relu=True)
+            x = self.maxpool(x)
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -26,6 +26,9 @@ signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, 
 signature("mi_bn_fwd_eval", P, P, P, I, I, F, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_train", P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_eval", P, P, P, P, P, I, I, I, P)
+signature("mi_bnpool_partial_rows", I, I)
+signature("mi_bnpool_fwd", P, P, P, P, P, I, I, I, I, I, I, I, I, I, P)
+signature("mi_bnpool_bwd", P, P, P, P, I, I, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P)
 
 # misc.hip
 signature("mi_maxpool_fwd", P, P, P, I, I, I, I, I, I, I, I, I, P)
