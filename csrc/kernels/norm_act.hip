@@ -485,6 +485,179 @@ __global__ __launch_bounds__(NT) void bnpool_bwd_apply_kernel(const bf16_t* __re
   }
 }
 
+// k=3, s=2, pad=1 (every ResNet stem) specialisations.  Forward: one thread per (output pixel,
+// 8 channels), all nine 16-byte taps issued before the first compare (out-of-image taps load the
+// always-valid centre and are skipped).  Backward: one thread per output pixel (p,q) owns the 2x2
+// input pixels (2p..2p+1, 2q..2q+1), whose gradients come only from windows (p..p+1, q..q+1):
+//   (0,0) <- W00 tap 4;  (0,1) <- W00 tap 5, W01 tap 3;  (1,0) <- W00 tap 7, W10 tap 1;
+//   (1,1) <- W00 tap 8, W01 tap 6, W10 tap 2, W11 tap 0   (same summation order as the gather).
+// 4 window loads + 4 pixel loads per thread, all independent, 32-bit index math.
+__global__ __launch_bounds__(NT) void bnpool3_fwd_kernel(const bf16_t* __restrict__ c, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, bf16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ idx, int H, int W, int C, int P, int Q,
+                                                         int total) {
+  const int C8 = C / 8;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
+    const int c8 = t % C8;
+    const int pix = t / C8;
+    const int q = pix % Q, np = pix / Q;
+    const int p = np % P, n = np / P;
+    const int cc = c8 * 8;
+    const bf16_t* base = c + ((size_t)n * H * W) * C + cc;
+    const int h0 = 2 * p, w0 = 2 * q;
+    uint4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int ih = h0 - 1 + r, iw = w0 - 1 + u;
+        const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        ok[r * 3 + u] = in;
+        v[r * 3 + u] = *(const uint4*)(base + ((size_t)(in ? ih : h0) * W + (in ? iw : w0)) * C);
+      }
+    }
+    float a[8], b[8], best[8];
+    uint32_t bi[8];
+    *(float4*)&a[0] = *(const float4*)(scale + cc); *(float4*)&a[4] = *(const float4*)(scale + cc + 4);
+    *(float4*)&b[0] = *(const float4*)(shift + cc); *(float4*)&b[4] = *(const float4*)(shift + cc + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      if (!ok[tp]) continue;
+      float f[8];
+      unpack8(v[tp], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float val = bf2f(f2bf(fmaxf(f[j] * a[j] + b[j], 0.f)));
+        if (val > best[j]) { best[j] = val; bi[j] = tp; }
+      }
+    }
+    const size_t o = (size_t)t * 8;
+    *(uint4*)(y + o) = pack8(best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    *(uint2*)(idx + o) = packed;
+  }
+}
+
+__device__ __forceinline__ uint32_t tap_of(const uint2& ii, int j) {
+  return ((j < 4 ? ii.x : ii.y) >> (8 * (j & 3))) & 0xffu;
+}
+
+// dz and c of the 2x2 input pixels owned by output pixel (n,p,q), channels cc..cc+7.
+// valid[i]: pixel i = (dh,dw) = (i>>1, i&1) lies inside the image.
+__device__ __forceinline__ void bnpool3_quad(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                             const bf16_t* __restrict__ c, const float* a, const float* b, int n,
+                                             int p, int q, int cc, int H, int W, int C, int P, int Q, float dz[4][8],
+                                             float cv[4][8], bool valid[4]) {
+  const bool pn = p + 1 < P, qn = q + 1 < Q;
+  const size_t o00 = (((size_t)n * P + p) * Q + q) * C + cc;
+  const size_t o01 = qn ? o00 + C : o00, o10 = pn ? o00 + (size_t)Q * C : o00;
+  const size_t o11 = (pn && qn) ? o00 + (size_t)Q * C + C : o00;
+  const uint4 g00 = *(const uint4*)(dy + o00), g01 = *(const uint4*)(dy + o01);
+  const uint4 g10 = *(const uint4*)(dy + o10), g11 = *(const uint4*)(dy + o11);
+  const uint2 i00 = *(const uint2*)(idx + o00), i01 = *(const uint2*)(idx + o01);
+  const uint2 i10 = *(const uint2*)(idx + o10), i11 = *(const uint2*)(idx + o11);
+  const int h0 = 2 * p, w0 = 2 * q;
+  uint4 xv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = h0 + (i >> 1), w = w0 + (i & 1);
+    valid[i] = h < H && w < W;
+    xv[i] = *(const uint4*)(c + (((size_t)n * H + (valid[i] ? h : h0)) * W + (valid[i] ? w : w0)) * C + cc);
+  }
+  float f00[8], f01[8], f10[8], f11[8];
+  unpack8(g00, f00); unpack8(g01, f01); unpack8(g10, f10); unpack8(g11, f11);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) unpack8(xv[i], cv[i]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t t00 = tap_of(i00, j), t01 = qn ? tap_of(i01, j) : 0xffu;
+    const uint32_t t10 = pn ? tap_of(i10, j) : 0xffu, t11 = (pn && qn) ? tap_of(i11, j) : 0xffu;
+    float acc[4];
+    acc[0] = t00 == 4u ? f00[j] : 0.f;
+    acc[1] = (t00 == 5u ? f00[j] : 0.f) + (t01 == 3u ? f01[j] : 0.f);
+    acc[2] = (t00 == 7u ? f00[j] : 0.f) + (t10 == 1u ? f10[j] : 0.f);
+    acc[3] = (t00 == 8u ? f00[j] : 0.f) + (t01 == 6u ? f01[j] : 0.f) + (t10 == 2u ? f10[j] : 0.f) +
+             (t11 == 0u ? f11[j] : 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dz[i][j] = bf2f(f2bf(cv[i][j] * a[j] + b[j])) > 0.f ? acc[i] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(NT) void bnpool3_bwd_stats_kernel(const bf16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx,
+                                                               const bf16_t* __restrict__ c,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift,
+                                                               const float* __restrict__ mean,
+                                                               float* __restrict__ part, int Nb, int H, int W, int C,
+                                                               int P, int Q, int rows_per_block) {
+  const SlabGeom g = slab_geom(C);
+  const int tid = threadIdx.x;
+  const int c8 = tid % g.tpr, r0 = tid / g.tpr;
+  const int cbase = blockIdx.y * g.cw;
+  const int cc = cbase + c8 * 8;
+  const int M = Nb * P * Q;
+  const int rb = blockIdx.x * rows_per_block, re = min(M, rb + rows_per_block);
+  float a[8], b[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a[j] = scale[cc + j]; b[j] = shift[cc + j]; mu[j] = mean[cc + j]; }
+  float sd[8] = {0}, sq[8] = {0};
+  for (int r = rb + r0; r < re; r += g.rp) {
+    const int q = r % Q, np = r / Q;
+    const int p = np % P, n = np / P;
+    float dz[4][8], cv[4][8];
+    bool valid[4];
+    bnpool3_quad(dy, idx, c, a, b, n, p, q, cc, H, W, C, P, Q, dz, cv, valid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!valid[i]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sd[j] += dz[i][j]; sq[j] += dz[i][j] * (cv[i][j] - mu[j]); }
+    }
+  }
+  block_reduce_store(sd, sq, part, C, cbase, g);
+}
+
+__global__ __launch_bounds__(NT) void bnpool3_bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx,
+                                                               const bf16_t* __restrict__ c,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift,
+                                                               const float* __restrict__ coef,
+                                                               bf16_t* __restrict__ dc, int H, int W, int C, int P,
+                                                               int Q, int total) {
+  const int C8 = C / 8;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
+    const int c8 = t % C8;
+    const int pix = t / C8;
+    const int q = pix % Q, np = pix / Q;
+    const int p = np % P, n = np / P;
+    const int cc = c8 * 8;
+    float a[8], b[8], k0[8], k1[8], k2[8];
+    *(float4*)&a[0] = *(const float4*)(scale + cc); *(float4*)&a[4] = *(const float4*)(scale + cc + 4);
+    *(float4*)&b[0] = *(const float4*)(shift + cc); *(float4*)&b[4] = *(const float4*)(shift + cc + 4);
+    *(float4*)&k0[0] = *(const float4*)(coef + cc); *(float4*)&k0[4] = *(const float4*)(coef + cc + 4);
+    *(float4*)&k1[0] = *(const float4*)(coef + C + cc); *(float4*)&k1[4] = *(const float4*)(coef + C + cc + 4);
+    *(float4*)&k2[0] = *(const float4*)(coef + 2 * C + cc); *(float4*)&k2[4] = *(const float4*)(coef + 2 * C + cc + 4);
+    float dz[4][8], cv[4][8];
+    bool valid[4];
+    bnpool3_quad(dy, idx, c, a, b, n, p, q, cc, H, W, C, P, Q, dz, cv, valid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!valid[i]) continue;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = k0[j] * dz[i][j] + k1[j] * cv[i][j] + k2[j];
+      *(uint4*)(dc + (((size_t)n * H + 2 * p + (i >> 1)) * W + 2 * q + (i & 1)) * C + cc) = pack8(o);
+    }
+  }
+}
+
 inline int ew_grid(int64_t nvec) {
   int64_t g = (nvec + NT * EW_U - 1) / (NT * EW_U);
   return (int)(g < 4096 ? g : 4096);
@@ -629,6 +802,11 @@ MI_API int mi_bnpool_fwd(const void* c, const float* scale, const float* shift, 
   if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)Nb * P * Q * (C / 8);
   const int64_t g = std::min<int64_t>((total + NT - 1) / NT, 16384);
+  if (k == 3 && s == 2 && pad == 1 && total < INT32_MAX && (int64_t)Nb * H * W * C < INT32_MAX * 8ll) {
+    hipLaunchKernelGGL(bnpool3_fwd_kernel, dim3((int)g), dim3(NT), 0, st, (const bf16_t*)c, scale, shift,
+                       (bf16_t*)y, (uint8_t*)idx, H, W, C, P, Q, (int)total);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bnpool_fwd_kernel, dim3((int)g), dim3(NT), 0, st, (const bf16_t*)c, scale, shift, (bf16_t*)y,
                      (uint8_t*)idx, Nb, H, W, C, P, Q, k, s, pad);
   return (int)hipGetLastError();
@@ -642,14 +820,26 @@ MI_API int mi_bnpool_bwd(const void* dy, const void* idx, const void* c, void* d
                          float* part, hipStream_t st) {
   if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
   const int M = Nb * H * W;
+  const bool k3 = k == 3 && s == 2 && pad == 1 && (int64_t)M * C < INT32_MAX;
   int nblk, rpb; dim3 grid;
-  bnpool_launch_dims(M, C, nblk, rpb, grid);
-  hipLaunchKernelGGL(bnpool_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,
-                     (const bf16_t*)c, scale, shift, save_mean, part, Nb, H, W, C, P, Q, k, s, pad, rpb);
+  bnpool_launch_dims(k3 ? Nb * P * Q : M, C, nblk, rpb, grid);
+  if (k3)
+    hipLaunchKernelGGL(bnpool3_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,
+                       (const bf16_t*)c, scale, shift, save_mean, part, Nb, H, W, C, P, Q, rpb);
+  else
+    hipLaunchKernelGGL(bnpool_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,
+                       (const bf16_t*)c, scale, shift, save_mean, part, Nb, H, W, C, P, Q, k, s, pad, rpb);
   const float* fin = part;
   nblk = tall_slab_split(part, nblk, C, st, fin);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
                      save_mean, save_invstd, dgamma, dbeta, coef);
+  if (k3) {
+    const int total3 = Nb * P * Q * (C / 8);
+    hipLaunchKernelGGL(bnpool3_bwd_apply_kernel, dim3(std::min(cdiv(total3, NT), 16384)), dim3(NT), 0, st,
+                       (const bf16_t*)dy, (const uint8_t*)idx, (const bf16_t*)c, scale, shift, coef, (bf16_t*)dc, H,
+                       W, C, P, Q, total3);
+    return (int)hipGetLastError();
+  }
   const int64_t total = (int64_t)M * (C / 8);
   const int64_t g = std::min<int64_t>((total + NT - 1) / NT, 16384);
   hipLaunchKernelGGL(bnpool_bwd_apply_kernel, dim3((int)g), dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,

@@ -77,8 +77,9 @@ class _Stem(torch.autograd.Function):
         lib = _lib.load()
         gw, gb = _grad_buffer(gamma), _grad_buffer(beta)
         M = N * P * Q
-        part = torch.empty((lib.mi_bnpool_partial_rows(M, K) + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32,
-                           device=dev)
+        # the k3/s2/p1 pass reduces over output-pixel quads, the generic one over input pixels
+        rows = max(lib.mi_bnpool_partial_rows(M, K), lib.mi_bnpool_partial_rows(N * P2 * Q2, K))
+        part = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=dev)
         coef = torch.empty((3, K), dtype=F32, device=dev)
         dc = torch.empty_like(c, memory_format=CL)
         _lib.call("mi_bnpool_bwd", ptr(dy), ptr(idx), ptr(c), ptr(dc), N, P, Q, K, P2, Q2, pk, ps, pp, ptr(scale),
