@@ -58,6 +58,10 @@ struct NTArgs {
   const bf16_t* aux2;
   const float* mean;
   int bn_relu;
+  // halo tiles (3x3 / stride 1 / pad 1, modes 1-2): a tile = halo_rp whole output rows of one image;
+  // halo_pb = row blocks per image; fPB / fHW2 divide by halo_pb / (Q + 2)
+  int halo_rp, halo_pb;
+  FastDiv fPB, fHW2;
   ConvGeom g;
 };
 
@@ -79,10 +83,13 @@ constexpr int BK = 64;
 // ----------------------------------------------------------------- NT kernel
 // modes: 0 plain GEMM, 1 conv fwd, 2 conv dgrad (stride-1 or masked), 3 conv dgrad
 // decomposed by output parity class (stride 2: only the taps that hit real dY pixels).
-template <int BM, int BN, int STAGES>
+// halo tile capacity (pixels of one 64-channel chunk, 128 B each): (rp + 2) x (Q + 2) <= HALO_PX
+constexpr int HALO_PX = 256;
+
+template <int BM, int BN, int STAGES, bool HALO = false>
 constexpr int nt_smem_u4() {
   // max(staging ring, epilogue C tile [BM][BN+8] bf16 + stats scratch [RPP][2][BN] fp32)
-  constexpr int stage = STAGES * (BM + BN) * 8;
+  constexpr int stage = HALO ? HALO_PX * 8 + 2 * BN * 8 : STAGES * (BM + BN) * 8;
   constexpr int epi = (BM * (BN + 8) * 2 + (256 / (BN / 8)) * 2 * BN * 4) / 16;
   return stage > epi ? stage : epi;
 }
@@ -92,19 +99,26 @@ constexpr int nt_smem_u4() {
 // STAGES = 2: double buffer, next k-step's loads in flight during this one's MFMAs, 2 blocks per CU.
 // Both stage with buffer_load ... lds (16 B per lane, zero-fill by range check) and track the
 // (tap, channel-chunk) position incrementally in scalar registers.
-template <int BM, int BN, int STAGES, bool SMALLC>
+//
+// HALO (3x3 / stride 1 / pad 1 forward and data gradient, C % 64 == 0): the tile is halo_rp whole
+// output rows of one image; per 64-channel chunk the (rp + 2) x (Q + 2) input halo is staged ONCE
+// into LDS and all nine taps read their A fragments from it (shifted row addresses), with the
+// weight tile of the next tap loading into the other B buffer during each tap's MFMAs.  The
+// per-tap gather re-reads every input pixel ~9x through L2; the halo reads it ~(rp+2)/rp x.
+template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false>
 __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
-  __shared__ __attribute__((aligned(16))) uint4 smem[nt_smem_u4<BM, BN, STAGES>()];
+  __shared__ __attribute__((aligned(16))) uint4 smem[nt_smem_u4<BM, BN, STAGES, HALO>()];
   uint4* As = smem;                      // [STAGES][BM][8]
   uint4* Bs = smem + STAGES * BM * 8;    // [STAGES][BN][8]
 
   const int nbn = (a.N + BN - 1) / BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / nbn;
-  const int m0 = tm * BM, n0 = (tile % nbn) * BN;
+  int m0 = tm * BM;
+  const int n0 = (tile % nbn) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int chk = tid & 7;
@@ -124,6 +138,15 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     fPQ = a.g.fPQc[cls]; fQ = a.g.fQc[cls];
     Mrows = (a.M / (a.g.P * a.g.Q)) * a.g.Pc[cls] * a.g.Qc[cls];
   }
+  // halo tile: image hi, output rows hp0 .. hp0 + hrows / Q - 1
+  int hi = 0, hp0 = 0, hrows = 0;
+  if constexpr (HALO) {
+    hi = (int)fdiv((uint32_t)tm, a.fPB);
+    hp0 = (tm - hi * a.halo_pb) * a.halo_rp;
+    hrows = min(a.halo_rp, a.g.P - hp0) * a.g.Q;
+    m0 = (hi * a.g.P + hp0) * a.g.Q;
+  }
+  const int Mlim = HALO ? m0 + hrows : Mrows;
   if (m0 >= Mrows) {
     // empty tile of a parity class: its statistics rows still have to be defined
     if (a.stats) {
@@ -266,7 +289,78 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     }
   };
 
-  if constexpr (STAGES == 1) {
+  if constexpr (HALO) {
+    uint4* Hs = smem;                   // [HALO_PX][8] input halo of one channel chunk
+    uint4* Bh = smem + HALO_PX * 8;     // [2][BN][8] weight tile of a tap
+    const int Q = a.g.Q, HW2 = Q + 2;
+    const int HP = (hrows / Q + 2) * HW2;
+    const int nit = (HP + 31) / 32;     // 32 halo pixels (256 x 16 B) per block-wide pass
+    int hb[MI];                         // halo pixel of tap (0,0) for this lane's fragment rows
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int ml = wm * WM + 16 * i + fr;
+      const uint32_t mc = ml < hrows ? (uint32_t)ml : 0u;
+      const uint32_t pr = fdiv(mc, a.g.fQ);
+      hb[i] = (int)pr * HW2 + (int)(mc - pr * (uint32_t)Q);
+    }
+    auto load_halo = [&](int kc) {
+      for (int it = 0; it < nit; ++it) {
+        const int f = it * 256 + tid;
+        const int px = f >> 3, chp = f & 7;
+        const uint32_t hr = fdiv((uint32_t)px, a.fHW2);
+        const int hc = px - (int)hr * HW2;
+        const int ih = hp0 - 1 + (int)hr, iw = hc - 1;
+        const bool ok = px < HP && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const uint32_t vo = ok ? (uint32_t)((((hi * H + ih) * W + iw) * Cs + kc + ((chp ^ (px & 7)) * 8)) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &Hs[it * 256 + wid * 64]), 16, vo, 0, 0, 0);
+      }
+    };
+    auto load_b = [&](int t, int kc, int buf) {
+      const int kB = t * Cs + kc;  // tap t = r*3 + s of [N][3][3][Cs]
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const bool ok = b_base[i] >= 0;
+        const uint32_t vo = ok ? (uint32_t)(b_base[i] + kB) * 2u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, LDS_PTR(void, &Bh[(buf * BN + 32 * i + 8 * wid) * 8]), 16,
+                                                 vo, 0, 0, 0);
+      }
+    };
+    auto compute_halo = [&](int t, int buf) {
+      const int r = t / 3, sx = t - 3 * r;
+      const int hoff = (a.mode == 1) ? r * HW2 + sx : (2 - r) * HW2 + (2 - sx);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int hx = hb[i] + hoff;
+          af[i] = __builtin_bit_cast(bf16x8, Hs[hx * 8 + ((kk * 4 + fq) ^ (hx & 7))]);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int row = wn * WN + 16 * j + fr;
+          bfr[j] = __builtin_bit_cast(bf16x8, Bh[(buf * BN + row) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    };
+    for (int kc = 0; kc < Cs; kc += 64) {
+      load_halo(kc);
+      load_b(0, kc, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) load_b(t + 1, kc, (t + 1) & 1);
+        compute_halo(t, t & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else if constexpr (STAGES == 1) {
     for (int kt = 0; kt < nk; ++kt) {
       issue_loads(kt, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -303,7 +397,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = m0 + wm * WM + 16 * i + fr;
-      if (m >= Mrows) continue;
+      if (m >= Mlim) continue;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = n0 + wn * WN + 16 * j + 4 * fq;
@@ -359,7 +453,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
       const int m = m0 + rr + (s0 + u) * RPP;
-      ok[u] = m < Mrows && n < a.N;
+      ok[u] = m < Mlim && n < a.N;
       offs[u] = ok[u] ? row_off(m) + n : 0;
       if (ok[u] && a.epi >= 4) {
         if (a.epi == 5) cv[u] = *(const uint4*)((const bf16_t*)a.C + offs[u]);
@@ -710,9 +804,12 @@ hipError_t launch_nt(NTArgs& a, hipStream_t st) {
     for (int c = 0; c < classes; ++c) mrows = std::max(mrows, nimg * a.g.Pc[c] * a.g.Qc[c]);
   }
   a.tiles_m = cdiv(mrows, BM);
+  if (a.halo_rp > 0) a.tiles_m = (a.M / (a.g.P * a.g.Q)) * a.halo_pb;
   int grid = a.tiles_m * cdiv(a.N, BN);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
-  if (a.mode == 4)
+  if (a.halo_rp > 0)
+    hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, true>), dim3(grid), dim3(256), 0, st, a);
+  else if (a.mode == 4)
     hipLaunchKernelGGL((nt_kernel<BM, BN, 1, true>), dim3(grid, classes), dim3(256), 0, st, a);
   else if (nt_stages() == 2)
     hipLaunchKernelGGL((nt_kernel<BM, BN, 2, false>), dim3(grid, classes), dim3(256), 0, st, a);
@@ -728,7 +825,35 @@ int nt_choice(int M, int N) {
   return 0;                                                      // 128x128
 }
 
+// Halo tiling (see nt_kernel) for a 3x3 / stride-1 / pad-1 conv whose row grid is P x Q (gathered
+// tensor the same size), Cs channels: rows per tile, or 0 when it does not apply (rows of >= 75 %
+// of a 128-row tile, halo within HALO_PX; 64x64-tile shapes keep the gather path).
+// MI355X_DP_HALO=0 disables.
+static int g_halo = -1;
+static int halo_rp(int M, int N, int R, int S, int stride, int pad, int Cs, int H, int W, int P, int Q) {
+  if (g_halo < 0) {
+    const char* e = std::getenv("MI355X_DP_HALO");
+    g_halo = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!g_halo || R != 3 || S != 3 || stride != 1 || pad != 1 || Cs % 64 != 0 || H != P || W != Q) return 0;
+  if (nt_choice(M, N) == 2) return 0;
+  const int rp = std::min(128 / Q, P);
+  if (rp < 1 || rp * Q * 4 < 128 * 3 || (rp + 2) * (Q + 2) > HALO_PX) return 0;
+  return rp;
+}
+
 hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
+  if (a.mode == 1 || a.mode == 2) {
+    const ConvGeom& g = a.g;
+    const int rp = halo_rp(a.M, a.N, g.R, g.S, g.stride, g.pad, g.Cs, g.H, g.W, g.P, g.Q);
+    if (rp > 0) {
+      a.halo_rp = rp;
+      a.halo_pb = cdiv(g.P, rp);
+      a.fPB = make_fastdiv((uint32_t)a.halo_pb);
+      a.fHW2 = make_fastdiv((uint32_t)(g.Q + 2));
+      return nt_choice(a.M, a.N) == 1 ? launch_nt<128, 64>(a, st) : launch_nt<128, 128>(a, st);
+    }
+  }
   switch (nt_choice(a.M, a.N)) {
     case 1: return launch_nt<128, 64>(a, st);
     case 2: return launch_nt<64, 64>(a, st);
@@ -824,7 +949,18 @@ MI_API void mi_set_conv256_min_k(int k) {
   g_conv256_min_k = k;
 }
 
-// Statistics-slab rows written by a conv forward (M output pixels, N channels, Cs input channels).
+// Statistics-slab rows written by mi_conv2d_fwd with stats (full geometry: the halo tiling of
+// 3x3 convs depends on the spatial shape).
+MI_API int mi_conv_stat_rows_g(int Nb, int H, int W, int C, int K, int R, int S, int stride, int pad, int P, int Q) {
+  const int M = Nb * P * Q;
+  if (C % 64 == 0 && use_gemm256_conv(M, K, C, R * S * C)) return 2 * cdiv(M, 256);
+  const int rp = C % 64 == 0 ? halo_rp(M, K, R, S, stride, pad, C, H, W, P, Q) : 0;
+  if (rp > 0) return Nb * cdiv(P, rp);
+  return cdiv(M, nt_choice(M, K) == 2 ? 64 : 128);
+}
+
+// Statistics-slab rows written by a conv forward (M output pixels, N channels, Cs input channels),
+// for shapes outside the halo tiling (1x1 / strided convs, GEMMs).
 MI_API int mi_conv_stat_rows(int M, int N, int Cs, int RS) {
   if (use_gemm256_conv(M, N, Cs, RS * Cs)) return 2 * cdiv(M, 256);
   const int bm = nt_choice(M, N) == 2 ? 64 : 128;
@@ -891,6 +1027,10 @@ MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int str
   const int M = Nb * H * W;
   if (stride == 1 && use_gemm256_conv(M, C, K, RS * K)) return 2 * cdiv(M, 256);
   const int bm = nt_choice(M, C) == 2 ? 64 : 128;
+  if (stride == 1 && RS == 9) {
+    const int rp = halo_rp(M, C, 3, 3, 1, 1, K, P, Q, H, W);
+    if (rp > 0) return Nb * cdiv(H, rp);
+  }
   if (stride == 1) return cdiv(M, bm);
   int mrows = 0;
   for (int c = 0; c < 4; ++c) mrows = std::max(mrows, Nb * ((H - c / 2 + 1) / 2) * ((W - c % 2 + 1) / 2));

@@ -206,7 +206,7 @@ def conv2d_with_stats(x, weight, stride=1, padding=0):
     K, _, R, S = weight.shape
     P, Q = _conv_out(H, R, stride, padding), _conv_out(W, S, stride, padding)
     lib = _lib.load()
-    rows = lib.mi_conv_stat_rows(N * P * Q, K, C if C % 64 == 0 else 8, R * S)
+    rows = lib.mi_conv_stat_rows_g(N, H, W, C if C % 64 == 0 else 8, K, R, S, stride, padding, P, Q)
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=torch.float32, device=x.device)
     y = _Conv2d.apply(x, weight, None, stride, padding, slab)
     return y, (slab, rows)

@@ -63,6 +63,7 @@ signature("mi_set_gemm256", I)
 signature("mi_gemm256_tn", P, P, P, I, I, I, I, I, I, P)
 signature("mi_dgrad_stat_rows", I, I, I, I, I, I, I, I, I)
 signature("mi_conv_stat_rows", I, I, I, I)
+signature("mi_conv_stat_rows_g", I, I, I, I, I, I, I, I, I, I, I)
 signature("mi_gemm256_conv", I, P, P, P, P, I, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_dgrad_ex", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, P)
 signature("mi_bn_bwd_train_pre", P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)

@@ -77,7 +77,7 @@ def _conv_fwd_stats(x, spec):
     K, _, R, S = spec.w.shape
     P, Q = _out_hw(H, R, spec.stride, spec.pad), _out_hw(W, S, spec.stride, spec.pad)
     lib = _lib.load()
-    rows = lib.mi_conv_stat_rows(N * P * Q, K, C, R * S)
+    rows = lib.mi_conv_stat_rows_g(N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q)
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=x.device)
     y = torch.empty((N, K, P, Q), dtype=BF16, device=x.device, memory_format=CL)
     _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), ptr(slab), N, H, W, C, K, R, S, spec.stride,

@@ -46,7 +46,7 @@ class _Stem(torch.autograd.Function):
         # conv: small-channel (8-wide tap) MFMA mode, BN statistics from the epilogue
         wp = torch.zeros((K, R, S, 8), dtype=BF16, device=dev)
         wp[..., :Cw].copy_(weight_bf16(wconv).permute(0, 2, 3, 1))
-        rows = lib.mi_conv_stat_rows(N * P * Q, K, 8, R * S)
+        rows = lib.mi_conv_stat_rows_g(N, H, W, 8, K, R, S, stride, pad, P, Q)
         slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=dev)
         c = torch.empty((N, K, P, Q), dtype=BF16, device=dev, memory_format=CL)
         _lib.call("mi_conv2d_fwd", ptr(x), ptr(wp), ptr(c), ptr(None), ptr(slab), N, H, W, 8, K, R, S, stride, pad,

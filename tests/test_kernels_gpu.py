@@ -36,6 +36,10 @@ CONV_SHAPES = [
     (3, 1024, 7, 2048, 1, 1, 0),
     (2, 128, 9, 192, 3, 1, 1),   # odd spatial / non-power-of-2 Cout
     (5, 64, 8, 128, 3, 2, 1),
+    # 3x3 / stride 1 halo tiles: 2 chunks x BN=128, 3 chunks + partial last row block, 2 rows of 50
+    (3, 128, 28, 128, 3, 1, 1),
+    (2, 192, 14, 64, 3, 1, 1),
+    (2, 64, 50, 128, 3, 1, 1),
 ]
 
 
@@ -226,7 +230,8 @@ def test_resnet18_train_step_matches_fp32():
         assert e_native <= 1.5 * e_stock + 0.02, (n, e_native, e_stock)
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 56, 256, 1, 1, 0), (4, 128, 28, 128, 3, 2, 1), (3, 3, 32, 64, 7, 2, 3)])
+@pytest.mark.parametrize("shape", [(4, 64, 56, 256, 1, 1, 0), (4, 128, 28, 128, 3, 2, 1), (3, 3, 32, 64, 7, 2, 3),
+                                   (4, 64, 56, 64, 3, 1, 1), (2, 128, 14, 128, 3, 1, 1)])
 def test_conv_bn_fused_stats(shape):
     """conv epilogue statistics + BN (fused path) == conv then BN with its own stats pass."""
     from mi355x_dp.models.layers import BatchNorm2d, Conv2d, conv_bn
