@@ -949,10 +949,25 @@ MI_API void mi_set_conv256_min_k(int k) {
   g_conv256_min_k = k;
 }
 
+// stem_conv.hip: persistent LDS-ring kernel for the 7x7/2 stem on 8-channel input
+extern "C" int mi_stem_conv_ok(int C, int K, int R, int S, int stride, int pad, int Q);
+extern "C" int mi_stem_conv_stat_rows(int Nb, int P);
+extern "C" int mi_stem_conv_fwd(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int P,
+                                int Q, int pad, hipStream_t st);
+static int g_stem = -1;
+static bool use_stem_kernel(int C, int K, int R, int S, int stride, int pad, int Q) {
+  if (g_stem < 0) {
+    const char* e = std::getenv("MI355X_DP_STEM_KERNEL");
+    g_stem = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_stem && mi_stem_conv_ok(C, K, R, S, stride, pad, Q);
+}
+
 // Statistics-slab rows written by mi_conv2d_fwd with stats (full geometry: the halo tiling of
 // 3x3 convs depends on the spatial shape).
 MI_API int mi_conv_stat_rows_g(int Nb, int H, int W, int C, int K, int R, int S, int stride, int pad, int P, int Q) {
   const int M = Nb * P * Q;
+  if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return mi_stem_conv_stat_rows(Nb, P);
   if (C % 64 == 0 && use_gemm256_conv(M, K, C, R * S * C)) return 2 * cdiv(M, 256);
   const int rp = C % 64 == 0 ? halo_rp(M, K, R, S, stride, pad, C, H, W, P, Q) : 0;
   if (rp > 0) return Nb * cdiv(P, rp);
@@ -979,6 +994,8 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
                          int Nb, int H, int W, int C, int K, int R, int S,
                          int stride, int pad, int P, int Q, int out_f32, hipStream_t st) {
   if ((C % 64 != 0 && C != 8) || K % 8 != 0) return (int)hipErrorInvalidValue;
+  if (!out_f32 && !bias && use_stem_kernel(C, K, R, S, stride, pad, Q))
+    return mi_stem_conv_fwd(x, w, y, stats, Nb, H, W, P, Q, pad, st);
   if (!out_f32 && !bias && use_gemm256_conv(Nb * P * Q, K, C, R * S * C))
     return mi_gemm256_conv(1, x, w, y, stats, 0, nullptr, nullptr, nullptr, 0, Nb, H, W, C, P, Q, R, S, stride, pad,
                            K, st);

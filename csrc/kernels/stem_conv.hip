@@ -1,0 +1,252 @@
+// ResNet stem convolution (7x7 / stride 2 / pad 3, 3 input channels zero-padded to 8, 64 output
+// channels) as a persistent MFMA kernel with an LDS-resident input ring, for gfx950.
+//
+// The generic implicit-GEMM path gathers every tap (16 B = one 8-channel pixel) from global memory,
+// so each input pixel crosses L2 -> LDS ~12 times (49 taps / stride^2) and the weight tile is
+// re-read by every block.  Here one block per CU owns whole images:
+//   * each wave keeps its 32 output channels x 49 taps of weights in registers (13 B fragments,
+//     loaded once), so the main loop reads only A fragments from LDS;
+//   * a ring of 13 input rows (4 KB each) holds the 9 rows a PAIR of output rows needs plus the 4
+//     new rows of the next pair, which are fetched with buffer_load ... lds while the current pair
+//     computes (8 waves: waves 0-3 output row 2j, waves 4-7 row 2j+1);
+//   * every A fragment (one tap of one output pixel = 16 B) comes from the ring, whose rows are
+//     stored column-parity split (even input columns, then odd) so the stride-2 reads of 16
+//     consecutive output pixels hit consecutive 16-B slots (no 2-way bank conflict);
+//   * the epilogue stores bf16 rows straight from the accumulators and keeps the BatchNorm
+//     (sum, sumsq) of the rounded outputs in registers across all rows; one statistics row per
+//     block is written at the end (the BN finalize reduces them).
+// Reference op: torchvision resnet conv1 (cifar10-distributed-smddp-gpu.py:30-32 via resnet18).
+#include "common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int SR = 7, SS = 7, SSTR = 2;            // kernel 7x7, stride 2
+constexpr int NTAP = SR * SS;                       // 49 taps of 8 channels (16 B)
+constexpr int KSTEPS = (NTAP + 3) / 4;              // MFMA k = 32 = 4 taps
+constexpr int KOUT = 64;
+constexpr int ROWPX = 256;                          // ring row capacity (pixels of 16 B)
+constexpr int PAIR_ROWS = SSTR + SR;                // input rows of two output rows: 9
+constexpr int NEW_ROWS = 2 * SSTR;                  // new input rows per output-row pair: 4
+constexpr int NRING = PAIR_ROWS + NEW_ROWS;         // 13
+constexpr int MAX_BLOCKS = 256;                     // one per CU
+constexpr int STEM_T = 512;
+
+struct StemArgs {
+  const bf16_t* x;    // [Nb][H][W][8]
+  const bf16_t* w;    // [64][7][7][8]
+  bf16_t* y;          // [Nb][P][Q][64]
+  float* stats;       // [gridDim.x][2][64] or null
+  int Nb, H, W, P, Q, pad;
+  int pairs_per_img, total_pairs, pairs_per_block;
+  int x_bytes;
+};
+
+__global__ __launch_bounds__(STEM_T, 1) void stem_conv_kernel(StemArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 sm[];
+  uint4* ring = sm;                                   // [NRING][ROWPX]: even columns, then odd
+  float* sred = (float*)(sm + NRING * ROWPX);         // [8 waves][2][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int half = wid >> 2, wq = wid & 3, wm = wq >> 1, wn = wq & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g0 = blockIdx.x * a.pairs_per_block;
+  const int g1 = min(a.total_pairs, g0 + a.pairs_per_block);
+  const int HC = (a.Q - 1) * SSTR + SS;               // ring row width in use (<= ROWPX)
+
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0xFFFFFFF0u;
+
+  // one input row -> ring slot (ih + pad) mod NRING; zero outside the image (padding)
+  auto load_rows = [&](int img, int ih0, int nrows) {
+    for (int c = wid; c < nrows * 4; c += 8) {         // 4 wave-loads of 64 pixels per row
+      const int k = c >> 2, part = c & 3;
+      const int ih = ih0 + k;
+      const int pos = part * 64 + lane;                // ring position -> input column (parity split)
+      const int px = pos < ROWPX / 2 ? 2 * pos : 2 * (pos - ROWPX / 2) + 1;
+      const int iw = px - a.pad;
+      const bool ok = px < HC && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const uint32_t vo = ok ? (uint32_t)((((img * a.H + ih) * a.W + iw) * 8) * 2) : OOB;
+      const int slot = (ih + a.pad) % NRING;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, &ring[slot * ROWPX + part * 64]), 16, vo, 0, 0, 0);
+    }
+  };
+
+  // this wave's weight fragments (channels wn*32 + 16j + fr, tap 4ks + fq), zero past tap 48
+  bf16x8 bw[KSTEPS][2];
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int t = 4 * ks + fq, n = wn * 32 + 16 * j + fr;
+      const bf16x8 zero = {};
+      bw[ks][j] = t < NTAP ? __builtin_bit_cast(bf16x8, ((const uint4*)a.w)[n * NTAP + t]) : zero;
+    }
+  for (int u = tid; u < 8 * 2 * KOUT; u += STEM_T) sred[u] = 0.f;
+  if (g0 < g1) {
+    const int img = g0 / a.pairs_per_img, j = g0 - img * a.pairs_per_img;
+    load_rows(img, 2 * SSTR * j - a.pad, PAIR_ROWS);
+  }
+
+  float s1[2][4], s2[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+
+  bool first = true;
+  int last_stores = 0;
+  for (int g = g0; g < g1; ++g) {
+    const int img = g / a.pairs_per_img, jp = g - img * a.pairs_per_img;
+    // the ring rows of this pair were issued BEFORE the previous pair's epilogue stores; vector
+    // memory counts retire in issue order, so leaving exactly those stores in flight still
+    // guarantees the loads landed.  The first pair and pairs after a fresh image load wait for all.
+    switch (first ? 0 : last_stores) {                 // wave-uniform: stores issued last pair
+      case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+    }
+    first = false;
+    __syncthreads();
+    const bool next_same = g + 1 < g1 && (g + 1) / a.pairs_per_img == img;
+    if (next_same) load_rows(img, 2 * SSTR * jp - a.pad + PAIR_ROWS, NEW_ROWS);  // prefetch next pair
+
+    const int p = 2 * jp + half;                       // this half's output row
+    last_stores = 0;
+    if (p < a.P) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) last_stores += (wm * 64 + 16 * i < a.Q) ? 2 : 0;
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int rbase = (SSTR * p) % NRING;            // slot of input row SSTR*p - pad (+ r)
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const int t = 4 * ks + fq;
+        const bool tv = t < NTAP;
+        const int r = t / SS, s = t - (t / SS) * SS;
+        int slot = rbase + r;
+        slot = slot >= NRING ? slot - NRING : slot;
+        slot = slot >= NRING ? slot - NRING : slot;
+        bf16x8 af[4];
+        const bf16x8 zero = {};
+        // input column 2q + s sits at ring position (s & 1) * ROWPX/2 + q + (s >> 1)
+        const int cbase = slot * ROWPX + (s & 1) * (ROWPX / 2) + (s >> 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = wm * 64 + 16 * i + fr;        // output column (rows >= Q are discarded)
+          const bf16x8 v = __builtin_bit_cast(bf16x8, ring[cbase + min(q, a.Q - 1)]);
+          af[i] = tv ? v : zero;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks][j], af[i], acc[i][j], 0, 0, 0);
+      }
+      // epilogue: lane holds D[n = wn*32 + 16j + 4fq + r][q = wm*64 + 16i + fr]
+      bf16_t* yrow = a.y + ((size_t)(img * a.P + p) * a.Q) * KOUT;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = wm * 64 + 16 * i + fr;
+        if (q >= a.Q) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = wn * 32 + 16 * j + 4 * fq;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = bf2f(f2bf(acc[i][j][r]));
+            s1[j][r] += v[r];
+            s2[j][r] += v[r] * v[r];
+          }
+          *(uint2*)(yrow + (size_t)q * KOUT + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
+      }
+    }
+    if (g + 1 < g1 && !next_same) {                    // next pair starts a new image: fresh ring
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int img2 = (g + 1) / a.pairs_per_img, j2 = (g + 1) - img2 * a.pairs_per_img;
+      load_rows(img2, 2 * SSTR * j2 - a.pad, PAIR_ROWS);
+      first = true;
+    }
+  }
+
+  if (!a.stats) return;
+  // lanes sharing channels (same fq) differ in fr: reduce over lane bits 0-3, then over waves
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+        s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      }
+  __syncthreads();
+  if (fr == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wn * 32 + 16 * j + 4 * fq + r;
+        sred[(wid * 2 + 0) * KOUT + n] = s1[j][r];
+        sred[(wid * 2 + 1) * KOUT + n] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  if (tid < 2 * KOUT) {
+    const int which = tid / KOUT, n = tid - which * KOUT;
+    float t = 0.f;
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) t += sred[(w8 * 2 + which) * KOUT + n];
+    a.stats[((size_t)blockIdx.x * 2 + which) * KOUT + n] = t;
+  }
+}
+
+constexpr size_t stem_lds_bytes() {
+  return (size_t)(NRING * ROWPX) * 16 + 8 * 2 * KOUT * 4;
+}
+
+inline int stem_blocks(int total_pairs) { return std::max(1, std::min(total_pairs, MAX_BLOCKS)); }
+
+}  // namespace
+
+// Does the persistent stem kernel take this conv?  (7x7 / stride 2 on an 8-channel NHWC input,
+// 64 output channels, output rows narrow enough for the ring.)
+MI_API int mi_stem_conv_ok(int C, int K, int R, int S, int stride, int pad, int Q) {
+  return C == 8 && K == KOUT && R == SR && S == SS && stride == SSTR && pad >= 0 && pad < SR &&
+         (Q - 1) * SSTR + SS <= ROWPX && Q <= 128;
+}
+
+// Statistics rows written by mi_stem_conv_fwd (one per block).
+MI_API int mi_stem_conv_stat_rows(int Nb, int P) { return stem_blocks(Nb * ((P + 1) / 2)); }
+
+// x [Nb][H][W][8] bf16, w [64][7][7][8] bf16, y [Nb][P][Q][64] bf16, stats [rows][2][64] fp32 (optional)
+MI_API int mi_stem_conv_fwd(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int P, int Q,
+                            int pad, hipStream_t st) {
+  if (!mi_stem_conv_ok(8, KOUT, SR, SS, SSTR, pad, Q)) return (int)hipErrorInvalidValue;
+  const int64_t xb = (int64_t)Nb * H * W * 8 * 2;
+  if (xb > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
+  StemArgs a{};
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y; a.stats = stats;
+  a.Nb = Nb; a.H = H; a.W = W; a.P = P; a.Q = Q; a.pad = pad;
+  a.pairs_per_img = (P + 1) / 2;
+  a.total_pairs = Nb * a.pairs_per_img;
+  const int blocks = stem_blocks(a.total_pairs);
+  a.pairs_per_block = cdiv(a.total_pairs, blocks);
+  a.x_bytes = (int)xb;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)stem_conv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)stem_lds_bytes());
+    attr = true;
+  }
+  hipLaunchKernelGGL(stem_conv_kernel, dim3(blocks), dim3(STEM_T), stem_lds_bytes(), st, a);
+  return (int)hipGetLastError();
+}

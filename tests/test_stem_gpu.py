@@ -83,3 +83,27 @@ def test_fused_stem_used_in_resnet():
     assert "_StemBackward" in names and "_MaxPoolBackward" not in names, names
     cross_entropy(out, torch.tensor([1, 2], device="cuda")).backward()
     assert m.conv1.weight.grad is not None and m.bn1.weight.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("n,size", [(40, 58), (2, 224), (3, 33)])
+def test_stem_conv_kernel_and_stats(n, size):
+    """persistent LDS-ring stem conv (7x7/2, 8-channel input, 64 outputs): output vs fp32 conv and
+    its per-block BN statistics rows vs sums over the bf16 output; (40, 58): odd output rows and
+    blocks whose pair range crosses image boundaries (fresh ring loads)."""
+    from mi355x_dp.models.layers import to_device_input
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops.functional import conv2d_with_stats
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = to_device_input(torch.randn(n, 3, size, size, device="cuda", generator=g))
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).to(torch.bfloat16).float()
+    P = (size + 6 - 7) // 2 + 1
+    assert lib.mi_stem_conv_ok(8, 64, 7, 7, 2, 3, P)
+    y, (slab, rows) = conv2d_with_stats(x, w, 2, 3)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x[:, :3].float(), w, None, 2, 3)
+    assert rel_err(y, ref) < 1e-2
+    yf = y.float()
+    s = slab[:rows].sum(0)
+    assert torch.allclose(s[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
