@@ -954,6 +954,8 @@ extern "C" int mi_stem_conv_ok(int C, int K, int R, int S, int stride, int pad, 
 extern "C" int mi_stem_conv_stat_rows(int Nb, int P);
 extern "C" int mi_stem_conv_fwd(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int P,
                                 int Q, int pad, hipStream_t st);
+extern "C" int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H, int W, int P, int Q, int pad,
+                             hipStream_t st);
 static int g_stem = -1;
 static bool use_stem_kernel(int C, int K, int R, int S, int stride, int pad, int Q) {
   if (g_stem < 0) {
@@ -1094,6 +1096,7 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
   if (C % 8 != 0 || K % 8 != 0) return (int)hipErrorInvalidValue;
+  if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return mi_stem_wgrad(x, dy, dw, Nb, H, W, P, Q, pad, st);
   TNArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
   a.M = K; a.N = R * S * C; a.K = Nb * P * Q;

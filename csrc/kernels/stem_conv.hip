@@ -209,6 +209,164 @@ __global__ __launch_bounds__(STEM_T, 1) void stem_conv_kernel(StemArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- weight gradient
+// dW[k][tap][c] = sum over output pixels of dy[pix][k] * x[window(pix, tap)][c]: an MFMA GEMM
+// (M = 64 output channels, N = 49 taps x 8 channels as 25 tiles of 2 taps, reduction = pixels)
+// whose operands are both pixel-major, so every fragment is a ds_read_b64_tr_b16 transposed read:
+// A (dy^T) from a staged pair of dy rows, B straight from the same parity-split input ring as the
+// forward (any 8-byte-aligned address per lane), so no operand is ever restaged.  Each block keeps
+// its partial dW in registers across all its rows and adds it into the fp32 gradient once.
+constexpr int NUT = (NTAP + 1) / 2;                 // 25 n-tiles of 2 taps x 8 channels
+constexpr int DYPX = 128;                           // staged pixels per output row (Q <= 128)
+
+struct StemWArgs {
+  const bf16_t* x;    // [Nb][H][W][8]
+  const bf16_t* dy;   // [Nb][P][Q][64]
+  float* dw;          // [64][7][7][8] fp32, accumulated
+  int Nb, H, W, P, Q, pad;
+  int pairs_per_img, total_pairs, pairs_per_block;
+  int x_bytes, dy_bytes;
+};
+
+// 16-B chunk swizzle of a staged dy row: the two 4-pixel row groups of a 16-lane transposed read
+// and the other group of its 32-lane half land on distinct bank octets
+__device__ __forceinline__ int dy_swz(int px) { return (((px >> 1) & 1) << 1) | (((px >> 3) & 1) << 2); }
+
+__global__ __launch_bounds__(STEM_T, 1) void stem_wgrad_kernel(StemWArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 sm[];
+  uint4* ring = sm;                                   // [NRING][ROWPX]: even columns, then odd
+  uint4* dys = sm + NRING * ROWPX;                    // [2 buffers][2 rows][DYPX][8 chunks]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  const int g0 = blockIdx.x * a.pairs_per_block;
+  const int g1 = min(a.total_pairs, g0 + a.pairs_per_block);
+  const int HC = (a.Q - 1) * SSTR + SS;
+
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsd = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
+  constexpr uint32_t OOB = 0xFFFFFFF0u;
+
+  auto load_rows = [&](int img, int ih0, int nrows) {
+    for (int c = wid; c < nrows * 4; c += 8) {
+      const int k = c >> 2, part = c & 3;
+      const int ih = ih0 + k;
+      const int pos = part * 64 + lane;
+      const int px = pos < ROWPX / 2 ? 2 * pos : 2 * (pos - ROWPX / 2) + 1;
+      const int iw = px - a.pad;
+      const bool ok = px < HC && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const uint32_t vo = ok ? (uint32_t)((((img * a.H + ih) * a.W + iw) * 8) * 2) : OOB;
+      const int slot = (ih + a.pad) % NRING;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, LDS_PTR(void, &ring[slot * ROWPX + part * 64]), 16, vo, 0, 0, 0);
+    }
+  };
+  // output rows 2j, 2j+1 of dy -> buffer buf; a wave-load covers 8 pixels x 8 chunks
+  auto load_dy = [&](int img, int jp, int buf) {
+    for (int c = wid; c < 2 * DYPX / 8; c += 8) {
+      const int h = c / (DYPX / 8), px = (c % (DYPX / 8)) * 8 + (lane >> 3);
+      const int p = 2 * jp + h;
+      const int lc = (lane & 7) ^ dy_swz(px);
+      const bool ok = px < a.Q && p < a.P;
+      const uint32_t vo = ok ? (uint32_t)((((img * a.P + p) * a.Q + px) * KOUT + lc * 8) * 2) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsd, LDS_PTR(void, &dys[((buf * 2 + h) * DYPX + (c % (DYPX / 8)) * 8) * 8]),
+                                               16, vo, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc[m][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nv = wid + 24 < NUT ? 4 : 3;              // n-tiles u = wid + 8v of this wave
+
+  if (g0 < g1) {
+    const int img = g0 / a.pairs_per_img, j = g0 - img * a.pairs_per_img;
+    load_rows(img, 2 * SSTR * j - a.pad, PAIR_ROWS);
+    load_dy(img, j, 0);
+  }
+  int buf = 0;
+  const uint2* ring2 = (const uint2*)ring;
+  const uint2* dys2 = (const uint2*)dys;
+  for (int gp = g0; gp < g1; ++gp) {
+    const int img = gp / a.pairs_per_img, jp = gp - img * a.pairs_per_img;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool next_same = gp + 1 < g1 && (gp + 1) / a.pairs_per_img == img;
+    if (next_same) {
+      load_rows(img, 2 * SSTR * jp - a.pad + PAIR_ROWS, NEW_ROWS);
+      load_dy(img, jp + 1, buf ^ 1);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = 2 * jp + h;
+      if (p >= a.P) continue;
+      const int rbase = (SSTR * p) % NRING;
+      for (int c = 0; c < DYPX / 32; ++c) {
+        if (32 * c >= a.Q) break;
+        const int px1 = 32 * c + 8 * g + q4, px2 = px1 + 4;
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int lc = 2 * m + (p4 >> 1);
+          const uint2* r1 = dys2 + ((buf * 2 + h) * DYPX + px1) * 16 + 2 * (lc ^ dy_swz(px1)) + (p4 & 1);
+          const uint2* r2 = dys2 + ((buf * 2 + h) * DYPX + px2) * 16 + 2 * (lc ^ dy_swz(px2)) + (p4 & 1);
+          short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, r1));
+          short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, r2));
+          short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[m] = __builtin_bit_cast(bf16x8, v8);
+        }
+        const int qa = min(px1, a.Q - 1), qb = min(px2, a.Q - 1);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          if (v >= nv) break;
+          const int u = wid + 8 * v;
+          const int t = min(2 * u + (p4 >> 1), NTAP - 1);
+          const int r = t / SS, sx = t - (t / SS) * SS;
+          int slot = rbase + r;
+          slot = slot >= NRING ? slot - NRING : slot;
+          const int cb = slot * ROWPX + (sx & 1) * (ROWPX / 2) + (sx >> 1);
+          short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, ring2 + (cb + qa) * 2 + (p4 & 1)));
+          short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, ring2 + (cb + qb) * 2 + (p4 & 1)));
+          short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[v] = __builtin_bit_cast(bf16x8, v8);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          if (v >= nv) break;
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            acc[m][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[v], acc[m][v], 0, 0, 0);
+        }
+      }
+    }
+    buf ^= 1;
+    if (gp + 1 < g1 && !next_same) {                  // next pair starts a new image: fresh stage
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int img2 = (gp + 1) / a.pairs_per_img, j2 = (gp + 1) - img2 * a.pairs_per_img;
+      load_rows(img2, 2 * SSTR * j2 - a.pad, PAIR_ROWS);
+      load_dy(img2, j2, buf);
+    }
+  }
+  // D[i = out channel 16m + 4g + r][j = 16u + li]: column j = tap 2u + (li >> 3), channel li & 7
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    if (v >= nv) break;
+    const int tap = 2 * (wid + 8 * v) + (li >> 3);
+    if (tap >= NTAP) continue;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * m + 4 * g + r;
+        atomicAdd(a.dw + ((size_t)k * NTAP + tap) * 8 + (li & 7), acc[m][v][r]);
+      }
+  }
+}
+
+constexpr size_t stem_wgrad_lds_bytes() { return (size_t)(NRING * ROWPX + 2 * 2 * DYPX * 8) * 16; }
+
 constexpr size_t stem_lds_bytes() {
   return (size_t)(NRING * ROWPX) * 16 + 8 * 2 * KOUT * 4;
 }
@@ -248,5 +406,30 @@ MI_API int mi_stem_conv_fwd(const void* x, const void* w, void* y, float* stats,
     attr = true;
   }
   hipLaunchKernelGGL(stem_conv_kernel, dim3(blocks), dim3(STEM_T), stem_lds_bytes(), st, a);
+  return (int)hipGetLastError();
+}
+
+// dw [64][7][7][8] fp32 += stem weight gradient; x [Nb][H][W][8], dy [Nb][P][Q][64] bf16.
+MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H, int W, int P, int Q, int pad,
+                         hipStream_t st) {
+  if (!mi_stem_conv_ok(8, KOUT, SR, SS, SSTR, pad, Q) || Q > DYPX) return (int)hipErrorInvalidValue;
+  const int64_t xb = (int64_t)Nb * H * W * 8 * 2, db = (int64_t)Nb * P * Q * KOUT * 2;
+  if (xb > 0x7FFFFFF0LL || db > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
+  StemWArgs a{};
+  a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;
+  a.Nb = Nb; a.H = H; a.W = W; a.P = P; a.Q = Q; a.pad = pad;
+  a.pairs_per_img = (P + 1) / 2;
+  a.total_pairs = Nb * a.pairs_per_img;
+  const int blocks = stem_blocks(a.total_pairs);
+  a.pairs_per_block = cdiv(a.total_pairs, blocks);
+  a.x_bytes = (int)xb;
+  a.dy_bytes = (int)db;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)stem_wgrad_lds_bytes());
+    attr = true;
+  }
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(STEM_T), stem_wgrad_lds_bytes(), st, a);
   return (int)hipGetLastError();
 }

@@ -107,3 +107,21 @@ def test_stem_conv_kernel_and_stats(n, size):
     s = slab[:rows].sum(0)
     assert torch.allclose(s[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
     assert torch.allclose(s[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,size", [(40, 58), (2, 224), (3, 33)])
+def test_stem_wgrad_kernel(n, size):
+    """persistent stem weight-gradient kernel (transposed LDS reads of dy and of the input ring,
+    per-block partials added atomically) vs the fp32 weight gradient of the same conv"""
+    from mi355x_dp.models.layers import to_device_input
+    from mi355x_dp.ops import conv2d
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = to_device_input(torch.randn(n, 3, size, size, device="cuda", generator=g))
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).to(torch.bfloat16).float()
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_()
+    y = conv2d(x, w, None, 2, 3)
+    dy = torch.randn(y.shape, device="cuda", generator=g).to(torch.bfloat16)
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    wr = w.detach().clone().requires_grad_()
+    F.conv2d(x[:, :3].float(), wr, None, 2, 3).backward(dy.float())
+    assert rel_err(w.grad, wr.grad) < 1e-2
