@@ -120,16 +120,24 @@ __global__ __launch_bounds__(FIN_T) void slab_split_kernel(const float* __restri
   out[(size_t)(2 * blockIdx.y + 1) * C + c] = (float)b;
 }
 
-// training-mode finalize
-__global__ __launch_bounds__(FIN_T) void bn_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C, float eps, float momentum,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                   float* __restrict__ scale, float* __restrict__ shift) {
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
-  double s, q;
-  if (!slab_reduce64(part, nblk, C, s, q)) return;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+// per-channel finalize operands of the training forward (F) and backward (B)
+struct FinArgs {
+  int M, C;
+  float eps, momentum;                                        // F
+  const float* gamma; const float* beta;                      // F (gamma also B)
+  float* rmean; float* rvar; int64_t* nbt;                    // F
+  float* save_mean; float* save_invstd; float* scale; float* shift;  // F
+  const float* mean; const float* invstd;                     // B
+  float* dgamma; float* dbeta; float* coef;                   // B
+};
+
+__device__ __forceinline__ void fin_fwd(int c, double s, double q, const FinArgs& f) {
+  const int M = f.M;
+  const float eps = f.eps, momentum = f.momentum;
+  const float* gamma = f.gamma; const float* beta = f.beta;
+  float* rmean = f.rmean; float* rvar = f.rvar;
+  float* save_mean = f.save_mean; float* save_invstd = f.save_invstd;
+  float* scale = f.scale; float* shift = f.shift;
   const double mean = s / M;
   double var = q / M - mean * mean;
   if (var < 0) var = 0;
@@ -144,6 +152,14 @@ __global__ __launch_bounds__(FIN_T) void bn_finalize_kernel(const float* __restr
     rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
     rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
   }
+}
+
+// training-mode finalize
+__global__ __launch_bounds__(FIN_T) void bn_finalize_kernel(const float* __restrict__ part, int nblk, FinArgs f) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+  double s, q;
+  if (!slab_reduce64(part, nblk, f.C, s, q)) return;
+  fin_fwd(blockIdx.x * 64 + (threadIdx.x & 63), s, q, f);
 }
 
 __global__ void bn_eval_coeffs_kernel(int C, float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -252,13 +268,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(const bf16_t* __restri
 }
 
 // -> dgamma/dbeta (+=) and coef[0..2][C] so that dx = coef0*dz + coef1*x + coef2
-__global__ __launch_bounds__(FIN_T) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int M, int C,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef) {
-  double s, q;
-  if (!slab_reduce64(part, nblk, C, s, q)) return;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+__device__ __forceinline__ void fin_bwd(int c, double s, double q, const FinArgs& f) {
+  const int M = f.M, C = f.C;
+  const float* gamma = f.gamma; const float* mean = f.mean; const float* invstd = f.invstd;
+  float* dgamma = f.dgamma; float* dbeta = f.dbeta; float* coef = f.coef;
   const float is = invstd[c];
   const float sum_dz = (float)s;
   const float sum_dz_xhat = (float)q * is;
@@ -273,6 +286,71 @@ __global__ __launch_bounds__(FIN_T) void bn_bwd_finalize_kernel(const float* __r
   coef[c] = k0;
   coef[C + c] = k1;
   coef[2 * C + c] = k2;
+}
+
+__global__ __launch_bounds__(FIN_T) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, FinArgs f) {
+  double s, q;
+  if (!slab_reduce64(part, nblk, f.C, s, q)) return;
+  fin_bwd(blockIdx.x * 64 + (threadIdx.x & 63), s, q, f);
+}
+
+// Tall slabs in ONE launch: block (cg, split) reduces its rows of 64 channels into out[split][2][C]
+// like slab_split_kernel, then counts its arrival; the last arriving split of channel group cg
+// (device-scope release/acquire) reduces the S rows and runs the finalize for those channels.
+// Deterministic: fixed split ranges, fixed reduction order.  cnt[cg] is reset by the finalizer.
+template <bool BWD>
+__global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __restrict__ part, int nblk,
+                                                               int rows_per, float* __restrict__ out,
+                                                               int* __restrict__ cnt, FinArgs f) {
+  __shared__ double red[2][FIN_G][64];
+  __shared__ int last;
+  const int C = f.C;
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int b0 = blockIdx.y * rows_per, b1 = min(nblk, b0 + rows_per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int i = b0 + rg; i < b1; i += FIN_G) {
+      a += part[(size_t)(2 * i) * C + c];
+      b += part[(size_t)(2 * i + 1) * C + c];
+    }
+  }
+  red[0][rg][cl] = a;
+  red[1][rg][cl] = b;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int g = 1; g < FIN_G; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
+    out[(size_t)(2 * blockIdx.y) * C + c] = (float)a;
+    out[(size_t)(2 * blockIdx.y + 1) * C + c] = (float)b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(cnt + blockIdx.x, 1) == (int)gridDim.y - 1;
+    if (last) __threadfence();
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    cnt[blockIdx.x] = 0;  // ready for the next launch (stream order)
+    if (!BWD && blockIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+  }
+  // second stage over the S split rows (other blocks' rows: nontemporal loads, past this CU's L1)
+  double s2 = 0.0, q2 = 0.0;
+  if (c < C) {
+    for (int i = rg; i < (int)gridDim.y; i += FIN_G) {
+      s2 += __builtin_nontemporal_load(out + (size_t)(2 * i) * C + c);
+      q2 += __builtin_nontemporal_load(out + (size_t)(2 * i + 1) * C + c);
+    }
+  }
+  __syncthreads();
+  red[0][rg][cl] = s2;
+  red[1][rg][cl] = q2;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  for (int g = 1; g < FIN_G; ++g) { s2 += red[0][g][cl]; q2 += red[1][g][cl]; }
+  if (BWD) fin_bwd(c, s2, q2, f);
+  else fin_fwd(c, s2, q2, f);
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
@@ -677,6 +755,7 @@ inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3&
 // Tall slabs (e.g. one row per conv M-tile) are first reduced by a (C/64) x S grid into S rows
 // written just past the slab (callers allocate SLAB_EXTRA_ROWS spare rows), then finalized.
 constexpr int SLAB_EXTRA_ROWS = 64;
+
 inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const float*& fin) {
   fin = part;
   if (nblk <= 256) return nblk;
@@ -686,6 +765,63 @@ inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const f
   hipLaunchKernelGGL(slab_split_kernel, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, C, rows_per, out);
   fin = out;
   return S;
+}
+
+// per-device arrival counters of slab_split_fin_kernel (one per 64-channel group, self-resetting)
+struct FinCounters { int* cnt = nullptr; int n = 0; };
+static FinCounters g_fin_cnt[16];
+static int* fin_counters(int groups) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  FinCounters& w = g_fin_cnt[dev & 15];
+  if (w.n < groups) {
+    const int n = std::max(groups, 128);
+    int* p = nullptr;
+    if (hipMalloc(&p, sizeof(int) * n) != hipSuccess) return nullptr;
+    hipMemset(p, 0, sizeof(int) * n);
+    hipDeviceSynchronize();
+    if (w.cnt) hipFree(w.cnt);
+    w.cnt = p;
+    w.n = n;
+  }
+  return w.cnt;
+}
+
+// finalize a [nblk][2][C] partial slab: one launch (finalize, or split + finalize for tall slabs)
+template <bool BWD>
+inline void slab_finalize(float* part, int nblk, const FinArgs& f, hipStream_t st) {
+  const int C = f.C;
+  int* cnt = nblk > 256 ? fin_counters(cdiv(C, 64)) : nullptr;
+  if (cnt) {
+    const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, 128));
+    const int rows_per = cdiv(nblk, S);
+    float* out = part + (size_t)nblk * 2 * C;
+    hipLaunchKernelGGL(slab_split_fin_kernel<BWD>, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, rows_per,
+                       out, cnt, f);
+    return;
+  }
+  const float* fin = part;
+  const int n = tall_slab_split(part, nblk, C, st, fin);
+  if (BWD) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, n, f);
+  else hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, n, f);
+}
+
+inline FinArgs fin_fwd_args(int M, int C, float eps, float momentum, const float* gamma, const float* beta,
+                            float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                            float* scale, float* shift) {
+  FinArgs f{};
+  f.M = M; f.C = C; f.eps = eps; f.momentum = momentum; f.gamma = gamma; f.beta = beta;
+  f.rmean = rmean; f.rvar = rvar; f.nbt = nbt; f.save_mean = save_mean; f.save_invstd = save_invstd;
+  f.scale = scale; f.shift = shift;
+  return f;
+}
+
+inline FinArgs fin_bwd_args(int M, int C, const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                            float* dbeta, float* coef) {
+  FinArgs f{};
+  f.M = M; f.C = C; f.gamma = gamma; f.mean = mean; f.invstd = invstd; f.dgamma = dgamma; f.dbeta = dbeta;
+  f.coef = coef;
+  return f;
 }
 
 }  // namespace
@@ -712,10 +848,8 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
   } else {
     hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
   }
-  const float* fin = part;
-  nblk = tall_slab_split(part, nblk, C, st, fin);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, eps, momentum,
-                     gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
+  slab_finalize<false>(part, nblk, fin_fwd_args(M, C, eps, momentum, gamma, beta, rmean, rvar, nbt, save_mean,
+                                               save_invstd, scale, shift), st);
   if (!y) return (int)hipGetLastError();  // statistics + coefficients only (the consumer applies them)
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
@@ -744,10 +878,7 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
   slab_launch_dims(M, C, nblk, rpb, grid);
   hipLaunchKernelGGL(bn_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
                      (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
-  const float* fin = part;
-  nblk = tall_slab_split(part, nblk, C, st, fin);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
-                     save_mean, save_invstd, dgamma, dbeta, coef);
+  slab_finalize<true>(part, nblk, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)y, (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
@@ -761,10 +892,7 @@ MI_API int mi_bn_bwd_train_pre(const void* dz, const void* x, void* dx, void* dr
                                const float* save_mean, const float* save_invstd, float* dgamma, float* dbeta,
                                float* coef, float* part, int pre_rows, hipStream_t st) {
   if (C % 8 != 0 || pre_rows <= 0) return (int)hipErrorInvalidValue;
-  const float* fin = part;
-  const int nblk = tall_slab_split(part, pre_rows, C, st, fin);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
-                     save_mean, save_invstd, dgamma, dbeta, coef);
+  slab_finalize<true>(part, pre_rows, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
   int64_t nvec = (int64_t)M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dz, (const bf16_t*)nullptr,
                      (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, 0);
@@ -829,10 +957,7 @@ MI_API int mi_bnpool_bwd(const void* dy, const void* idx, const void* c, void* d
   else
     hipLaunchKernelGGL(bnpool_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const uint8_t*)idx,
                        (const bf16_t*)c, scale, shift, save_mean, part, Nb, H, W, C, P, Q, k, s, pad, rpb);
-  const float* fin = part;
-  nblk = tall_slab_split(part, nblk, C, st, fin);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, nblk, M, C, gamma,
-                     save_mean, save_invstd, dgamma, dbeta, coef);
+  slab_finalize<true>(part, nblk, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
   if (k3) {
     const int total3 = Nb * P * Q * (C / 8);
     hipLaunchKernelGGL(bnpool3_bwd_apply_kernel, dim3(std::min(cdiv(total3, NT), 16384)), dim3(NT), 0, st,

@@ -118,7 +118,8 @@ def build_reducer(force=False, verbose=True):
 
 
 def build_all(force=False, verbose=True):
-    outs = [build_kernels(force, verbose), build_launcher(force, verbose)]
+    # the -DMI_DEBUG library is rebuilt with the release one so the two never diverge in symbols
+    outs = [build_kernels(force, verbose), build_kernels(force, verbose, debug=True), build_launcher(force, verbose)]
     try:
         outs.append(build_comm(force, verbose))
         outs.append(build_reducer(force, verbose))

@@ -40,6 +40,7 @@ CONV_SHAPES = [
     (3, 128, 28, 128, 3, 1, 1),
     (2, 192, 14, 64, 3, 1, 1),
     (2, 64, 50, 128, 3, 1, 1),
+    (3, 64, 17, 64, 3, 1, 1),    # persistent 3x3 wgrad: row blocks crossing image boundaries
 ]
 
 
