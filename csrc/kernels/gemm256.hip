@@ -64,6 +64,7 @@ struct G256Args {
   int full_blocks, tail_split;
   float* ws;
   int* counters;
+  int aux_even;         // epi 3 / 5: accumulated-into gradient defined only at even (h, w) (gemm_conv.hip)
 };
 
 // Wave priority (A/B knob, MI_G256_PRIO): 0 none; 1 static s_setprio 1 for the second-dispatched
@@ -375,12 +376,18 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const int m = m0 + wm * 128 + mq * 64 + rl;
         ok[u] = m < a.M && n < a.N;
         offs[u] = ok[u] ? (size_t)m * a.ldc + n : 0;
+        bool acc_ok = true;
+        if (ok[u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
+          const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
+          const uint32_t h = fdiv(rem, a.fQ), w = rem - h * a.fQ.d;
+          acc_ok = ((h | w) & 1u) == 0u;
+        }
         if (ok[u] && a.epi >= 4) {
-          if (a.epi == 5) cv[u] = *(const uint4*)((const bf16_t*)a.C + offs[u]);
+          if (a.epi == 5) cv[u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[u]) : make_uint4(0, 0, 0, 0);
           if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
           if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
         } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
-          yq[u] = *(const uint4*)(a.aux + offs[u]);
+          yq[u] = acc_ok ? *(const uint4*)(a.aux + offs[u]) : make_uint4(0, 0, 0, 0);
         }
       }
 #pragma unroll
@@ -736,9 +743,21 @@ MI_API int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, i
 // gathered = dy [Nb,H,W,Cs] (H,W = the forward output grid, Cs = forward K), rows = dx pixels
 // [Nb,P,Q], B = wt [N][R][S][Cs].  Cs % 64 == 0.  stats: [2 * cdiv(M, 256)][2][N] partials
 // (forward: sum / sum of squares; epi 4: BN-backward sums).  C bf16 [M][N].
+MI_API int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                            const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
+                            int Q, int R, int S, int stride, int pad, int N, int aux_even, hipStream_t st);
+
 MI_API int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
                            const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
                            int Q, int R, int S, int stride, int pad, int N, hipStream_t st) {
+  return mi_gemm256_conv2(mode, A, B, C, stats, epi, aux, aux2, mean, bn_relu, Nb, H, W, Cs, P, Q, R, S, stride, pad,
+                          N, 0, st);
+}
+
+// as mi_gemm256_conv; aux_even: see G256Args
+MI_API int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                            const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
+                            int Q, int R, int S, int stride, int pad, int N, int aux_even, hipStream_t st) {
   if ((mode != 1 && mode != 2) || Cs % 64 != 0 || N % 8 != 0 || (mode == 2 && stride != 1) ||
       !(epi == 0 || epi == 3 || epi == 4 || epi == 5) || (epi == 3 && !aux) || (epi >= 4 && bn_relu && !aux) ||
       (epi >= 4 && stats && (!aux2 || !mean)))
@@ -747,6 +766,7 @@ MI_API int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, floa
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = nullptr;
   a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu; a.epi = epi;
   a.stats = stats;
+  a.aux_even = aux_even;
   a.M = Nb * P * Q; a.N = N; a.K = R * S * Cs; a.lda = 0; a.ldb = a.K; a.ldc = N;
   a.out_f32 = 0; a.accumulate = 0;
   a.H = H; a.W = W; a.Cs = Cs; a.S = S; a.stride = stride; a.pad = pad;

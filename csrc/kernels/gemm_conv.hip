@@ -62,6 +62,12 @@ struct NTArgs {
   // halo_pb = row blocks per image; fPB / fHW2 divide by halo_pb / (Q + 2)
   int halo_rp, halo_pb;
   FastDiv fPB, fHW2;
+  // mode 3: blockIdx.y -> parity class (empty classes -- no tap reaches them -- can be skipped when
+  // their zero output is not needed); epi 3 / 5 with aux_even: the gradient accumulated into is
+  // defined only at even (h, w) of the row grid (a stride-2 1x1 data gradient written by class
+  // (0, 0) alone) and reads as 0 elsewhere
+  int cls_map[4], ncls;
+  int aux_even;
   ConvGeom g;
 };
 
@@ -129,7 +135,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
   int Mrows = a.M;
   FastDiv fPQ = a.g.fPQ, fQ = a.g.fQ;
   if (a.mode == 3) {
-    cls = blockIdx.y;
+    cls = a.cls_map[blockIdx.y];
     ph = cls / a.g.stride; pw = cls - ph * a.g.stride;
     r0 = (ph + a.g.pad) % a.g.stride; s0 = (pw + a.g.pad) % a.g.stride;
     nr = r0 < a.g.R ? (a.g.R - r0 + a.g.stride - 1) / a.g.stride : 0;
@@ -455,12 +461,22 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
       const int m = m0 + rr + (s0 + u) * RPP;
       ok[u] = m < Mlim && n < a.N;
       offs[u] = ok[u] ? row_off(m) + n : 0;
+      bool acc_ok = true;  // the accumulated-into operand exists at this pixel (aux_even)
+      if (ok[u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
+        if (a.mode == 3) {
+          acc_ok = cls == 0;  // stride-2 parity class (0, 0) = even h, even w
+        } else {
+          const uint32_t img = fdiv((uint32_t)m, a.g.fPQ), rem = (uint32_t)m - img * a.g.fPQ.d;
+          const uint32_t h = fdiv(rem, a.g.fQ), w = rem - h * a.g.fQ.d;
+          acc_ok = ((h | w) & 1u) == 0u;
+        }
+      }
       if (ok[u] && a.epi >= 4) {
-        if (a.epi == 5) cv[u] = *(const uint4*)((const bf16_t*)a.C + offs[u]);
+        if (a.epi == 5) cv[u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[u]) : make_uint4(0, 0, 0, 0);
         if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
         if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
       } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
-        yq[u] = *(const uint4*)(a.aux + offs[u]);
+        yq[u] = acc_ok ? *(const uint4*)(a.aux + offs[u]) : make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -798,10 +814,11 @@ template <int BM, int BN>
 hipError_t launch_nt(NTArgs& a, hipStream_t st) {
   int classes = 1, mrows = a.M;
   if (a.mode == 3) {
-    classes = a.g.stride * a.g.stride;
+    classes = a.ncls;
     mrows = 0;
     const int nimg = a.M / (a.g.P * a.g.Q);
-    for (int c = 0; c < classes; ++c) mrows = std::max(mrows, nimg * a.g.Pc[c] * a.g.Qc[c]);
+    for (int c = 0; c < classes; ++c)
+      mrows = std::max(mrows, nimg * a.g.Pc[a.cls_map[c]] * a.g.Qc[a.cls_map[c]]);
   }
   a.tiles_m = cdiv(mrows, BM);
   if (a.halo_rp > 0) a.tiles_m = (a.M / (a.g.P * a.g.Q)) * a.halo_pb;
@@ -918,6 +935,9 @@ MI_API int mi_set_nt_stages(int stages) {
 // Convolutions with >= 256 output channels and enough 256x256 tiles run on the deep-pipelined
 // kernel (gemm256.hip): forward and stride-1 data gradient (MI355X_DP_GEMM256=0 disables;
 // MI355X_DP_CONV256_MIN_TILES sets the minimum tile count, default 96).
+extern "C" int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                                const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs,
+                                int P, int Q, int R, int S, int stride, int pad, int N, int aux_even, hipStream_t st);
 extern "C" int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
                                const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs,
                                int P, int Q, int R, int S, int stride, int pad, int N, hipStream_t st);
@@ -1036,7 +1056,9 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
       a.g.Qc[c] = (W - pw + 1) / 2;
       a.g.fPQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Pc[c] * a.g.Qc[c]));
       a.g.fQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Qc[c]));
+      a.cls_map[c] = c;
     }
+    a.ncls = 4;
   }
   return (int)dispatch_nt(a, st);
 }
@@ -1060,33 +1082,56 @@ MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int str
 // dx -- the residual-gradient sum of a block input), epi 4 emits dz of the BatchNorm that produced
 // this conv's input (aux = BN output y for the relu mask, aux2 = BN input, mean = its batch
 // mean) plus its backward statistics into `stats` ([mi_dgrad_stat_rows][2][C]).
+MI_API int mi_conv2d_dgrad_ex2(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                               const float* mean, int bn_relu, float* stats, int flags, hipStream_t st);
+
 MI_API int mi_conv2d_dgrad_ex(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
                               const float* mean, int bn_relu, float* stats, hipStream_t st) {
+  return mi_conv2d_dgrad_ex2(dy, wt, dx, Nb, H, W, C, K, R, S, stride, pad, P, Q, epi, aux, aux2, mean, bn_relu, stats,
+                             0, st);
+}
+
+// mi_conv2d_dgrad_ex with flags: bit 0 (stride 2, epi 0) leaves the parity classes no tap reaches
+// unwritten instead of zero-filling them (a 1x1 / stride-2 data gradient then writes only the even
+// pixels); bit 1 (epi 3 / 5) reads the accumulated-into gradient only at even (h, w) -- the
+// consumer of such a sparse write.  Together they skip 3/4 of a downsample dgrad's bytes.
+MI_API int mi_conv2d_dgrad_ex2(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                               const float* mean, int bn_relu, float* stats, int flags, hipStream_t st) {
   if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4 || epi == 5) ||
-      (epi && !aux && bn_relu) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)))
+      (epi && !aux && bn_relu) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)) ||
+      ((flags & 1) && (stride != 2 || epi != 0)) || ((flags & 2) && epi != 3 && epi != 5))
     return (int)hipErrorInvalidValue;
+  const int aux_even = (flags >> 1) & 1;
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
-    return mi_gemm256_conv(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
-                           bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, st);
+    return mi_gemm256_conv2(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
+                            bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
   a.lda = 0; a.ldb = a.K; a.ldc = C; a.mode = 2; a.out_f32 = 0; a.accumulate = 0;
   a.epi = epi; a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu;
   a.stats = (epi >= 4) ? stats : nullptr;
+  a.aux_even = aux_even;
   a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
   a.b_bytes = rsrc_bytes((int64_t)C * a.K);
   a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);
   if (stride == 2) {
     a.mode = 3;
+    a.ncls = 0;
     for (int c = 0; c < 4; ++c) {
       const int ph = c / 2, pw = c % 2;
       a.g.Pc[c] = (H - ph + 1) / 2;
       a.g.Qc[c] = (W - pw + 1) / 2;
       a.g.fPQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Pc[c] * a.g.Qc[c]));
       a.g.fQc[c] = make_fastdiv((uint32_t)std::max(1, a.g.Qc[c]));
+      // flags bit 0: drop the classes no tap reaches (first tap row/column of the class >= R/S)
+      if ((flags & 1) && ((ph + pad) % 2 >= R || (pw + pad) % 2 >= S)) continue;
+      a.cls_map[a.ncls++] = c;
     }
+    if (a.ncls == 0) return (int)hipSuccess;
   }
   return (int)dispatch_nt(a, st);
 }

@@ -66,6 +66,7 @@ signature("mi_conv_stat_rows", I, I, I, I)
 signature("mi_conv_stat_rows_g", I, I, I, I, I, I, I, I, I, I, I)
 signature("mi_gemm256_conv", I, P, P, P, P, I, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_dgrad_ex", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, P)
+signature("mi_conv2d_dgrad_ex2", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P)
 signature("mi_bn_bwd_train_pre", P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)
 signature("mi_set_conv256_min_tiles", I)
 signature("mi_set_conv256_min_k", I)

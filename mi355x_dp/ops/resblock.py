@@ -37,6 +37,9 @@ from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, weight_bf16
 
 F32 = torch.float32
 EPI_ACCUM, EPI_BN_BWD, EPI_ACCUM_BN_BWD = 3, 4, 5
+# mi_conv2d_dgrad_ex2 flags: write only the parity classes some tap reaches (stride 2) / read the
+# accumulated-into gradient only at even (h, w)
+DGRAD_SPARSE, DGRAD_ACC_EVEN = 1, 2
 
 # Cross-block hand-off: the dgrad that completes block k+1's input gradient (residual sum) also
 # applies block k's final relu mask and emits block k's last-BN backward statistics (epilogue 5).
@@ -110,14 +113,14 @@ def _wgrad(x, dy, spec):
     return _finish_grad(spec.w, g)
 
 
-def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0, stats=None):
+def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0, stats=None, flags=0):
     N, C, H, W = x_shape
     K, _, R, S = spec.w.shape
     P, Q = dy.shape[2], dy.shape[3]
     st = stream_of(dy)
     wt = weight_bf16_t(spec.w)
-    _lib.call("mi_conv2d_dgrad_ex", ptr(dy), ptr(wt), ptr(out), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
-              int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), st)
+    _lib.call("mi_conv2d_dgrad_ex2", ptr(dy), ptr(wt), ptr(out), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
+              int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), int(flags), st)
     return out
 
 
@@ -235,11 +238,19 @@ class _ResBlock(torch.autograd.Function):
             dc, gw, gb = _bn_bwd_pre(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
             grads[id(bns[i - 1].w)], grads[id(bns[i - 1].b)] = gw, gb
         grads[id(convs[0].w)] = _wgrad(x, dc, convs[0])
+        acc_flags = 0
         if has_ds:
             dcd, gw, gb = _bn_bwd(dyd, dyd, cd, bns[-1], md, isd, relu=0)
             grads[id(bns[-1].w)], grads[id(bns[-1].b)] = gw, gb
             grads[id(convs[-1].w)] = _wgrad(x, dcd, convs[-1])
-            _dgrad(dcd, convs[-1], x.shape, dx)                            # dx = dgrad_ds
+            ds = convs[-1]
+            if ds.stride == 2 and ds.pad == 0 and ds.w.shape[2] == 1 and ds.w.shape[3] == 1:
+                # 1x1 / stride-2 shortcut: its data gradient lives on the even pixels only -- write
+                # just those and let conv1's dgrad read the sum there (DGRAD_SPARSE / DGRAD_ACC_EVEN)
+                _dgrad(dcd, ds, x.shape, dx, flags=DGRAD_SPARSE)
+                acc_flags = DGRAD_ACC_EVEN
+            else:
+                _dgrad(dcd, ds, x.shape, dx)                               # dx = dgrad_ds
         if ctx.prev_bnsrc is not None:
             # dx = mask_prev * (dx + dgrad_1) + the previous block's last-BN backward statistics
             c_prev, m_prev = ctx.prev_bnsrc
@@ -248,10 +259,10 @@ class _ResBlock(torch.autograd.Function):
             rows = lib.mi_dgrad_stat_rows(N, H, W, C, dc.shape[2], dc.shape[3], convs[0].stride,
                                           convs[0].w.shape[0], convs[0].w.shape[2] * convs[0].w.shape[3])
             slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dx.device)
-            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab)
+            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab, flags=acc_flags)
             _HANDOFF[(dx.data_ptr(), dx.device.index)] = (slab, rows, dx._version, c_prev.data_ptr())
         else:
-            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx)               # dx += dgrad_1
+            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx, flags=acc_flags)   # dx += dgrad_1
         ctx.prev_bnsrc = None
         ctx.out_bnsrc = None
         out = [dx, None, None]

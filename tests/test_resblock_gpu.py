@@ -129,12 +129,27 @@ def test_single_bottleneck_fused_vs_per_op(inpl, planes, stride, ds, size):
         assert rel_err(b1[n], b0[n]) < 1e-4, n
 
 
-def test_block_chain_handoff_matches_per_op():
+@pytest.mark.parametrize("force256", [False, True])
+def test_block_chain_handoff_matches_per_op(force256):
     """three consecutive fused blocks (identity, downsample, identity): the cross-block hand-off
-    (epilogue 5) is used and gradients match the per-op path"""
+    (epilogue 5) is used and gradients match the per-op path.  The stride-2 shortcut's dgrad writes
+    only the even pixels and conv1's dgrad reads the sum there only; force256 runs those dgrads on
+    the 256x256 pipeline (its even-pixel epilogue) instead of the 128-tile kernel."""
     import mi355x_dp.models.resnet as R
     from mi355x_dp.models.layers import BatchNorm2d
-    from mi355x_dp.ops import resblock
+    from mi355x_dp.ops import _lib, resblock
+    lib = _lib.load()
+    if force256:
+        lib.mi_set_conv256_min_tiles(1)
+        lib.mi_set_conv256_min_k(0)
+    try:
+        _chain_handoff(R, BatchNorm2d, resblock)
+    finally:
+        lib.mi_set_conv256_min_tiles(96)
+        lib.mi_set_conv256_min_k(512)
+
+
+def _chain_handoff(R, BatchNorm2d, resblock):
     g = torch.Generator(device="cuda").manual_seed(2)
     x0 = torch.randn(16, 256, 28, 28, device="cuda", generator=g).to(torch.bfloat16)
     x0 = x0.contiguous(memory_format=torch.channels_last)
