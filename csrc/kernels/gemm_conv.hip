@@ -80,6 +80,7 @@ struct TNArgs {
   int mode;
   int k_per_split;
   int a_bytes, b_bytes;
+  float* colsum;    // optional [M] fp32 += column sums of A (a Linear layer's bias gradient)
   ConvGeom g;
 };
 
@@ -649,6 +650,15 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  // fused bias gradient: the first column-tile's blocks also reduce their A fragments against a
+  // ones operand (one extra MFMA per 16 rows in the wn == 0 waves): D[m][*] = sum_k A[k][m]
+  const bool do_cs = a.colsum != nullptr && (tile % nbn) == 0 && wn == 0;
+  f32x4 acc_cs[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) acc_cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  short ones_s __attribute__((ext_vector_type(8))) = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                      0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_s);
   auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -676,6 +686,10 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_cs) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) acc_cs[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, acc_cs[i], 0, 0, 0);
+      }
     }
   };
 
@@ -718,6 +732,15 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
         else atomicAdd(dst, acc[i][j][r]);
       }
     }
+  }
+  if (do_cs && li == 0) {  // every column of the ones-product holds the sum; lane li == 0 adds it
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + 16 * i + 4 * g + r;
+        if (m < a.M) atomicAdd(a.colsum + m, acc_cs[i][r]);
+      }
   }
 }
 
@@ -1237,6 +1260,21 @@ MI_API int mi_gemm_tn(const void* A, const void* B, float* C, int M, int N, int 
   if (lda % 8 == 0 && ldb % 8 == 0 && use_gemm256_tn(M, N, K)) return mi_gemm256_tn(A, B, C, M, N, K, lda, ldb, ldc, st);
   TNArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.mode = 0;
+  a.a_bytes = rsrc_bytes((int64_t)K * lda);
+  a.b_bytes = rsrc_bytes((int64_t)K * ldb);
+  a.g = make_geom(1, 1, 64, 1, 1, 1, 1, 0);
+  return (int)dispatch_tn(a, st);
+}
+
+// mi_gemm_tn that also adds the column sums of A (sum over K of A[k][m], i.e. a Linear layer's
+// bias gradient from its output gradient) into colsum[M] fp32 -- one extra MFMA per A fragment in
+// the first column tile instead of a separate pass over A.  Always the 128-tile split-K kernel.
+MI_API int mi_gemm_tn_bias(const void* A, const void* B, float* C, float* colsum, int M, int N, int K, int lda,
+                           int ldb, int ldc, hipStream_t st) {
+  if (M % 8 != 0 || N % 8 != 0 || !colsum) return (int)hipErrorInvalidValue;
+  TNArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.colsum = colsum;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.mode = 0;
   a.a_bytes = rsrc_bytes((int64_t)K * lda);
   a.b_bytes = rsrc_bytes((int64_t)K * ldb);

@@ -61,6 +61,15 @@ def weight_bf16_t(w: torch.Tensor) -> torch.Tensor:
     return wt
 
 
+def linear_weight_t(w: torch.Tensor) -> torch.Tensor:
+    """Linear data-gradient operand W^T [in][out] (bf16): the flat engine's cached transpose
+    (refreshed once per optimizer step) or a fresh one."""
+    wt = getattr(w, "_mi_bf16_t", None)
+    if wt is not None and wt.dim() == 2:
+        return wt
+    return weight_bf16(w).t().contiguous()
+
+
 def _flat(p) -> bool:
     return p is not None and getattr(p, "_mi_flat", False) and p.grad is not None
 
@@ -405,7 +414,7 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             # dX[M][Kd] = dY[M][Np] * W[Np][Kd]  ->  NT with B = W^T [Kd][Np]
-            wt = w16.t().contiguous()
+            wt = linear_weight_t(weight) if Np == N else w16.t().contiguous()
             dxf = torch.empty((M, Kd), dtype=BF16, device=dy.device)
             _lib.call("mi_gemm_nt", ptr(dy2), ptr(wt), ptr(dxf), ptr(None), ptr(None), M, Kd, Np, Np, Np, Kd, 0, 0, st)
             dx = dxf.reshape(ctx.in_shape).to(ctx.in_dtype)

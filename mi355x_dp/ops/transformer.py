@@ -5,16 +5,18 @@
 with an explicit backward, so every elementwise op rides on a kernel that runs anyway:
 
   forward                                   backward
-  ln_1            mi_layernorm_fwd          dz -> fc2: colsum(db2), TN(dW2), NT+gelu' epilogue -> du
-  qkv = h1 Wqkvᵀ  NT (+bias)                du -> fc1: colsum, TN, NT -> dh2
+  ln_1            mi_layernorm_fwd          dz -> fc2: TN(dW2 + db2), NT+gelu' epilogue -> du
+  qkv = h1 Wqkvᵀ  NT (+bias)                du -> fc1: TN(dW1 + db1), NT -> dh2
   attention       attention kernel          dy = dz + ln_2ᵀ(dh2)       (LN bwd, residual add fused)
-  y = x + o Woᵀ   NT, residual epilogue     dy -> proj: colsum, TN, NT -> do -> attention bwd -> dqkv
-  ln_2            mi_layernorm_fwd          dqkv -> colsum, TN, NT -> dh1
+  y = x + o Woᵀ   NT, residual epilogue     dy -> proj: TN(+bias), NT -> do -> attention bwd -> dqkv
+  ln_2            mi_layernorm_fwd          dqkv -> TN(+bias), NT -> dh1
   g = gelu(h2W1ᵀ) NT, GELU epilogue         dx = dy + ln_1ᵀ(dh1)       (LN bwd, residual add fused)
   z = y + g W2ᵀ   NT, residual epilogue
 
 No torch elementwise kernels, no autograd-inserted residual-gradient adds, and the bias
-gradients are column sums of the bf16 gradient (never a fp32 copy).  Weight gradients go
+gradients are column sums of the bf16 gradient computed by the weight-gradient GEMM itself (an
+extra MFMA against a ones operand on fragments it already holds -- no second pass over dY).
+The data-gradient GEMMs read the flat engine's cached transposed weights.  Weight gradients go
 straight into the flat fp32 gradient buffer of the DP engine (``functional._grad_buffer``).
 
 Reference: the ViT-B/16 config is a BASELINE.json target (config 5), not part of the
@@ -28,7 +30,7 @@ import torch.nn.functional as F
 from . import _lib
 from . import kernels as _k  # noqa: F401
 from ._lib import ptr, stream_of
-from .functional import BF16, _finish_grad, _grad_buffer, weight_bf16
+from .functional import BF16, _finish_grad, _grad_buffer, linear_weight_t, weight_bf16
 
 F32 = torch.float32
 EPI_NONE, EPI_GELU, EPI_GELU_BWD, EPI_RESIDUAL = 0, 1, 2, 3
@@ -67,24 +69,19 @@ def _gemm(a2, w16, bias=None, epi=EPI_NONE, aux=None):
     return (out, aux) if epi == EPI_GELU else out
 
 
-def _wgrad(weight, dy2, x2):
-    g = _grad_buffer(weight)
+def _wbgrad(weight, bias, dy2, x2):
+    """weight AND bias gradient from one TN GEMM (the bias column sums ride on its A fragments)."""
+    g, gb = _grad_buffer(weight), _grad_buffer(bias)
     M, N = dy2.shape
     K = x2.shape[1]
-    _lib.call("mi_gemm_tn", ptr(dy2), ptr(x2), ptr(g), N, K, M, N, K, K, stream_of(dy2))
-    return _finish_grad(weight, g)
+    _lib.call("mi_gemm_tn_bias", ptr(dy2), ptr(x2), ptr(g), ptr(gb), N, K, M, N, K, K, stream_of(dy2))
+    return _finish_grad(weight, g), _finish_grad(bias, gb)
 
 
-def _bgrad(bias, dy2):
-    g = _grad_buffer(bias)
-    M, N = dy2.shape
-    _lib.call("mi_colsum_bf16", ptr(dy2), ptr(g), M, N, N, stream_of(dy2))
-    return _finish_grad(bias, g)
-
-
-def _dgrad(dy2, w16, epi=EPI_NONE, aux=None):
-    """dX[M][K] = dY[M][N] · W[N][K] (NT against the transposed bf16 weight)."""
-    return _gemm(dy2, w16.t().contiguous(), None, epi, aux)
+def _dgrad(dy2, weight, epi=EPI_NONE, aux=None):
+    """dX[M][K] = dY[M][N] · W[N][K] (NT against the transposed bf16 weight, cached by the flat
+    engine once per optimizer step)."""
+    return _gemm(dy2, linear_weight_t(weight), None, epi, aux)
 
 
 # ------------------------------------------------------------------ attention
@@ -196,22 +193,18 @@ class _EncoderLayer(torch.autograd.Function):
             dz2 = dz2.to(BF16)
         dz2 = dz2.contiguous()
         # MLP
-        d_b2 = _bgrad(b2, dz2)
-        d_w2 = _wgrad(w2, dz2, g)
-        du = _dgrad(dz2, weight_bf16(w2), EPI_GELU_BWD, u)
-        d_b1 = _bgrad(b1, du)
-        d_w1 = _wgrad(w1, du, h2)
-        dh2 = _dgrad(du, weight_bf16(w1))
+        d_w2, d_b2 = _wbgrad(w2, b2, dz2, g)
+        du = _dgrad(dz2, w2, EPI_GELU_BWD, u)
+        d_w1, d_b1 = _wbgrad(w1, b1, du, h2)
+        dh2 = _dgrad(du, w1)
         dy, d_ln2w, d_ln2b = _ln_bwd(dh2, y, ln2w, ln2b, m2, r2, dres=dz2)
         # attention
-        d_bo = _bgrad(bo, dy)
-        d_wo = _wgrad(wo, dy, o)
-        do = _dgrad(dy, weight_bf16(wo))
+        d_wo, d_bo = _wbgrad(wo, bo, dy, o)
+        do = _dgrad(dy, wo)
         dqkv = _attn_bwd(ctx.attn, qkv, do, B, T, heads)
         ctx.attn = None
-        d_bqkv = _bgrad(bqkv, dqkv)
-        d_wqkv = _wgrad(wqkv, dqkv, h1)
-        dh1 = _dgrad(dqkv, weight_bf16(wqkv))
+        d_wqkv, d_bqkv = _wbgrad(wqkv, bqkv, dqkv, h1)
+        dh1 = _dgrad(dqkv, wqkv)
         dx, d_ln1w, d_ln1b = _ln_bwd(dh1, x2, ln1w, ln1b, m1, r1, dres=dy)
         dx = dx.view(B, T, D)
         if ctx.in_dtype != BF16:

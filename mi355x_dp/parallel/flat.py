@@ -77,10 +77,11 @@ class FlatParams:
         self._init_transposed()
 
     def _init_transposed(self):
-        """Conv-dgrad operands: every kernel-layout conv weight [K][R][S][C] also kept transposed as
-        [C][R][S][K] in a second bf16 buffer (same offsets), rebuilt for ALL convs by ONE kernel
-        launch whenever the bf16 copy changes (``refresh_transposed``), instead of one transpose
-        per conv per backward.  Attached as ``p._mi_bf16_t``; GPU + native kernels only."""
+        """Data-gradient operands: every kernel-layout conv weight [K][R][S][C] also kept transposed
+        as [C][R][S][K], and every Linear weight [N][K] as [K][N], in a second bf16 buffer (same
+        offsets), rebuilt for ALL of them by ONE kernel launch whenever the bf16 copy changes
+        (``refresh_transposed``), instead of one transpose per layer per backward.  Attached as
+        ``p._mi_bf16_t``; GPU + native kernels only."""
         self.bf16_t = None
         if self.bf16 is None or self.device.type != "cuda":
             return
@@ -89,21 +90,31 @@ class FlatParams:
             return
         desc, blk = [], 0
         for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
-            if p.dim() != 4 or not kl:
-                continue
-            K, C, R, S = p.shape
-            desc.append([o, o, K, R * S, C, blk])
-            blk += R * S * ((K + 63) // 64) * ((C + 63) // 64)
+            if self._transposed(p, kl):
+                K, C, R, S = p.shape if p.dim() == 4 else (p.shape[0], p.shape[1], 1, 1)
+                desc.append([o, o, K, R * S, C, blk])
+                blk += R * S * ((K + 63) // 64) * ((C + 63) // 64)
         if not desc:
             return
         self.bf16_t = torch.zeros_like(self.bf16)
         self._wt_desc = torch.tensor(desc, dtype=torch.int32, device=self.device)
         self._wt_blocks = blk
         for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
-            if p.dim() == 4 and kl:
-                K, C, R, S = p.shape
-                p._mi_bf16_t = self.bf16_t[o:o + p.numel()].view(C, R, S, K)
+            if self._transposed(p, kl):
+                if p.dim() == 4:
+                    K, C, R, S = p.shape
+                    p._mi_bf16_t = self.bf16_t[o:o + p.numel()].view(C, R, S, K)
+                else:  # Linear weight [out][in] -> W^T [in][out], the data-gradient GEMM operand
+                    p._mi_bf16_t = self.bf16_t[o:o + p.numel()].view(p.shape[1], p.shape[0])
         self.refresh_transposed()
+
+    @staticmethod
+    def _transposed(p, kernel_layout) -> bool:
+        """kernel-layout conv weights and Linear weights (both dims multiples of 8) get a cached
+        transposed bf16 copy."""
+        if p.dim() == 4:
+            return kernel_layout
+        return p.dim() == 2 and p.shape[0] % 8 == 0 and p.shape[1] % 8 == 0
 
     def refresh_transposed(self):
         if getattr(self, "bf16_t", None) is None:
