@@ -18,6 +18,7 @@
 // Reference op: torchvision resnet conv1 (cifar10-distributed-smddp-gpu.py:30-32 via resnet18).
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -371,7 +372,17 @@ constexpr size_t stem_lds_bytes() {
   return (size_t)(NRING * ROWPX) * 16 + 8 * 2 * KOUT * 4;
 }
 
-inline int stem_blocks(int total_pairs) { return std::max(1, std::min(total_pairs, MAX_BLOCKS)); }
+// Blocks of the persistent stem kernels: MAX_BLOCKS = one per CU by default.  MI355X_DP_STEM_BLOCKS
+// raises it (e.g. 512: half-image row ranges, so CUs shared with concurrent RCCL kernels during
+// the overlapped gradient all-reduce hold back less of the work).
+static int g_stem_blocks = -1;
+inline int stem_blocks(int total_pairs) {
+  if (g_stem_blocks < 0) {
+    const char* e = std::getenv("MI355X_DP_STEM_BLOCKS");
+    g_stem_blocks = e ? std::max(1, std::atoi(e)) : MAX_BLOCKS;
+  }
+  return std::max(1, std::min(total_pairs, g_stem_blocks));
+}
 
 }  // namespace
 

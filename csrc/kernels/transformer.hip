@@ -3,6 +3,8 @@
 // fp32 statistics / parameters / gradients.  The GEMMs themselves (QKV, projections, MLP with
 // fused GELU and residual epilogues) are the MFMA kernels of gemm_conv.hip.
 #include "common.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -189,7 +191,12 @@ MI_API int mi_layernorm_fwd(const void* x, const float* w, const float* b, void*
 MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
                             const void* dres, void* dx, float* dw, float* db, int M, int D, hipStream_t st) {
   if (D % 4 != 0 || D > 64 * 4 * LN_MAXV || M <= 0) return (int)hipErrorInvalidValue;
-  const int blocks = min(cdiv(M, 4), 1024);
+  static int max_blocks = -1;  // MI355X_DP_LN_BWD_BLOCKS: rows in flight vs dW/dB atomics per block
+  if (max_blocks < 0) {
+    const char* e = std::getenv("MI355X_DP_LN_BWD_BLOCKS");
+    max_blocks = e ? std::max(1, std::atoi(e)) : 1024;
+  }
+  const int blocks = min(cdiv(M, 4), max_blocks);
   const size_t lds = (size_t)4 * D * sizeof(float);
 #define MI_LN_BWD(V)                                                                                    \
   case V:                                                                                               \
