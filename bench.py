@@ -36,7 +36,7 @@ def parse():
     p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--num-classes", type=int, default=1000)
-    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--lr", type=float, default=0.01)  # reference hyperparameter (nb2:110)
     p.add_argument("--backend", default=os.environ.get("MI355X_DP_BACKEND", "nccl"))
     p.add_argument("--bucket-mb", type=float, default=None)
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")

@@ -195,10 +195,16 @@ struct EwIter {
   }
 };
 
-// y = act(x*scale + shift (+ res)); grid-stride over 8-element vectors
-__global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                                      bf16_t* __restrict__ y, const float* __restrict__ scale,
-                                                      const float* __restrict__ shift, int64_t nvec, int C, int relu) {
+// y = act(x*scale + shift (+ res)); grid-stride over 8-element vectors.  RES_BN: the residual is
+// itself a raw BN input, normalised on the fly (res*rscale + rshift) -- the downsample branch's
+// BatchNorm output is never stored (ResNet projection shortcut).
+template <bool RES_BN>
+__global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                        bf16_t* __restrict__ y, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ rscale,
+                                                        const float* __restrict__ rshift, int64_t nvec, int C,
+                                                        int relu) {
   for (EwIter it(nvec, C); it.v0 < nvec; it.next(C)) {
     uint4 xv[EW_U], rv[EW_U];
 #pragma unroll
@@ -223,6 +229,15 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const bf16_t* __restrict__
       if (res) {
         float r[8];
         unpack8(rv[u], r);
+        if (RES_BN) {
+          const float4 p0 = *(const float4*)(rscale + c), p1 = *(const float4*)(rscale + c + 4);
+          const float4 q0 = *(const float4*)(rshift + c), q1 = *(const float4*)(rshift + c + 4);
+          r[0] = r[0] * p0.x + q0.x; r[1] = r[1] * p0.y + q0.y; r[2] = r[2] * p0.z + q0.z; r[3] = r[3] * p0.w + q0.w;
+          r[4] = r[4] * p1.x + q1.x; r[5] = r[5] * p1.y + q1.y; r[6] = r[6] * p1.z + q1.z; r[7] = r[7] * p1.w + q1.w;
+          // round like a stored bf16 shortcut activation: bit-identical to the unfused sequence
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = bf2f(f2bf(r[j]));
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] += r[j];
       }
@@ -852,8 +867,21 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
                                                save_invstd, scale, shift), st);
   if (!y) return (int)hipGetLastError();  // statistics + coefficients only (the consumer applies them)
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
-                     (bf16_t*)y, scale, shift, nvec, C, relu);
+  hipLaunchKernelGGL(bn_apply_kernel_t<false>, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x,
+                     (const bf16_t*)res, (bf16_t*)y, scale, shift, (const float*)nullptr, (const float*)nullptr, nvec,
+                     C, relu);
+  return (int)hipGetLastError();
+}
+
+// y = act(x*scale + shift + res*rscale + rshift): a block's last BatchNorm (coefficients from
+// mi_bn_fwd_train with y = null) fused with its projection shortcut's BatchNorm applied to the raw
+// shortcut conv output -- one pass, the shortcut's normalised activation never written.
+MI_API int mi_bn_apply_dual(const void* x, const void* res, void* y, int M, int C, const float* scale,
+                            const float* shift, const float* rscale, const float* rshift, int relu, hipStream_t st) {
+  if (C % 8 != 0 || !x || !res || !y) return (int)hipErrorInvalidValue;
+  int64_t nvec = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel_t<true>, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x,
+                     (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu);
   return (int)hipGetLastError();
 }
 
@@ -864,8 +892,9 @@ MI_API int mi_bn_fwd_eval(const void* x, const void* res, void* y, int M, int C,
   hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, C, eps, gamma, beta, rmean, rvar,
                      scale, shift);
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x, (const bf16_t*)res,
-                     (bf16_t*)y, scale, shift, nvec, C, relu);
+  hipLaunchKernelGGL(bn_apply_kernel_t<false>, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x,
+                     (const bf16_t*)res, (bf16_t*)y, scale, shift, (const float*)nullptr, (const float*)nullptr, nvec,
+                     C, relu);
   return (int)hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ signature("mi_gemm_tn_bias", P, P, P, P, I, I, I, I, I, I, P)
 signature("mi_bn_partial_rows", I, I)
 signature("mi_bn_slab_extra_rows")
 signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, I, I, P)
+signature("mi_bn_apply_dual", P, P, P, I, I, P, P, P, P, I, P)
 signature("mi_bn_fwd_eval", P, P, P, I, I, F, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_train", P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_eval", P, P, P, P, P, I, I, I, P)

@@ -21,8 +21,9 @@ With the block as one node the backward is scheduled explicitly:
   the previous block's final relu mask + its last-BN backward statistics, handed over so the
   previous block skips its statistics pass and uses the buffer as its residual gradient.
 
-Forward is the same kernel sequence as the per-op path (conv epilogue emits the BN forward
-statistics, BN apply fuses residual + ReLU).  Weight gradients go into the flat fp32 gradient
+Forward is the per-op kernel sequence (conv epilogue emits the BN forward statistics, BN apply
+fuses residual + ReLU), except that a projection shortcut's BatchNorm is applied inside the last
+BN's pass (``mi_bn_apply_dual``) instead of being written out and re-read as the residual.  Weight gradients go into the flat fp32 gradient
 buffer of the DP engine.  Reference: torchvision BasicBlock / Bottleneck semantics, reached by
 the reference through ``torchvision.models.resnet18`` (cifar10-distributed-smddp-gpu.py:30-32).
 """
@@ -88,10 +89,12 @@ def _conv_fwd_stats(x, spec):
     return y, slab, rows
 
 
-def _bn_fwd(c, slab, rows, bn, relu, res=None):
+def _bn_fwd(c, slab, rows, bn, relu, res=None, apply=True):
+    """BN forward from conv-epilogue statistics.  ``apply=False``: statistics, running-stat update and
+    (scale, shift) only -- returns (None, mean, invstd, scale, shift) for a fused consumer."""
     N, C, H, W = c.shape
     dev = c.device
-    y = torch.empty_like(c, memory_format=CL)
+    y = torch.empty_like(c, memory_format=CL) if apply else None
     mean = torch.empty(C, dtype=F32, device=dev)
     invstd = torch.empty(C, dtype=F32, device=dev)
     scale = torch.empty(C, dtype=F32, device=dev)
@@ -99,7 +102,21 @@ def _bn_fwd(c, slab, rows, bn, relu, res=None):
     _lib.call("mi_bn_fwd_train", ptr(c), ptr(res), ptr(y), N * H * W, C, bn.eps, bn.momentum, ptr(bn.w), ptr(bn.b),
               ptr(bn.rm), ptr(bn.rv), ptr(bn.nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(slab),
               int(rows), int(relu), stream_of(c))
+    if not apply:
+        return None, mean, invstd, scale, shift
     return y, mean, invstd
+
+
+def _bn_fwd_dual(c, slab, rows, bn, cd, slabd, rowsd, bnd):
+    """A block's last BN + ReLU with the projection shortcut's BN folded into the same pass:
+    y = relu(bn(c) + bn_d(cd)) -- the shortcut's normalised activation is never materialised."""
+    _, md, isd, sd, hd = _bn_fwd(cd, slabd, rowsd, bnd, relu=False, apply=False)
+    _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bn, relu=True, apply=False)
+    N, C, H, W = c.shape
+    y = torch.empty_like(c, memory_format=CL)
+    _lib.call("mi_bn_apply_dual", ptr(c), ptr(cd), ptr(y), N * H * W, C, ptr(sc), ptr(sh), ptr(sd), ptr(hd), 1,
+              stream_of(c))
+    return y, m, inv, md, isd
 
 
 # ---------------------------------------------------------------------- backward pieces
@@ -183,11 +200,9 @@ class _ResBlock(torch.autograd.Function):
             if last:
                 if has_ds:
                     cd, slabd, rowsd = _conv_fwd_stats(x, convs[-1])
-                    yd, md, isd = _bn_fwd(cd, slabd, rowsd, bns[-1], relu=False)
-                    res = yd
+                    y, m, inv, md, isd = _bn_fwd_dual(c, slab, rows, bns[i], cd, slabd, rowsd, bns[-1])
                 else:
-                    res = x
-                y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True, res=res)
+                    y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True, res=x)
             else:
                 y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True)
             saved_c.append(c); saved_y.append(y); saved_m.append(m); saved_i.append(inv)
