@@ -9,6 +9,9 @@
 namespace {
 
 constexpr int LN_MAXV = 8;  // 4-element (8-byte) vectors per lane: D <= 64 * 4 * 8 = 2048
+#ifndef MI_LN_BWD_RW
+#define MI_LN_BWD_RW 2  // LayerNorm backward rows in flight per wave (D <= 1024); A/B knob
+#endif
 
 __device__ __forceinline__ void load4(const bf16_t* p, float* f) {
   const uint2 v = *(const uint2*)p;
@@ -86,43 +89,68 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 4; ++e) { pw[i][e] = 0.f; pb[i][e] = 0.f; }
 
-  for (int row = blockIdx.x * 4 + wv; row < M; row += gridDim.x * 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    const bf16_t* dyr = dy + (size_t)row * D;
-    const bf16_t* xr = x + (size_t)row * D;
-    float xh[LN_V][4], g[LN_V][4];
-    float s1 = 0.f, s2 = 0.f;
+  // A wave owns RW adjacent rows per iteration and issues every load of them (dy, x and the
+  // residual gradient, kept packed) before the first cross-lane reduction: 2x the bytes in
+  // flight of a row-at-a-time loop, and the dres read no longer waits behind the reductions.
+  constexpr int RW = LN_V <= 4 ? MI_LN_BWD_RW : 1;
+  for (int row0 = (blockIdx.x * 4 + wv) * RW; row0 < M; row0 += gridDim.x * 4 * RW) {
+    uint2 qd[RW][LN_V], qx[RW][LN_V], qr[RW][LN_V];
+    float mean[RW], rstd[RW];
 #pragma unroll
-    for (int i = 0; i < LN_V; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nv) {
-        float d[4];
-        load4(dyr + 4 * c, d);
-        load4(xr + 4 * c, xh[i]);
-        const float4 wq = *(const float4*)(w + 4 * c);
-        const float wa[4] = {wq.x, wq.y, wq.z, wq.w};
+    for (int r = 0; r < RW; ++r) {
+      const int row = row0 + r;
+      if (row < M) {
+        mean[r] = mean_in[row];
+        rstd[r] = rstd_in[row];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xh[i][e] = (xh[i][e] - mean) * rstd;
-          g[i][e] = d[e] * wa[e];
-          s1 += g[i][e];
-          s2 += g[i][e] * xh[i][e];
-          pw[i][e] += d[e] * xh[i][e];
-          pb[i][e] += d[e];
+        for (int i = 0; i < LN_V; ++i) {
+          const int c = lane + 64 * i;
+          if (c < nv) {
+            qd[r][i] = *(const uint2*)(dy + (size_t)row * D + 4 * c);
+            qx[r][i] = *(const uint2*)(x + (size_t)row * D + 4 * c);
+            qr[r][i] = dres ? *(const uint2*)(dres + (size_t)row * D + 4 * c) : make_uint2(0u, 0u);
+          }
         }
       }
     }
-    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
-    bf16_t* dxr = dx + (size_t)row * D;
 #pragma unroll
-    for (int i = 0; i < LN_V; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nv) {
-        float o[4], r[4] = {0.f, 0.f, 0.f, 0.f};
-        if (dres) load4(dres + (size_t)row * D + 4 * c, r);
+    for (int r = 0; r < RW; ++r) {
+      const int row = row0 + r;
+      if (row >= M) break;
+      float xh[LN_V][4], g[LN_V][4];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = r[e] + rstd * (g[i][e] - m1 - xh[i][e] * m2);
-        store4(dxr + 4 * c, o);
+      for (int i = 0; i < LN_V; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nv) {
+          float d[4];
+          load4((const bf16_t*)&qd[r][i], d);
+          load4((const bf16_t*)&qx[r][i], xh[i]);
+          const float4 wq = *(const float4*)(w + 4 * c);
+          const float wa[4] = {wq.x, wq.y, wq.z, wq.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xh[i][e] = (xh[i][e] - mean[r]) * rstd[r];
+            g[i][e] = d[e] * wa[e];
+            s1 += g[i][e];
+            s2 += g[i][e] * xh[i][e];
+            pw[i][e] += d[e] * xh[i][e];
+            pb[i][e] += d[e];
+          }
+        }
+      }
+      const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+      bf16_t* dxr = dx + (size_t)row * D;
+#pragma unroll
+      for (int i = 0; i < LN_V; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nv) {
+          float o[4], rv[4];
+          load4((const bf16_t*)&qr[r][i], rv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = rv[e] + rstd[r] * (g[i][e] - m1 - xh[i][e] * m2);
+          store4(dxr + 4 * c, o);
+        }
       }
     }
   }
@@ -191,16 +219,34 @@ MI_API int mi_layernorm_fwd(const void* x, const float* w, const float* b, void*
 MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
                             const void* dres, void* dx, float* dw, float* db, int M, int D, hipStream_t st) {
   if (D % 4 != 0 || D > 64 * 4 * LN_MAXV || M <= 0) return (int)hipErrorInvalidValue;
-  static int max_blocks = -1;  // MI355X_DP_LN_BWD_BLOCKS: rows in flight vs dW/dB atomics per block
-  if (max_blocks < 0) {
+  // Grid-stride kernel: launch at most one resident wave of blocks (CUs x occupancy, per LN_V
+  // instantiation), so no block waits for a slot while the others already stride past its rows.
+  // MI355X_DP_LN_BWD_BLOCKS overrides (rows in flight vs dW/dB atomics per block).
+  static int env_blocks = -2, resident[LN_MAXV + 1] = {0};
+  if (env_blocks == -2) {
     const char* e = std::getenv("MI355X_DP_LN_BWD_BLOCKS");
-    max_blocks = e ? std::max(1, std::atoi(e)) : 1024;
+    env_blocks = e ? std::max(1, std::atoi(e)) : -1;
   }
-  const int blocks = min(cdiv(M, 4), max_blocks);
   const size_t lds = (size_t)4 * D * sizeof(float);
+  const int nvec = cdiv(D, 256);
+  auto cap = [&](const void* fn) {
+    if (env_blocks > 0) return env_blocks;
+    if (resident[nvec] == 0) {
+      int dev = 0, cus = 256, per_cu = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+      resident[nvec] = cus * per_cu;
+    }
+    return resident[nvec];
+  };
+  const int rw = nvec <= 4 ? MI_LN_BWD_RW : 1;
 #define MI_LN_BWD(V)                                                                                    \
   case V:                                                                                               \
-    hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(blocks), dim3(256), lds, st, (const bf16_t*)dy,            \
+    hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(min(cdiv(M, 4 * rw), cap((const void*)ln_bwd_kernel<V>))),  \
+                       dim3(256), lds, st, (const bf16_t*)dy,                                            \
                        (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, dw, db, M, D);  \
     break;
   switch (cdiv(D, 256)) {
