@@ -47,6 +47,9 @@ def parse():
 
 def main():
     args = parse()
+    if os.environ.get("MI355X_DP_BENCH_STACKS"):  # hang diagnosis: every rank dumps its Python stacks
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["MI355X_DP_BENCH_STACKS"]), repeat=True, file=sys.stderr)
     if args.graph and args.warmup < 2:
         args.warmup = 2  # the graph is captured during warmup, never inside the timed region
     import torch
@@ -132,6 +135,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     last_loss = float(loss.detach())
+    replicas_ok = None
+    if world > 1:  # after the timed region: every rank's flat fp32 master weights bit-identical?
+        from mi355x_dp.parallel.health import ReplicaChecker, ReplicaDivergence
+        try:
+            replicas_ok = ReplicaChecker(engine)(force=True)
+        except ReplicaDivergence as e:
+            print(f"[bench] {e}", file=sys.stderr)
+            replicas_ok = False
 
     for i in range(args.profile_steps):
         step(10_000 + i)
@@ -170,6 +181,7 @@ def main():
             "loss_first_warmup": round(first_loss, 4),
             "loss_last": round(last_loss, 4),
             "warmup_s": round(t_w1 - t_w0, 2),
+            "replicas_identical": replicas_ok,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -211,3 +211,4 @@ def test_bench_two_ranks_torchrun_gloo():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 64 and out["value"] > 0
+    assert out["replicas_identical"] is True
