@@ -59,6 +59,26 @@ class CIFAR10(VisionDataset):
             target = self.target_transform(target)
         return img, target
 
+    def __getitems__(self, indices):
+        """Batched fetch used by DataLoader auto-collation: the whole batch is transformed
+        with a few vectorised ops (transforms.batch_apply) instead of one PIL round trip per
+        image; falls back to per-image __getitem__ for pipelines it does not recognise."""
+        return _batched_items(self, self.data, indices)
+
+
+def _batched_items(ds, data, indices):
+    from torchvision import transforms as _T
+    idx = np.asarray(indices, dtype=np.int64)
+    batch = None
+    if ds.transform is not None and ds.target_transform is None and len(idx):
+        cache = ds.__dict__.setdefault("_batch_cache", {})
+        batch = _T.batch_apply(ds.transform, (data, idx), cache=cache)
+    if batch is None:
+        return [ds[int(i)] for i in idx]
+    tg = ds.targets
+    labels = [int(tg[int(i)]) for i in idx]
+    return list(zip(batch.unbind(0), labels))
+
 
 def _read_idx(path):
     op = gzip.open if path.endswith(".gz") else open
@@ -123,3 +143,6 @@ class MNIST(VisionDataset):
         if self.target_transform is not None:
             target = self.target_transform(target)
         return img, target
+
+    def __getitems__(self, indices):
+        return _batched_items(self, self.data, indices)

@@ -166,3 +166,84 @@ class Lambda:
 
     def __call__(self, x):
         return self.fn(x)
+
+
+def batch_apply(transform, images, cache=None):
+    """Vectorised form of ``transform`` over a whole batch of uint8 HWC images.
+
+    The reference's input path (cifar10-distributed-smddp-gpu.py:55-62,70-87) runs
+    RandomCrop(pad) -> RandomHorizontalFlip -> ToTensor -> Normalize once per image in the
+    DataLoader's main process (``num_workers=0``), which makes the unmodified script
+    loader-bound.  Datasets call this from ``__getitems__`` (the DataLoader's batched
+    fetch hook) so one batch costs a few array ops instead of B Python round trips.
+
+    ``images`` is either a uint8 [B, H, W(, C)] array, or ``(source, index)`` where
+    ``source`` is the dataset's whole uint8 array: then the padded CHW copy of ``source``
+    is built once and kept in ``cache`` (a dict owned by the dataset), and crops are
+    gathered straight out of it as strided windows.
+
+    Recognises exactly these transform classes (not subclasses) in this order, each
+    optional: RandomCrop, RandomHorizontalFlip, ToTensor, Normalize -- with ToTensor
+    required.  Crop offsets and flips are drawn from torch's global RNG like the per-image
+    path, as one vector per batch (same distribution; a different draw order).  Returns a
+    float [B, C, H, W] tensor, or None when the pipeline is not of that form (the caller
+    then falls back to per-image calls).
+    """
+    ts = transform.transforms if type(transform) is Compose else [transform]
+    order = (RandomCrop, RandomHorizontalFlip, ToTensor, Normalize)
+    pos = -1
+    for t in ts:
+        k = next((i for i, c in enumerate(order) if type(t) is c), None)
+        if k is None or k <= pos:
+            return None
+        pos = k
+    if not any(type(t) is ToTensor for t in ts):
+        return None
+    if isinstance(images, tuple):
+        source, index = images
+    else:
+        source, index = images, None
+    src = source if isinstance(source, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(source))
+    if src.dtype != torch.uint8:
+        return None
+    if src.dim() == 3:
+        src = src.unsqueeze(-1)
+    idx = torch.arange(src.shape[0]) if index is None else torch.as_tensor(index, dtype=torch.int64)
+    b = int(idx.numel())
+    x = None  # uint8 [B, C, H, W]
+    out = None
+    for t in ts:
+        if type(t) is RandomCrop:
+            th, tw = t.size
+            p = int(t.padding or 0)
+            if not isinstance(t.fill, numbers.Number):
+                return None
+            key = ("pad_chw", p, t.fill, id(source))
+            padded = cache.get(key) if cache is not None else None
+            if padded is None:
+                n, h, w, c = src.shape
+                padded = torch.full((n, c, h + 2 * p, w + 2 * p), t.fill, dtype=torch.uint8)
+                padded[:, :, p:p + h, p:p + w] = src.permute(0, 3, 1, 2)
+                if cache is not None and index is not None:
+                    cache[key] = padded
+            hp, wp = padded.shape[2], padded.shape[3]
+            if th > hp or tw > wp:
+                return None
+            i = torch.randint(0, hp - th + 1, (b,))
+            j = torch.randint(0, wp - tw + 1, (b,))
+            win = padded.unfold(2, th, 1).unfold(3, tw, 1)  # [N, C, nI, nJ, th, tw] view
+            x = win[idx, :, i, j]
+        elif type(t) is RandomHorizontalFlip:
+            if x is None:
+                x = src[idx].permute(0, 3, 1, 2)
+            m = torch.rand(b) < t.p
+            x = torch.where(m.view(-1, 1, 1, 1), x.flip(-1), x)
+        elif type(t) is ToTensor:
+            if x is None:
+                x = src[idx].permute(0, 3, 1, 2)
+            out = x.float().div_(255.0).contiguous()
+        elif type(t) is Normalize:
+            mean = torch.as_tensor(t.mean, dtype=torch.float32).view(1, -1, 1, 1)
+            std = torch.as_tensor(t.std, dtype=torch.float32).view(1, -1, 1, 1)
+            out = out.sub_(mean).div_(std)
+    return out

@@ -117,6 +117,31 @@ def build_reducer(force=False, verbose=True):
     return _smddp_build.build(srcs, NATIVE, force=force, verbose=verbose, name="_reducer_ext", hip=False)
 
 
+REF_NOTEBOOKS = os.environ.get("MI355X_DP_REF_SRC", "/root/reference/notebooks")
+FIXTURE = os.path.join(ROOT, "ref_fixture", "notebooks")
+
+
+def stage_reference_fixture(src=REF_NOTEBOOKS, dst=FIXTURE, verbose=True):
+    """Copy the reference workshop's notebooks and top-level scripts (no checkpoints) into the
+    git-ignored ``ref_fixture/`` so a GPU box -- which has no reference checkout -- can run
+    them unmodified (tests/test_gpu_integration.py, tools/run_notebook.py).  Never committed:
+    the files are the reference's own, used as test inputs only."""
+    if not os.path.isdir(src):
+        return None
+    os.makedirs(os.path.join(dst, "code"), exist_ok=True)
+    names = [f for f in os.listdir(src) if f.endswith(".ipynb")]
+    for f in names:
+        shutil.copyfile(os.path.join(src, f), os.path.join(dst, f))
+    code = os.path.join(src, "code")
+    for f in sorted(os.listdir(code)):
+        p = os.path.join(code, f)
+        if os.path.isfile(p) and f.endswith((".py", ".txt")):
+            shutil.copyfile(p, os.path.join(dst, "code", f))
+    if verbose:
+        print(f"[build] staged reference notebooks/scripts into {os.path.relpath(dst, ROOT)}")
+    return dst
+
+
 def build_all(force=False, verbose=True):
     # the -DMI_DEBUG library is rebuilt with the release one so the two never diverge in symbols
     outs = [build_kernels(force, verbose), build_kernels(force, verbose, debug=True), build_launcher(force, verbose)]

@@ -147,7 +147,23 @@ class TrainingJob:
         print(f"Training seconds: {self.training_seconds}")
         print(f"Billable seconds: {self.training_seconds}", flush=True)
         self.wall_seconds = time.time() - t_start
+        self.loop_seconds = self._loop_seconds(env.get("MI355X_DP_DEBUGGER"))
+        if self.loop_seconds is not None:
+            # the reference's ~166 s figure is the same span: first forward (hook's parameter
+            # inventory, nb2:1521) -> "Completed" (nb2:2609-2610), BASELINE.md row 2
+            print(f"Training loop seconds (first forward -> completed): {self.loop_seconds:.1f}", flush=True)
         return self
+
+    @staticmethod
+    def _loop_seconds(tensors_dir):
+        if not tensors_dir:
+            return None
+        try:
+            with open(os.path.join(tensors_dir, "collections", "parameters.json")) as f:
+                t0 = json.load(f).get("first_forward_time")
+        except (OSError, ValueError):
+            return None
+        return None if t0 is None else time.time() - float(t0)
 
     def _package(self) -> str:
         out = os.path.join(s3_to_local(self.output_path.rstrip("/")), self.job_name, "output")

@@ -43,6 +43,7 @@ class DebuggerHook:
         if self.module is not None:
             return
         self.module = module
+        self.first_forward_time = time.time()
         total = 0
         lines = []
         for name, p in module.named_parameters():
@@ -53,7 +54,7 @@ class DebuggerHook:
             print("\n".join(lines), flush=True)
             print(f"[mi355x_dp.debugger] Total Trainable Params: {total}", flush=True)
         with open(os.path.join(self.out_dir, "collections", "parameters.json"), "w") as f:
-            json.dump({"total_trainable_params": total,
+            json.dump({"total_trainable_params": total, "first_forward_time": self.first_forward_time,
                        "params": {n: p.numel() for n, p in module.named_parameters() if p.requires_grad}}, f)
 
     # ------------------------------------------------------------------ losses

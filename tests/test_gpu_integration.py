@@ -9,7 +9,19 @@ import torch
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REF_CODE = "/root/reference/notebooks/code"
+
+def _ref_notebooks():
+    """The reference workshop's notebooks dir: $MI355X_DP_REF_NOTEBOOKS, the read-only checkout,
+    or the git-ignored copy build() stages into ref_fixture/ (what a GPU box has)."""
+    for d in (os.environ.get("MI355X_DP_REF_NOTEBOOKS"), "/root/reference/notebooks",
+              os.path.join(ROOT, "ref_fixture", "notebooks")):
+        if d and os.path.exists(os.path.join(d, "code", "cifar10-distributed-smddp-gpu.py")):
+            return d
+    return None
+
+
+REF_NB = _ref_notebooks()
+REF_CODE = os.path.join(REF_NB, "code") if REF_NB else None
 
 
 def test_graft_smoke():
@@ -44,7 +56,7 @@ def test_smddp_backend_world1(tmp_path):
     assert "OK" in r.stdout
 
 
-@pytest.mark.skipif(not os.path.exists(REF_CODE), reason="reference checkout not mounted")
+@pytest.mark.skipif(REF_CODE is None, reason="reference scripts not staged (run build())")
 def test_reference_gpu_script_unmodified(tmp_path):
     """notebook-2 flow: PyTorch(distribution=smddp).fit() runs cifar10-distributed-smddp-gpu.py as-is."""
     code = (
@@ -212,3 +224,30 @@ def test_bench_two_ranks_torchrun_gloo():
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 64 and out["value"] > 0
     assert out["replicas_identical"] is True
+
+
+@pytest.mark.skipif(REF_NB is None, reason="reference notebooks not staged (run build())")
+def test_reference_notebook2_verbatim(tmp_path):
+    """The reference's OWN notebook 2 (2_pytorch_dist_smddp_gpu.ipynb), every code cell verbatim:
+    synthetic 'download' of full-size CIFAR-10 (50k/10k) -> upload -> PyTorch(distribution=smddp)
+    .fit() of the unmodified cifar10-distributed-smddp-gpu.py with the notebook's hyperparameters
+    (15 epochs, global batch 256, resnet18, smddp) on every local MI355X.  BASELINE.md rows 1-2:
+    438 s job / ~166 s loop on 8 x A100."""
+    import json
+    import re
+    report = tmp_path / "nb2.json"
+    env = {**os.environ, "MI355X_DP_S3_ROOT": str(tmp_path / "s3"), "MI355X_DP_JOBS_ROOT": str(tmp_path / "jobs")}
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "run_notebook.py"), "--compat",
+                        "--workdir", str(tmp_path / "nb"), "--report", str(report),
+                        os.path.join(REF_NB, "2_pytorch_dist_smddp_gpu.ipynb")],
+                       capture_output=True, text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    cells = json.load(open(report))["cells"]
+    assert all(c["status"] == "ok" for c in cells), cells
+    assert "Initialized the distributed environment: 'smddp' backend on" in out
+    accs = [float(a) for a in re.findall(r"Test set: Average loss: -?[\d.]+, Accuracy: ([\d.]+)", out)]
+    assert len(accs) >= 15
+    assert accs[-1] > 0.3  # learned something (synthetic data; Bayes accuracy ~0.78)
+    secs = int(re.search(r"Training seconds: (\d+)", out).group(1))
+    assert secs < 438, f"job slower than the reference's 8xA100 438 s: {secs}"
