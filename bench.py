@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--lr", type=float, default=0.01)  # reference hyperparameter (nb2:110)
     p.add_argument("--backend", default=os.environ.get("MI355X_DP_BACKEND", "nccl"))
     p.add_argument("--bucket-mb", type=float, default=None)
+    p.add_argument("--force-comm", action="store_true",
+                   help="create the process group and issue every bucket collective even at N=1 "
+                        "(comm-stream / overlap traces on one GPU); the headline N=1 run leaves it off")
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as one captured HIP graph (launch-bound small-batch configs)")
@@ -66,8 +69,14 @@ def main():
     gpu = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    use_pg = world > 1 or args.force_comm
+    if use_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.backend == "smddp":
+            sys.path.append(os.path.join(ROOT, "compat"))
             import smdistributed.dataparallel.torch.torch_smddp  # noqa: F401  (registers 'smddp')
         dist.init_process_group(backend=args.backend, device_id=dev if args.backend == "nccl" else None)
 
@@ -80,6 +89,8 @@ def main():
     kw = {}
     if args.bucket_mb:
         kw["bucket_cap_mb"] = args.bucket_mb
+    if args.force_comm:
+        kw["force_comm"] = True
     engine = DataParallel(model, **kw)
     opt = FlatSGD(engine, lr=args.lr, momentum=0.9, weight_decay=1e-4)
 
@@ -174,7 +185,8 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "optimizer": "SGD(momentum=0.9, wd=1e-4), fp32 master weights, bf16 compute",
-                "backend": args.backend if world > 1 else "none",
+                "backend": args.backend if use_pg else "none",
+                "comm_forced_at_world1": bool(args.force_comm and world == 1),
                 "buckets": len(engine.buckets),
                 "hip_graph": bool(args.graph),
             },
@@ -182,9 +194,10 @@ def main():
             "loss_last": round(last_loss, 4),
             "warmup_s": round(t_w1 - t_w0, 2),
             "replicas_identical": replicas_ok,
+            "bucket_launch_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -15,9 +15,10 @@
 //   * Work::wait() makes the caller's stream wait on the completion event (no host
 //     block); getFuture() returns a device-aware ivalue::Future completed under the
 //     comm-stream guard, which is what DDP comm hooks and torch.distributed use;
-//   * a watchdog thread aborts the communicator and the process if a collective does
-//     not complete within the timeout (the launcher then tears down every rank --
-//     SURVEY.md §5.3 failure detection);
+//   * a watchdog thread polls ncclCommGetAsyncError and the collectives' completion events:
+//     on an RCCL async error or a collective exceeding the timeout it records the failure
+//     (Work::isSuccess()/wait() report it), aborts the communicator and the process (the
+//     launcher then tears down every rank -- SURVEY.md §5.3 failure detection);
 //   * allreduce AVG maps to ncclAvg; large all-reduces can be split into link-sized
 //     chunks queued back to back (MI355X_DP_SMDDP_CHUNK_MB) so a long bucket does not
 //     hold the comm stream in one monolithic kernel;
@@ -111,21 +112,31 @@ struct DoneEvent {
   ~DoneEvent() { hipEventDestroy(ev); }
 };
 
+// Backend-wide failure state, shared with every Work: set by the watchdog when RCCL reports an
+// asynchronous error (ncclCommGetAsyncError: a peer died, a network / xGMI fault) or a collective
+// times out, so isSuccess()/wait() tell the truth instead of assuming success.
+struct CommError {
+  std::atomic<int> code{0};  // 0 = healthy, else the ncclResult_t (or -1 for a timeout)
+  std::string what;
+};
+
 class SmddpWork : public c10d::Work {
  public:
   SmddpWork(int rank, c10d::OpType op, int device, HIPStreamMasqueradingAsCUDA comm, std::vector<at::Tensor> outputs,
-            bool blocking)
-      : c10d::Work(rank, op), device_(device), comm_(comm), outputs_(std::move(outputs)), blocking_(blocking) {
+            bool blocking, std::shared_ptr<CommError> err)
+      : c10d::Work(rank, op), device_(device), comm_(comm), outputs_(std::move(outputs)), blocking_(blocking),
+        err_(std::move(err)) {
     done_ = std::make_shared<DoneEvent>(comm_.stream());
     std::vector<c10::Device> devs{c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device)};
     future_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()), devs);
     c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_);
     future_->markCompleted(c10::IValue(outputs_));
   }
-  bool isCompleted() override { return hipEventQuery(done_->ev) == hipSuccess; }
-  bool isSuccess() const override { return true; }
+  bool isCompleted() override { return err_->code.load() != 0 || hipEventQuery(done_->ev) == hipSuccess; }
+  bool isSuccess() const override { return err_->code.load() == 0; }
 
   bool wait(std::chrono::milliseconds timeout) override {
+    TORCH_CHECK(err_->code.load() == 0, "smddp: communicator failed: ", err_->what);
     auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_);
     HIPCHECK(hipStreamWaitEvent(cur.stream(), done_->ev, 0));
     if (blocking_) HIPCHECK(hipEventSynchronize(done_->ev));
@@ -142,6 +153,7 @@ class SmddpWork : public c10d::Work {
   HIPStreamMasqueradingAsCUDA comm_;
   std::vector<at::Tensor> outputs_;
   bool blocking_;
+  std::shared_ptr<CommError> err_;
   c10::intrusive_ptr<c10::ivalue::Future> future_;
 };
 
@@ -172,6 +184,7 @@ class SmddpBackend : public c10d::Backend {
     }
     HIPCHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
     if (const char* c = std::getenv("MI355X_DP_SMDDP_CHUNK_MB")) chunk_bytes_ = (size_t)(atof(c) * (1 << 20));
+    if (const char* c = std::getenv("MI355X_DP_SMDDP_ABORT_ON_ERROR")) abort_on_error_ = c[0] != '0';
     const char* ipc = std::getenv("MI355X_DP_SMDDP_IPC");
     if (ipc && ipc[0] == '1' && size > 1) setup_ipc();
     if (!ipc_on_) comm();  // eager RCCL bootstrap unless the IPC path may serve the first collectives
@@ -304,7 +317,8 @@ class SmddpBackend : public c10d::Backend {
       c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(),
                                                                                        comm_stream_);
     fn(comm_stream_.stream());
-    auto w = c10::make_intrusive<SmddpWork>(rank_, op, device_, comm_stream_, std::move(outputs), blocking);
+    TORCH_CHECK(err_->code.load() == 0, "smddp: communicator failed: ", err_->what);
+    auto w = c10::make_intrusive<SmddpWork>(rank_, op, device_, comm_stream_, std::move(outputs), blocking, err_);
     {
       std::lock_guard<std::mutex> lk(mu_);
       pending_.push_back(w->done_);
@@ -450,14 +464,52 @@ class SmddpBackend : public c10d::Backend {
   void setTimeout(std::chrono::milliseconds t) override { timeout_ = t; }
 
  private:
+  // ncclCommGetAsyncError on the live communicator (ProcessGroupNCCL's async error handling):
+  // an error is recorded in err_ (Works report it), the communicator is aborted so no rank stays
+  // blocked inside RCCL, and the process exits non-zero -- the launcher then tears down all ranks.
+  void poll_async_error() {
+    ncclComm_t c = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(init_mu_, std::try_to_lock);
+      if (!lk.owns_lock()) return;  // communicator being created right now
+      c = comm_;
+    }
+    if (!c) return;
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return;
+    if (r == ncclSuccess || r == ncclInProgress) return;
+    fail((int)r, std::string("RCCL async error: ") + ncclGetErrorString(r));
+  }
+
+  void fail(int code, const std::string& what) {
+    err_->what = what;
+    err_->code.store(code);
+    fprintf(stderr, "smddp watchdog: rank %d %s; aborting communicator and process\n", rank_, what.c_str());
+    fflush(stderr);
+    if (abort_on_error_) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      std::abort();
+    }
+  }
+
+ public:
+  // testing hook: report an error through the same path the watchdog uses (no abort when
+  // MI355X_DP_SMDDP_ABORT_ON_ERROR=0), so isSuccess()/wait() behaviour can be checked
+  void inject_error(int code, const std::string& what) { fail(code, what); }
+  bool healthy() const { return err_->code.load() == 0; }
+  int64_t comm_stream_handle() const { return (int64_t)(intptr_t)comm_stream_.stream(); }
+
+ private:
   void watchdog_loop() {
     while (!stop_) {
       std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      if (err_->code.load() != 0) continue;
       if (ipc_err_ && __atomic_load_n(ipc_err_, __ATOMIC_RELAXED)) {
-        fprintf(stderr, "smddp watchdog: rank %d IPC all-reduce timed out waiting for peers; aborting\n", rank_);
-        fflush(stderr);
-        std::abort();
+        fail(-2, "IPC all-reduce timed out waiting for peers");
+        continue;
       }
+      poll_async_error();
       std::lock_guard<std::mutex> lk(mu_);
       while (!pending_.empty()) {
         auto& w = pending_.front();
@@ -466,12 +518,7 @@ class SmddpBackend : public c10d::Backend {
           continue;
         }
         if (std::chrono::steady_clock::now() - w->start > timeout_) {
-          fprintf(stderr, "smddp watchdog: rank %d collective did not complete within %lld ms; aborting\n", rank_,
-                  (long long)timeout_.count());
-          fflush(stderr);
-          if (comm_) ncclCommAbort(comm_);
-          comm_ = nullptr;
-          std::abort();
+          fail(-1, "collective did not complete within " + std::to_string((long long)timeout_.count()) + " ms");
         }
         break;
       }
@@ -499,6 +546,8 @@ class SmddpBackend : public c10d::Backend {
   size_t chunk_bytes_ = 0;
   std::mutex mu_;
   std::deque<std::shared_ptr<DoneEvent>> pending_;
+  std::shared_ptr<CommError> err_ = std::make_shared<CommError>();
+  bool abort_on_error_ = true;  // MI355X_DP_SMDDP_ABORT_ON_ERROR=0: record only (tests)
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
 };
@@ -532,6 +581,20 @@ c10::intrusive_ptr<c10d::Backend> create_backend(const c10::intrusive_ptr<c10d::
   return b;
 }
 
+static SmddpBackend* as_smddp(const c10::intrusive_ptr<c10d::Backend>& b) {
+  auto* s = dynamic_cast<SmddpBackend*>(b.get());
+  TORCH_CHECK(s, "not an smddp backend");
+  return s;
+}
+
+void inject_error(const c10::intrusive_ptr<c10d::Backend>& b, int code, const std::string& what) {
+  as_smddp(b)->inject_error(code, what);
+}
+
+bool healthy(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->healthy(); }
+
+int64_t comm_stream(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->comm_stream_handle(); }
+
 int rccl_version() {
   int v = 0;
   ncclGetVersion(&v);
@@ -545,4 +608,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("create_backend", &smddp::create_backend, "create the smddp backend", pybind11::arg("store"),
         pybind11::arg("rank"), pybind11::arg("size"), pybind11::arg("device"), pybind11::arg("timeout_s"));
   m.def("rccl_version", &smddp::rccl_version);
+  m.def("inject_error", &smddp::inject_error, pybind11::arg("backend"), pybind11::arg("code"), pybind11::arg("what"));
+  m.def("healthy", &smddp::healthy, pybind11::arg("backend"));
+  m.def("comm_stream", &smddp::comm_stream, pybind11::arg("backend"));
 }

@@ -25,7 +25,9 @@
 #include <torch/csrc/distributed/c10d/Work.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <tuple>
 #include <mutex>
 #include <vector>
 
@@ -45,9 +47,36 @@ int64_t link_aware_cap(int world, double link_gbps, int links, double alpha_us, 
 }
 
 // Greedy contiguous buckets over tensors in backward order.  The first bucket is capped at
-// `first`, the last at `last` (planned from the end), the rest at `cap`.
+// `first`, the last at `last` (planned from the end), the rest at `cap`.  Afterwards every
+// bucket smaller than `min_bytes` is merged into its successor (the tail into its predecessor):
+// with parameters in reverse registration order the first bucket would otherwise be a lone
+// 4 KB fc.bias -- a collective that pays the full launch latency for nothing.
+std::vector<std::vector<int64_t>> merge_small(std::vector<std::vector<int64_t>> out, const std::vector<int64_t>& bytes,
+                                              int64_t min_bytes) {
+  auto size = [&](const std::vector<int64_t>& b) {
+    int64_t s = 0;
+    for (int64_t i : b) s += bytes[i];
+    return s;
+  };
+  size_t i = 0;
+  while (out.size() > 1 && i < out.size()) {
+    if (size(out[i]) >= min_bytes) {
+      ++i;
+      continue;
+    }
+    if (i + 1 < out.size()) {
+      out[i].insert(out[i].end(), out[i + 1].begin(), out[i + 1].end());
+      out.erase(out.begin() + i + 1);
+    } else {
+      out[i - 1].insert(out[i - 1].end(), out[i].begin(), out[i].end());
+      out.erase(out.begin() + i);
+    }
+  }
+  return out;
+}
+
 std::vector<std::vector<int64_t>> plan_buckets(const std::vector<int64_t>& bytes, int64_t cap, int64_t first,
-                                               int64_t last) {
+                                               int64_t last, int64_t min_bytes) {
   const int64_t n = (int64_t)bytes.size();
   std::vector<std::vector<int64_t>> out;
   if (n == 0) return out;
@@ -57,7 +86,9 @@ std::vector<std::vector<int64_t>> plan_buckets(const std::vector<int64_t>& bytes
   std::vector<int64_t> cur;
   int64_t cur_bytes = 0, lim = first;
   for (int64_t i = 0; i < tail_begin; ++i) {
-    if (!cur.empty() && cur_bytes + bytes[i] > lim) {
+    // a bucket is closed only once it holds >= min_bytes: a first bucket capped below the
+    // first large tensor takes that tensor instead of leaving a sliver in front of it
+    if (!cur.empty() && cur_bytes + bytes[i] > lim && cur_bytes >= min_bytes) {
       out.push_back(cur);
       cur.clear();
       cur_bytes = 0;
@@ -70,15 +101,16 @@ std::vector<std::vector<int64_t>> plan_buckets(const std::vector<int64_t>& bytes
   std::vector<int64_t> tail;
   for (int64_t i = tail_begin; i < n; ++i) tail.push_back(i);
   out.push_back(tail);
-  return out;
+  return merge_small(std::move(out), bytes, min_bytes);
 }
 
 class Reducer {
  public:
   Reducer(at::Tensor flat_grad, std::vector<int64_t> offsets, std::vector<int64_t> numels,
-          std::vector<std::vector<int64_t>> buckets, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t align)
+          std::vector<std::vector<int64_t>> buckets, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t align,
+          bool force_comm)
       : grad_(std::move(flat_grad)), offsets_(std::move(offsets)), numels_(std::move(numels)),
-        buckets_(std::move(buckets)), pg_(std::move(pg)) {
+        buckets_(std::move(buckets)), pg_(std::move(pg)), force_comm_(force_comm) {
     TORCH_CHECK(offsets_.size() == numels_.size(), "offsets / numels mismatch");
     const int64_t np = (int64_t)offsets_.size();
     bucket_of_.assign(np, -1);
@@ -106,6 +138,8 @@ class Reducer {
     param_ready_.assign(offsets_.size(), false);
     works_.clear();
     next_ = 0;
+    trace_.clear();
+    t0_ = std::chrono::steady_clock::now();
   }
 
   void mark_ready(int64_t i) {
@@ -129,6 +163,8 @@ class Reducer {
       works.swap(works_);
     }
     for (auto& w : works) w->wait();
+    std::lock_guard<std::mutex> g(mu_);
+    trace_.emplace_back(-1, 0, since_reset_us());
   }
 
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
@@ -137,12 +173,23 @@ class Reducer {
   int64_t comm_bytes() const { return comm_bytes_; }
   std::vector<std::pair<int64_t, int64_t>> ranges() const { return ranges_; }
   std::vector<std::vector<int64_t>> buckets() const { return buckets_; }
+  // (bucket, bytes, host launch time in us since reset()) of every bucket of the current step,
+  // in launch order; finish() appends (-1, 0, time all collectives were waited on)
+  std::vector<std::tuple<int64_t, int64_t, double>> trace() {
+    std::lock_guard<std::mutex> g(mu_);
+    return trace_;
+  }
 
  private:
+  double since_reset_us() const {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0_).count();
+  }
+
   void launch_ready_locked() {
     while (next_ < (int64_t)buckets_.size() && ready_[next_]) {
-      if (pg_ && pg_->getSize() > 1) {
-        const auto& r = ranges_[next_];
+      const auto& r = ranges_[next_];
+      trace_.emplace_back(next_, (r.second - r.first) * grad_.element_size(), since_reset_us());
+      if (pg_ && (pg_->getSize() > 1 || force_comm_)) {
         std::vector<at::Tensor> ts{grad_.narrow(0, r.first, r.second - r.first)};
         c10d::AllreduceOptions opts;
         opts.reduceOp = c10d::ReduceOp::SUM;
@@ -162,6 +209,9 @@ class Reducer {
   std::vector<int64_t> bucket_of_, pending_;
   std::vector<bool> ready_, param_ready_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  bool force_comm_ = false;
+  std::vector<std::tuple<int64_t, int64_t, double>> trace_;
+  std::chrono::steady_clock::time_point t0_ = std::chrono::steady_clock::now();
   int64_t next_ = 0, comm_calls_ = 0, comm_bytes_ = 0;
   std::mutex mu_;
 };
@@ -173,13 +223,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mi355x_dp native gradient-bucket reducer";
   m.def("link_aware_cap", &mi_ddp::link_aware_cap, py::arg("world"), py::arg("link_gbps") = 153.0,
         py::arg("links") = 7, py::arg("alpha_us") = 25.0, py::arg("overhead") = 0.1,
-        py::arg("min_bytes") = int64_t(4) << 20, py::arg("max_bytes") = int64_t(64) << 20);
-  m.def("plan_buckets", &mi_ddp::plan_buckets, py::arg("bytes"), py::arg("cap"), py::arg("first"), py::arg("last"));
+        py::arg("min_bytes") = int64_t(4) << 20, py::arg("max_bytes") = int64_t(32) << 20);
+  m.def("plan_buckets", &mi_ddp::plan_buckets, py::arg("bytes"), py::arg("cap"), py::arg("first"), py::arg("last"),
+        py::arg("min_bytes") = 0);
   py::class_<mi_ddp::Reducer>(m, "Reducer")
       .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>, std::vector<std::vector<int64_t>>,
-                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t>(),
+                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t, bool>(),
            py::arg("flat_grad"), py::arg("offsets"), py::arg("numels"), py::arg("buckets"), py::arg("process_group"),
-           py::arg("align") = 64)
+           py::arg("align") = 64, py::arg("force_comm") = false)
       .def("reset", &mi_ddp::Reducer::reset)
       .def("mark_ready", &mi_ddp::Reducer::mark_ready, py::call_guard<py::gil_scoped_release>())
       .def("finish", &mi_ddp::Reducer::finish, py::call_guard<py::gil_scoped_release>())
@@ -188,5 +239,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("comm_calls", &mi_ddp::Reducer::comm_calls)
       .def_property_readonly("comm_bytes", &mi_ddp::Reducer::comm_bytes)
       .def_property_readonly("ranges", &mi_ddp::Reducer::ranges)
-      .def_property_readonly("buckets", &mi_ddp::Reducer::buckets);
+      .def_property_readonly("buckets", &mi_ddp::Reducer::buckets)
+      .def_property_readonly("trace", &mi_ddp::Reducer::trace);
 }

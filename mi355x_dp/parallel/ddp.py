@@ -39,14 +39,34 @@ _ENV_BUCKET_MB = os.environ.get("MI355X_DP_BUCKET_MB")
 DEFAULT_BUCKET_MB = float(_ENV_BUCKET_MB) if _ENV_BUCKET_MB else None  # None: link-aware planner
 DEFAULT_FIRST_BUCKET_MB = float(os.environ.get("MI355X_DP_FIRST_BUCKET_MB", "2"))
 DEFAULT_LAST_BUCKET_MB = float(os.environ.get("MI355X_DP_LAST_BUCKET_MB", "4"))
+# buckets below this are merged into a neighbour (a 4 KB fc.bias bucket is a latency-only collective)
+DEFAULT_MIN_BUCKET_MB = float(os.environ.get("MI355X_DP_MIN_BUCKET_MB", "1"))
+# issue every bucket collective even at world size 1 (exercises the comm stream / overlap on one GPU)
+FORCE_COMM = os.environ.get("MI355X_DP_FORCE_COMM", "0") == "1"
+# debug: stage each bucket through a copy taken where its collective starts, and check at the end
+# of backward that no gradient was written after its bucket was launched (parallel/health.py)
+CHECK_STREAM_ORDER = os.environ.get("MI355X_DP_CHECK_STREAM_ORDER", "0") == "1"
 
 
-def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int) -> List[List[int]]:
-    """Greedy contiguous bucketing of tensors (given in backward order)."""
+def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int, last_cap_bytes: int = None,
+                 min_bytes: int = 0) -> List[List[int]]:
+    """Greedy contiguous bucketing of tensors (given in backward order); Python twin of the
+    native planner (csrc/ddp/reducer.cpp plan_buckets): first bucket capped at
+    ``first_cap_bytes``, a tail bucket of at most ``last_cap_bytes`` (planned from the end), the
+    rest at ``cap_bytes``; then any bucket below ``min_bytes`` is merged into a neighbour."""
+    n = len(sizes_bytes)
+    if n == 0:
+        return []
+    last = cap_bytes if last_cap_bytes is None else last_cap_bytes
+    tail_begin, acc = n - 1, sizes_bytes[-1]
+    while tail_begin > 0 and acc + sizes_bytes[tail_begin - 1] <= last:
+        tail_begin -= 1
+        acc += sizes_bytes[tail_begin]
     buckets, cur, cur_bytes = [], [], 0
     cap = first_cap_bytes
-    for i, b in enumerate(sizes_bytes):
-        if cur and cur_bytes + b > cap:
+    for i in range(tail_begin):
+        b = sizes_bytes[i]
+        if cur and cur_bytes + b > cap and cur_bytes >= min_bytes:
             buckets.append(cur)
             cur, cur_bytes = [], 0
             cap = cap_bytes
@@ -54,7 +74,27 @@ def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int) -
         cur_bytes += b
     if cur:
         buckets.append(cur)
-    return buckets
+    buckets.append(list(range(tail_begin, n)))
+    return merge_small_buckets(buckets, sizes_bytes, min_bytes)
+
+
+def merge_small_buckets(buckets: List[List[int]], sizes_bytes: List[int], min_bytes: int) -> List[List[int]]:
+    """Merge every bucket smaller than ``min_bytes`` into its successor (the last one into its
+    predecessor), so no collective is issued for a latency-only sliver."""
+    out = [list(b) for b in buckets]
+    size = lambda b: sum(sizes_bytes[i] for i in b)  # noqa: E731
+    i = 0
+    while len(out) > 1 and i < len(out):
+        if size(out[i]) >= min_bytes:
+            i += 1
+            continue
+        if i + 1 < len(out):
+            out[i + 1] = out[i] + out[i + 1]
+            del out[i]
+        else:
+            out[i - 1] = out[i - 1] + out[i]
+            del out[i]
+    return out
 
 
 class DataParallel(nn.Module):
@@ -69,7 +109,9 @@ class DataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = DEFAULT_BUCKET_MB,
                  first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB, broadcast_buffers: bool = True,
-                 bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB):
+                 bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
+                 min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
+                 check_stream_order: bool = CHECK_STREAM_ORDER):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -77,6 +119,10 @@ class DataParallel(nn.Module):
         self.world_size = dist.get_world_size(process_group) if self.distributed else 1
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.broadcast_buffers = broadcast_buffers and self.distributed and self.world_size > 1
+        # collectives are issued when there is a peer -- or at world 1 when forced (trace / overlap runs)
+        self.comm_on = self.distributed and (self.world_size > 1 or force_comm)
+        self.check_stream_order = bool(check_stream_order)
+        self.order_violations = []
 
         params = [p for p in module.parameters() if p.requires_grad]
         params = list(reversed(params))  # approximate backward order
@@ -94,11 +140,12 @@ class DataParallel(nn.Module):
         else:
             cap = int(bucket_cap_mb * 2**20)
         self.bucket_cap_bytes = cap
+        first_b, last_b = int(first_bucket_mb * 2**20), min(cap, int(last_bucket_mb * 2**20))
+        min_b = int(min_bucket_mb * 2**20)
         if native is not None:
-            self.buckets = [list(b) for b in native.plan_buckets(sizes, cap, int(first_bucket_mb * 2**20),
-                                                                 min(cap, int(last_bucket_mb * 2**20)))]
+            self.buckets = [list(b) for b in native.plan_buckets(sizes, cap, first_b, last_b, min_b)]
         else:
-            self.buckets = plan_buckets(sizes, cap, int(first_bucket_mb * 2**20))
+            self.buckets = plan_buckets(sizes, cap, first_b, last_b, min_b)
         self.bucket_of = {}
         for b, idxs in enumerate(self.buckets):
             for i in idxs:
@@ -117,12 +164,14 @@ class DataParallel(nn.Module):
         self._py_comm_calls = 0
 
         self.reducer = None
-        if native is not None:
+        self._staging = {}
+        if native is not None and not self.check_stream_order:
             pg = None
-            if self.distributed and self.world_size > 1:
+            if self.comm_on:
                 pg = process_group if process_group is not None else dist.distributed_c10d._get_default_group()
             self.reducer = native.Reducer(self.flat.grad, [int(o) for o in self.flat.offsets],
-                                          [p.numel() for p in self.flat.params], self.buckets, pg, 64)
+                                          [p.numel() for p in self.flat.params], self.buckets, pg, 64,
+                                          bool(force_comm))
         for i, p in enumerate(self.flat.params):
             cb = functools.partial(self.reducer.mark_ready, i) if self.reducer is not None \
                 else self._make_ready_cb(i)
@@ -139,6 +188,12 @@ class DataParallel(nn.Module):
         # place; the bf16 compute copy and the transposed dgrad copies follow it
         module.register_load_state_dict_post_hook(lambda _m, _keys: self.flat.refresh_bf16())
         self._reset()
+
+    @property
+    def bucket_trace(self):
+        """(bucket, bytes, launch_us) of the last step, launch time relative to forward start
+        (native reducer only): the order and timing in which buckets went to the comm stream."""
+        return list(self.reducer.trace) if self.reducer is not None else []
 
     @property
     def comm_calls(self) -> int:
@@ -187,12 +242,66 @@ class DataParallel(nn.Module):
             self._next += 1
 
     def _launch(self, b):
-        if not (self.distributed and self.world_size > 1):
-            return
         lo, hi = self.bucket_ranges[b]
+        if self.check_stream_order:
+            self._launch_checked(b, lo, hi)
+            return
+        if not self.comm_on:
+            return
         w = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
         self._works.append(w)
         self._py_comm_calls += 1
+
+    def _launch_checked(self, b, lo, hi):
+        """Stream-order check mode: the bucket's collective runs on a copy of its slice taken on
+        a side stream that waits for everything the compute stream had enqueued when the bucket
+        became ready -- i.e. exactly what the comm stream sees.  finish_gradient_sync compares a
+        checksum of that copy with one of the final local gradient; a mismatch means a kernel
+        wrote a gradient after its bucket was handed to the collective (grad-ready signalled
+        too early, or a producer on an unsynchronised stream)."""
+        from mi355x_dp.ops import checksum
+        g = self.flat.grad
+        if g.is_cuda:
+            side = self._staging.get("stream")
+            if side is None:
+                side = self._staging["stream"] = torch.cuda.Stream(device=g.device)
+            side.wait_stream(torch.cuda.current_stream(g.device))
+            with torch.cuda.stream(side):
+                stage = g[lo:hi].clone()
+                seen = checksum(stage)
+                w = None
+                if self.comm_on:
+                    w = dist.all_reduce(stage, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+        else:
+            stage = g[lo:hi].clone()
+            seen = checksum(stage)
+            w = dist.all_reduce(stage, op=dist.ReduceOp.SUM, group=self.process_group,
+                                async_op=True) if self.comm_on else None
+        if w is not None:
+            self._py_comm_calls += 1
+        self._works.append((b, lo, hi, stage, seen, w))
+
+    def _finish_checked(self):
+        from mi355x_dp.ops import checksum
+        g = self.flat.grad
+        side = self._staging.get("stream")
+        if side is not None:
+            torch.cuda.current_stream(g.device).wait_stream(side)
+        for b, lo, hi, stage, seen, w in self._works:
+            final = checksum(g[lo:hi])
+            if w is not None:
+                w.wait()
+            if float(seen) != float(final):
+                self.order_violations.append((b, float(seen), float(final)))
+            g[lo:hi].copy_(stage)
+        self._works = []
+        if self.order_violations:
+            from .health import StreamOrderViolation
+            b, s0, s1 = self.order_violations[0]
+            raise StreamOrderViolation(
+                f"bucket {b} (params {self.buckets[b]}) changed after its all-reduce was launched: checksum "
+                f"seen by the collective {s0!r} != final local gradient {s1!r} ({len(self.order_violations)} "
+                f"bucket(s) affected)")
 
     # ------------------------------------------------------------ public
     def forward(self, *args, **kwargs):
@@ -211,9 +320,12 @@ class DataParallel(nn.Module):
         for b in range(len(self.buckets)):
             self._ready[b] = True
         self._launch_ready()
-        for w in self._works:
-            w.wait()
-        self._works = []
+        if self.check_stream_order:
+            self._finish_checked()
+        else:
+            for w in self._works:
+                w.wait()
+            self._works = []
         if average and self.world_size > 1:
             self.flat.grad.mul_(1.0 / self.world_size)
 

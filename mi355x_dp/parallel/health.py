@@ -9,9 +9,12 @@
   torch backends (the native smddp backend has its own C++ watchdog that aborts the
   communicator); on timeout it reports the rank and exits non-zero so the launcher tears
   down every rank (abort-on-non-zero-status).
-* ``check_stream_order`` -- debug assertion that the gradient buffer a bucket all-reduce
-  reads has been produced before the collective starts (compares a per-bucket checksum
-  taken on the compute stream with the one seen by a synchronous re-read).
+* stream-order checking -- ``DataParallel(check_stream_order=True)`` (or
+  MI355X_DP_CHECK_STREAM_ORDER=1) runs every bucket's collective on a copy taken on a side
+  stream ordered exactly like the comm stream, and at the end of backward compares its
+  checksum with the final local gradient; ``StreamOrderViolation`` names the bucket whose
+  gradient was written after its collective had been launched (the race class of a
+  grad-ready signal issued before the producing kernel, or a producer on another stream).
 """
 from __future__ import annotations
 
@@ -25,6 +28,10 @@ import torch.distributed as dist
 
 
 class ReplicaDivergence(RuntimeError):
+    pass
+
+
+class StreamOrderViolation(RuntimeError):
     pass
 
 
@@ -88,9 +95,7 @@ class CollectiveWatchdog:
         return False
 
 
-def check_stream_order(engine, bucket: int) -> bool:
-    """Debug: re-read a bucket's slice after a device sync and compare with the value the comm saw."""
-    lo, hi = engine.bucket_ranges[bucket]
-    seen = engine.flat.grad[lo:hi].double().sum()
-    torch.cuda.synchronize()
-    return bool(torch.equal(seen, engine.flat.grad[lo:hi].double().sum()))
+def check_stream_order(engine) -> list:
+    """Violations recorded by an engine built with ``check_stream_order=True``:
+    [(bucket, checksum seen by the collective, final checksum)] of the last step."""
+    return list(engine.order_violations)

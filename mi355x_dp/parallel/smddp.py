@@ -11,8 +11,9 @@ works unmodified.  The creator:
      device at init (SURVEY.md C45);
   2. returns the native C++ backend (``csrc/comm/smddp_backend.cpp``: RCCL
      communicator on its own high-priority HIP stream, event-ordered with the
-     caller's stream, plus xGMI-aware bucket chunking) when it is built, else
-     torch's RCCL ``ProcessGroupNCCL``;
+     caller's stream, plus xGMI-aware bucket chunking).  A missing build is an
+     error, not a silent fallback; ``MI355X_DP_SMDDP_IMPL=nccl`` deliberately
+     selects torch's RCCL ``ProcessGroupNCCL`` instead;
   3. on a host with no GPU (CPU tests, gloo plumbing) returns a gloo backend
      bound to the loopback interface so the same user code runs.
 """
@@ -60,19 +61,20 @@ def create_backend(store, rank, world_size, timeout):
     if dev is None:
         return _gloo(store, rank, world_size, timeout)
     if os.environ.get("MI355X_DP_SMDDP_IMPL", "native") == "native":
-        try:
-            from . import _smddp_native
-            mod = _smddp_native.load()
-            if mod is not None:
-                if os.environ.get("MI355X_DP_SMDDP_IPC") == "1":
-                    # the one-shot IPC all-reduce kernel lives in the HIP kernel library
-                    from mi355x_dp.ops import _lib
-                    _lib.load(True)
-                    os.environ.setdefault("MI355X_DP_KERNELS_LIB", _lib.KERNEL_LIB)
-                secs = timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout)
-                return mod.create_backend(store, rank, world_size, dev, secs)
-        except ImportError:
-            pass
+        # the native backend is the product: a missing / broken build fails loudly instead of
+        # silently running torch's ProcessGroupNCCL (MI355X_DP_SMDDP_IMPL=nccl selects that on purpose)
+        from . import _smddp_native
+        mod = _smddp_native.load()
+        if mod is None:
+            raise RuntimeError("smddp: native backend extension (_smddp_native_ext) is not built; run "
+                               "`python -m mi355x_dp.build` or set MI355X_DP_SMDDP_IMPL=nccl")
+        if os.environ.get("MI355X_DP_SMDDP_IPC") == "1":
+            # the one-shot IPC all-reduce kernel lives in the HIP kernel library
+            from mi355x_dp.ops import _lib
+            _lib.load(True)
+            os.environ.setdefault("MI355X_DP_KERNELS_LIB", _lib.KERNEL_LIB)
+        secs = timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout)
+        return mod.create_backend(store, rank, world_size, dev, secs)
     return dist.ProcessGroupNCCL(store, rank, world_size, timeout)
 
 

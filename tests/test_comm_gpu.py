@@ -1,0 +1,101 @@
+"""Comm path on one MI355X: the DP engine's bucket collectives issued through a real process
+group at world size 1 (``force_comm``), the stream-order checker over every native backward
+kernel, and the smddp backend's error reporting (RCCL async errors / timeouts must make
+Work.is_success() false and wait() raise instead of being assumed successful)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_stream_order_checker_native_step():
+    """Every native backward kernel signals grad-ready only after the kernel writing that gradient
+    is enqueued: with check_stream_order=True each bucket is snapshotted on a side stream ordered
+    like the comm stream; no bucket may differ from the final gradient, and the gradients equal
+    the unchecked engine's bit for bit."""
+    sys.path.insert(0, ROOT)
+    from mi355x_dp.models import resnet18
+    from mi355x_dp.ops import cross_entropy
+    from mi355x_dp.parallel import DataParallel
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(16, 3, 64, 64, device=dev, generator=g)
+    y = torch.randint(0, 1000, (16,), device=dev, generator=g)
+    grads = {}
+    for check in (False, True):
+        torch.manual_seed(0)
+        e = DataParallel(resnet18().to(dev), bucket_cap_mb=4, first_bucket_mb=1, min_bucket_mb=0,
+                         check_stream_order=check)
+        assert len(e.buckets) > 3
+        for _ in range(2):
+            e.zero_grad()
+            cross_entropy(e(x), y).backward()
+            e.finish_gradient_sync()
+        torch.cuda.synchronize()
+        assert e.order_violations == []
+        grads[check] = e.flat.grad.clone()
+    assert torch.allclose(grads[False], grads[True], rtol=1e-4, atol=1e-6)
+
+
+def _bench(args, env=None):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, env={**os.environ, **(env or {})})
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line)
+
+
+@pytest.mark.parametrize("backend", ["smddp", "nccl"])
+def test_force_comm_world1_bench(backend):
+    """bench.py --force-comm: a real process group at N=1 (native smddp or ProcessGroupNCCL) and
+    one collective per bucket, launched in bucket order while backward runs."""
+    out = _bench(["--model", "resnet18", "--batch", "32", "--image-size", "64", "--steps", "3", "--warmup", "1",
+                  "--force-comm", "--backend", backend], {"MASTER_PORT": str(29600 + (backend == "nccl"))})
+    cfg = out["config"]
+    assert cfg["backend"] == backend and cfg["comm_forced_at_world1"] is True
+    trace = out["bucket_launch_ms"]
+    assert [t[0] for t in trace[:-1]] == list(range(cfg["buckets"])) and trace[-1][0] == -1
+    launch_ms = [t[2] for t in trace[:-1]]
+    assert launch_ms == sorted(launch_ms)
+
+
+def test_smddp_error_reporting_and_stream():
+    """A failure recorded by the backend's watchdog path makes in-flight and later Works report
+    is_success() False and wait() raise; collectives run on the backend's own comm stream."""
+    code = r'''
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"]); sys.path.append(os.path.join(os.environ["ROOT"], "compat"))
+import smdistributed.dataparallel.torch.torch_smddp
+dist.init_process_group(backend="smddp")
+from mi355x_dp.parallel import _smddp_native
+mod = _smddp_native.load()
+pg = dist.distributed_c10d._get_default_group()
+b = pg._get_backend(torch.device("cuda"))
+t = torch.ones(1 << 20, device="cuda")
+w = dist.all_reduce(t, async_op=True); w.wait(); torch.cuda.synchronize()
+assert w.is_success() and mod.healthy(b)
+assert mod.comm_stream(b) != torch.cuda.current_stream().cuda_stream
+w2 = dist.all_reduce(t, async_op=True)
+mod.inject_error(b, 6, "injected remote error")
+assert not mod.healthy(b) and not w2.is_success()
+try:
+    w2.wait(); print("NO_RAISE")
+except Exception as e:
+    print("RAISED", "injected remote error" in str(e))
+try:
+    dist.all_reduce(t); print("NO_RAISE2")
+except Exception as e:
+    print("RAISED2")
+os._exit(0)
+'''
+    env = {**os.environ, "ROOT": ROOT, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29613", "RANK": "0",
+           "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MI355X_DP_SMDDP_ABORT_ON_ERROR": "0"}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "RAISED True" in r.stdout and "RAISED2" in r.stdout, r.stdout + r.stderr

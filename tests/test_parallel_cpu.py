@@ -52,7 +52,7 @@ def _worker_engine(rank, world, port, q, backend):
 def _worker_engine_body(rank, world, port, q, backend):
     _init(rank, world, port, backend)
     from mi355x_dp.parallel import DataParallel, FlatSGD
-    m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01)
+    m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0)
     opt = FlatSGD(m, lr=0.1, momentum=0.9, weight_decay=1e-3)
     x, y = _data()
     shard = slice(rank * 8, (rank + 1) * 8)
@@ -171,7 +171,7 @@ def _worker_reducer(rank, world, port, q, py):
             os.environ["MI355X_DP_PY_REDUCER"] = "1"
         _init(rank, world, port)
         from mi355x_dp.parallel import DataParallel, FlatSGD
-        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01)
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0)
         opt = FlatSGD(m, lr=0.05, momentum=0.9)
         x, y = _data()
         shard = slice(rank * 8, (rank + 1) * 8)
@@ -207,3 +207,99 @@ def test_native_reducer_matches_python_reducer():
             assert calls > 2
         out[py] = res[0][2]
     assert (out[False] == out[True]).all()
+
+
+def test_planner_merges_small_buckets():
+    """No latency-only sliver buckets (the lone 4 KB fc.bias first bucket): every
+    planned bucket is >= min_bytes unless it is the only one; native == Python planner; a first
+    bucket capped below the first big tensor takes that tensor."""
+    from mi355x_dp.parallel import _reducer_native
+    from mi355x_dp.parallel.ddp import plan_buckets
+    from mi355x_dp.models import get_model
+    ext = _reducer_native.load()
+    for name in ("resnet18", "resnet50", "vit_b_16"):
+        ps = list(reversed([p for p in get_model(name).parameters() if p.requires_grad]))
+        sizes = [p.numel() * 4 for p in ps]
+        cap, first, last, mn = 32 << 20, 2 << 20, 4 << 20, 1 << 20
+        plan = plan_buckets(sizes, cap, first, last, mn)
+        assert [i for b in plan for i in b] == list(range(len(sizes)))
+        bsz = [sum(sizes[i] for i in b) for b in plan]
+        assert len(plan) == 1 or min(bsz) >= mn, (name, bsz)
+        assert max(bsz) <= cap + max(sizes), (name, bsz)
+        if ext is not None:
+            assert [list(b) for b in ext.plan_buckets(sizes, cap, first, last, mn)] == plan
+    # resnet50: fc.bias (4 KB) + fc.weight (8 MB) form the first bucket
+    ps = list(reversed([n for n, p in get_model("resnet50").named_parameters()]))
+    plan = plan_buckets([p.numel() * 4 for p in reversed(list(get_model("resnet50").parameters()))],
+                        32 << 20, 2 << 20, 4 << 20, 1 << 20)
+    assert [ps[i] for i in plan[0]] == ["fc.bias", "fc.weight"]
+    assert merge_ok([[0], [1, 2], [3]], [10, 1, 1, 10], 5) == [[0], [1, 2, 3]]
+    assert merge_ok([[0], [1], [2]], [10, 10, 1], 5) == [[0], [1, 2]]
+
+
+def merge_ok(b, sizes, mn):
+    from mi355x_dp.parallel.ddp import merge_small_buckets
+    return merge_small_buckets(b, sizes, mn)
+
+
+def test_stream_order_checker_cpu():
+    """check_stream_order=True: a normal step passes and yields the same gradients as the plain
+    path; a gradient changed after its bucket was handed to the collective is reported."""
+    from mi355x_dp.parallel import DataParallel
+    from mi355x_dp.parallel.health import StreamOrderViolation
+    x, y = _data()
+    grads = {}
+    for check in (False, True):
+        e = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0,
+                         check_stream_order=check)
+        assert e.reducer is None or not check
+        e.zero_grad()
+        torch.nn.functional.cross_entropy(e(x), y).backward()
+        e.finish_gradient_sync()
+        grads[check] = e.flat.grad.clone()
+        assert e.order_violations == []
+    assert torch.equal(grads[False], grads[True])
+    # a "producer" that writes after the grad-ready signal: mark ready, then modify the slice
+    e = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0, check_stream_order=True)
+    e.zero_grad()
+    e._reset()
+    for i in e.buckets[0]:
+        e._mark_ready(i)
+    lo, hi = e.bucket_ranges[0]
+    e.flat.grad[lo:hi] += 1.0  # late write
+    with pytest.raises(StreamOrderViolation, match="bucket 0"):
+        e.finish_gradient_sync()
+
+
+def _worker_force_comm(q, port):
+    try:
+        _init(0, 1, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0, force_comm=True)
+        opt = FlatSGD(m, lr=0.05, momentum=0.9)
+        x, y = _data()
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+        q.put((len(m.buckets), m.comm_calls, [t[0] for t in m.bucket_trace]))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(e)
+        raise
+
+
+def test_force_comm_world1():
+    """force_comm issues every bucket collective at world size 1 (the comm path a one-GPU box can
+    trace); the native reducer records the launch order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_force_comm, args=(q, _port()))
+    p.start()
+    r = q.get(timeout=120)
+    p.join(60)
+    assert not isinstance(r, Exception), repr(r)
+    nb, calls, trace = r
+    assert nb > 1 and calls == nb
+    from mi355x_dp.parallel import _reducer_native
+    if _reducer_native.load() is not None:
+        assert trace[:nb] == list(range(nb)) and trace[-1] == -1
