@@ -177,7 +177,24 @@ __global__ void bn_eval_coeffs_kernel(int C, float eps, const float* __restrict_
 // apart, so every wave-instruction stays 1 KB contiguous) in flight before using any, instead of
 // one load -> use -> store chain per iteration.  Channel of vector v: (8 v) mod C, advanced
 // incrementally by the (uniform) stride's channel step.
-constexpr int EW_U = 4;
+#ifndef MI_EW_U
+#define MI_EW_U 4
+#endif
+#ifndef MI_EW_GRID_CAP
+#define MI_EW_GRID_CAP 65536
+#endif
+#ifndef MI_EW_NTSTORE
+#define MI_EW_NTSTORE 1
+#endif
+constexpr int EW_U = MI_EW_U;
+
+// 16-byte store of an elementwise result (MI_EW_NTSTORE=1: non-temporal, streaming past L2)
+__device__ __forceinline__ void st16(void* base, int64_t v, uint4 val) {
+  if (MI_EW_NTSTORE)
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, val), (u32x4*)base + v);
+  else
+    ((uint4*)base)[v] = val;
+}
 
 struct EwIter {
   int64_t v0, stride;
@@ -198,14 +215,33 @@ struct EwIter {
 // y = act(x*scale + shift (+ res)); grid-stride over 8-element vectors.  RES_BN: the residual is
 // itself a raw BN input, normalised on the fly (res*rscale + rshift) -- the downsample branch's
 // BatchNorm output is never stored (ResNet projection shortcut).
-template <bool RES_BN>
+// FIXC: the grid stride (in elements) is a multiple of C, so every vector a thread touches has the
+// same 8 channels -- the coefficients are loaded into registers once instead of four 16-byte L1
+// loads per 16 bytes of data (which made the pass TA/L1-issue-bound at ~3 TB/s).  Host picks it
+// when (grid * NT * 8) % C == 0 (every ResNet width).
+__device__ __forceinline__ void load8f(const float* __restrict__ p, int c, float* o) {
+  *(float4*)&o[0] = *(const float4*)(p + c);
+  *(float4*)&o[4] = *(const float4*)(p + c + 4);
+}
+
+template <bool RES_BN, bool FIXC>
 __global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                         bf16_t* __restrict__ y, const float* __restrict__ scale,
                                                         const float* __restrict__ shift,
                                                         const float* __restrict__ rscale,
                                                         const float* __restrict__ rshift, int64_t nvec, int C,
                                                         int relu) {
-  for (EwIter it(nvec, C); it.v0 < nvec; it.next(C)) {
+  EwIter it(nvec, C);
+  float a[8], b[8], pr[8], qr[8];
+  if (FIXC) {
+    load8f(scale, it.c0, a);
+    load8f(shift, it.c0, b);
+    if (RES_BN) {
+      load8f(rscale, it.c0, pr);
+      load8f(rshift, it.c0, qr);
+    }
+  }
+  for (; it.v0 < nvec; it.next(C)) {
     uint4 xv[EW_U], rv[EW_U];
 #pragma unroll
     for (int u = 0; u < EW_U; ++u) {
@@ -222,21 +258,23 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict
       if (v >= nvec) break;
       float f[8];
       unpack8(xv[u], f);
-      const float4 a0 = *(const float4*)(scale + c), a1 = *(const float4*)(scale + c + 4);
-      const float4 b0 = *(const float4*)(shift + c), b1 = *(const float4*)(shift + c + 4);
-      f[0] = f[0] * a0.x + b0.x; f[1] = f[1] * a0.y + b0.y; f[2] = f[2] * a0.z + b0.z; f[3] = f[3] * a0.w + b0.w;
-      f[4] = f[4] * a1.x + b1.x; f[5] = f[5] * a1.y + b1.y; f[6] = f[6] * a1.z + b1.z; f[7] = f[7] * a1.w + b1.w;
+      if (!FIXC) {
+        load8f(scale, c, a);
+        load8f(shift, c, b);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = f[j] * a[j] + b[j];
       if (res) {
         float r[8];
         unpack8(rv[u], r);
         if (RES_BN) {
-          const float4 p0 = *(const float4*)(rscale + c), p1 = *(const float4*)(rscale + c + 4);
-          const float4 q0 = *(const float4*)(rshift + c), q1 = *(const float4*)(rshift + c + 4);
-          r[0] = r[0] * p0.x + q0.x; r[1] = r[1] * p0.y + q0.y; r[2] = r[2] * p0.z + q0.z; r[3] = r[3] * p0.w + q0.w;
-          r[4] = r[4] * p1.x + q1.x; r[5] = r[5] * p1.y + q1.y; r[6] = r[6] * p1.z + q1.z; r[7] = r[7] * p1.w + q1.w;
+          if (!FIXC) {
+            load8f(rscale, c, pr);
+            load8f(rshift, c, qr);
+          }
           // round like a stored bf16 shortcut activation: bit-identical to the unfused sequence
 #pragma unroll
-          for (int j = 0; j < 8; ++j) r[j] = bf2f(f2bf(r[j]));
+          for (int j = 0; j < 8; ++j) r[j] = bf2f(f2bf(r[j] * pr[j] + qr[j]));
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] += r[j];
@@ -245,8 +283,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
       }
-      ((uint4*)y)[v] = pack8(f);
-      c = it.chan(c, C);
+      st16(y, v, pack8(f));
+      if (!FIXC) c = it.chan(c, C);
     }
   }
 }
@@ -368,11 +406,19 @@ __global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __re
   else fin_fwd(c, s2, q2, f);
 }
 
+template <bool FIXC>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                           const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
                                                           int64_t nvec, int C, int relu) {
-  for (EwIter it(nvec, C); it.v0 < nvec; it.next(C)) {
+  EwIter it(nvec, C);
+  float k0[8], k1[8], k2[8];
+  if (FIXC) {  // see bn_apply_kernel_t: one channel octet per thread for the whole pass
+    load8f(coef, it.c0, k0);
+    load8f(coef + C, it.c0, k1);
+    load8f(coef + 2 * C, it.c0, k2);
+  }
+  for (; it.v0 < nvec; it.next(C)) {
     uint4 dv[EW_U], xq[EW_U], yq[EW_U];
 #pragma unroll
     for (int u = 0; u < EW_U; ++u) {
@@ -397,15 +443,17 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
 #pragma unroll
         for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
       }
-      if (dres) ((uint4*)dres)[v] = pack8(d);
-      float k0[8], k1[8], k2[8], o[8];
-      *(float4*)&k0[0] = *(const float4*)(coef + c); *(float4*)&k0[4] = *(const float4*)(coef + c + 4);
-      *(float4*)&k1[0] = *(const float4*)(coef + C + c); *(float4*)&k1[4] = *(const float4*)(coef + C + c + 4);
-      *(float4*)&k2[0] = *(const float4*)(coef + 2 * C + c); *(float4*)&k2[4] = *(const float4*)(coef + 2 * C + c + 4);
+      if (dres) st16(dres, v, pack8(d));
+      if (!FIXC) {
+        load8f(coef, c, k0);
+        load8f(coef + C, c, k1);
+        load8f(coef + 2 * C, c, k2);
+      }
+      float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = k0[j] * d[j] + k1[j] * xv[j] + k2[j];
-      ((uint4*)dx)[v] = pack8(o);
-      c = it.chan(c, C);
+      st16(dx, v, pack8(o));
+      if (!FIXC) c = it.chan(c, C);
     }
   }
 }
@@ -753,7 +801,33 @@ __global__ __launch_bounds__(NT) void bnpool3_bwd_apply_kernel(const bf16_t* __r
 
 inline int ew_grid(int64_t nvec) {
   int64_t g = (nvec + NT * EW_U - 1) / (NT * EW_U);
-  return (int)(g < 4096 ? g : 4096);
+  return (int)(g < MI_EW_GRID_CAP ? g : MI_EW_GRID_CAP);
+}
+
+// channel octet fixed per thread for the whole grid-stride pass (bn_apply_kernel_t FIXC)
+inline bool ew_fixc(int grid, int C) { return ((int64_t)grid * NT * 8) % C == 0; }
+
+template <bool RES_BN>
+inline void launch_bn_apply(const void* x, const void* res, void* y, const float* scale, const float* shift,
+                            const float* rscale, const float* rshift, int64_t nvec, int C, int relu, hipStream_t st) {
+  const int grid = ew_grid(nvec);
+  if (ew_fixc(grid, C))
+    hipLaunchKernelGGL((bn_apply_kernel_t<RES_BN, true>), dim3(grid), dim3(NT), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel_t<RES_BN, false>), dim3(grid), dim3(NT), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu);
+}
+
+inline void launch_bn_bwd_apply(const void* dy, const void* y, const void* x, const float* coef, void* dx, void* dres,
+                                int64_t nvec, int C, int relu, hipStream_t st) {
+  const int grid = ew_grid(nvec);
+  if (ew_fixc(grid, C))
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                       (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                       (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
 }
 
 inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3& grid) {
@@ -867,9 +941,7 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
                                                save_invstd, scale, shift), st);
   if (!y) return (int)hipGetLastError();  // statistics + coefficients only (the consumer applies them)
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel_t<false>, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x,
-                     (const bf16_t*)res, (bf16_t*)y, scale, shift, (const float*)nullptr, (const float*)nullptr, nvec,
-                     C, relu);
+  launch_bn_apply<false>(x, res, y, scale, shift, nullptr, nullptr, nvec, C, relu, st);
   return (int)hipGetLastError();
 }
 
@@ -880,8 +952,7 @@ MI_API int mi_bn_apply_dual(const void* x, const void* res, void* y, int M, int 
                             const float* shift, const float* rscale, const float* rshift, int relu, hipStream_t st) {
   if (C % 8 != 0 || !x || !res || !y) return (int)hipErrorInvalidValue;
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel_t<true>, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x,
-                     (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu);
+  launch_bn_apply<true>(x, res, y, scale, shift, rscale, rshift, nvec, C, relu, st);
   return (int)hipGetLastError();
 }
 
@@ -892,9 +963,7 @@ MI_API int mi_bn_fwd_eval(const void* x, const void* res, void* y, int M, int C,
   hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, C, eps, gamma, beta, rmean, rvar,
                      scale, shift);
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel_t<false>, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)x,
-                     (const bf16_t*)res, (bf16_t*)y, scale, shift, (const float*)nullptr, (const float*)nullptr, nvec,
-                     C, relu);
+  launch_bn_apply<false>(x, res, y, scale, shift, nullptr, nullptr, nvec, C, relu, st);
   return (int)hipGetLastError();
 }
 
@@ -909,8 +978,7 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
                      (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
   slab_finalize<true>(part, nblk, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)y, (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
+  launch_bn_bwd_apply(dy, y, x, coef, dx, dres, nvec, C, relu, st);
   return (int)hipGetLastError();
 }
 
@@ -923,8 +991,7 @@ MI_API int mi_bn_bwd_train_pre(const void* dz, const void* x, void* dx, void* dr
   if (C % 8 != 0 || pre_rows <= 0) return (int)hipErrorInvalidValue;
   slab_finalize<true>(part, pre_rows, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
   int64_t nvec = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(NT), 0, st, (const bf16_t*)dz, (const bf16_t*)nullptr,
-                     (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, 0);
+  launch_bn_bwd_apply(dz, nullptr, x, coef, dx, dres, nvec, C, 0, st);
   return (int)hipGetLastError();
 }
 

@@ -80,7 +80,7 @@ def test_conv_stem_im2col():
 
 
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
-@pytest.mark.parametrize("C", [64, 256, 2048])
+@pytest.mark.parametrize("C", [64, 200, 256, 2048])  # 200: channel octet not fixed per thread (non-FIXC path)
 def test_batchnorm_act(relu, res, C):
     from mi355x_dp.ops import batch_norm_act
     N, H = 8, 7
@@ -117,6 +117,37 @@ def test_batchnorm_act(relu, res, C):
     if relu:
         y2r = F.relu(y2r)
     assert rel_err(y2, y2r) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C", [(256, 56, 64), (256, 7, 2048), (64, 28, 200)])
+def test_batchnorm_production_shapes(N, H, C):
+    """BN at ResNet-50 bs256 sizes (M = 802,816 rows for layer1): the statistics slab is taller than
+    256 rows, so the one-launch split + last-arriving-block finalize (slab_split_fin_kernel, device
+    scope counters that reset themselves) runs.  Two back-to-back steps: running stats, the batch
+    counter (+1 exactly once per step) and the gradients all match fp32 PyTorch each time."""
+    from mi355x_dp.ops import batch_norm_act
+    torch.manual_seed(0)
+    gamma = torch.rand(C, device="cuda").add_(0.5).requires_grad_()
+    beta = torch.randn(C, device="cuda").requires_grad_()
+    gr, br = gamma.detach().clone().requires_grad_(), beta.detach().clone().requires_grad_()
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    rm2, rv2 = rm.clone(), rv.clone()
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    for step in range(2):
+        x = (torch.randn(N, C, H, H, device="cuda") * 2 + step).to(BF).contiguous(memory_format=CL).requires_grad_()
+        y = batch_norm_act(x, gamma, beta, rm, rv, nbt, True, 0.1, 1e-5, relu=True)
+        xr = x.detach().float().requires_grad_()
+        yr = F.relu(F.batch_norm(xr, rm2, rv2, gr, br, True, 0.1, 1e-5))
+        assert rel_err(y, yr) < 1e-2
+        assert torch.allclose(rm, rm2, rtol=1e-3, atol=1e-3) and torch.allclose(rv, rv2, rtol=1e-3, atol=1e-3)
+        assert int(nbt) == step + 1
+        g = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+        y.backward(g)
+        yr.backward(g.float())
+        assert rel_err(x.grad, xr.grad) < 3e-2
+        assert rel_err(gamma.grad, gr.grad) < 1e-2 and rel_err(beta.grad, br.grad) < 1e-2
+        del x, y, xr, yr, g
+        torch.cuda.empty_cache()
 
 
 def test_maxpool_gap():
