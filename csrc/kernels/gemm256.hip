@@ -27,6 +27,12 @@
 //    ds_read_b128 fragment reads spread over the banks;
 //  * XCD-aware, M-grouped tile order (GROUP_M 8) for L2 reuse of the B panel.
 #include "common.h"
+#ifndef MI_CONV_NTSTORE
+#define MI_CONV_NTSTORE 0
+#endif
+#ifndef MI_TN_NOATOMIC
+#define MI_TN_NOATOMIC 0  // timing experiment only (wrong results)
+#endif
 #include "epilogue.h"
 #include <algorithm>
 #include <cstdlib>
@@ -429,7 +435,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
             for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
           }
         }
+#if MI_CONV_NTSTORE
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16_t*)a.C + off));
+#else
         *(uint4*)((bf16_t*)a.C + off) = o;
+#endif
       }
     }
     lgkm_wait0();  // this wave's reads of the slice retire before the next quadrant row overwrites it
@@ -620,7 +630,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
       if (n >= a.N) continue;
       float* dst = a.C + (size_t)m * a.ldc + n;
       const f32x4 v = acc[i][j];
-      if (a.splits > 1) {
+      if (a.splits > 1 && MI_TN_NOATOMIC) {
+        *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+      } else if (a.splits > 1) {
         atomicAdd(dst, v[0]); atomicAdd(dst + 1, v[1]); atomicAdd(dst + 2, v[2]); atomicAdd(dst + 3, v[3]);
       } else {
         const float4 o = *(float4*)dst;

@@ -17,11 +17,20 @@
 //      - mode 0 plain, mode 1 conv wgrad (B gathered from NHWC input)
 //    LDS tiles stay in global (row = reduction index) order and the MFMA
 //    fragments are read transposed with ds_read_b64_tr_b16; split-K over the
-//    (huge) N*P*Q reduction with fp32 atomics into the fp32 gradient buffer.
+//    (huge) N*P*Q reduction: every split writes its partial tile to a slab and a
+//    reduce kernel sums the splits into the fp32 gradient (deterministic; the
+//    fp32-atomic variant cost ~1 ms per ResNet-50 step at ~1.3 TB/s of atomics).
 #include "common.h"
 #include "epilogue.h"
 #include <algorithm>
 #include <cstdlib>
+
+#ifndef MI_CONV_NTSTORE
+#define MI_CONV_NTSTORE 0
+#endif
+#ifndef MI_TN_NOATOMIC
+#define MI_TN_NOATOMIC 0  // timing experiment only: split-K partials stored, not added (wrong results)
+#endif
 
 namespace {
 
@@ -81,6 +90,7 @@ struct TNArgs {
   int k_per_split;
   int a_bytes, b_bytes;
   float* colsum;    // optional [M] fp32 += column sums of A (a Linear layer's bias gradient)
+  float* ws;        // split-K partial slabs [tiles][splits][BM*BN] (fragment order), or null: atomics
   ConvGeom g;
 };
 
@@ -521,7 +531,10 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
           for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
         }
       }
-      *(uint4*)((bf16_t*)a.C + off) = o;
+      if (MI_CONV_NTSTORE)
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16_t*)a.C + off));
+      else
+        *(uint4*)((bf16_t*)a.C + off) = o;
     }
   }
   if (a.stats) {
@@ -715,21 +728,33 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
     }
   }
 
-  // epilogue: lane holds D[m = 16i + 4g + r][n = 16j + li]; fp32 atomics (split-K)
+  // epilogue: lane holds D[m = 16i + 4g + r][n = 16j + li]
   const bool single = (gridDim.y == 1);
+  if (!single && a.ws) {
+    // split-K: this block's partial tile goes to its own slab in fragment order -- every store is one
+    // fully coalesced 1 KB wave-instruction (64 lanes x float4) -- and tn_splitk_reduce_kernel sums
+    // the splits into C: deterministic, and no fp32 atomics (~1.3 TB/s chip-wide) on the hot path
+    f32x4* slab = (f32x4*)a.ws + ((size_t)tile * gridDim.y + blockIdx.y) * (BM * BN / 4);
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * WN + 16 * j + li;
-      if (n >= a.N) continue;
+      for (int j = 0; j < NJ; ++j) slab[((i * NJ + j) * 4 + wid) * 64 + lane] = acc[i][j];
+  } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + 16 * i + 4 * g + r;
-        if (m >= a.M) continue;
-        float* dst = a.C + (size_t)m * a.ldc + n;
-        if (single) *dst += acc[i][j][r];
-        else atomicAdd(dst, acc[i][j][r]);
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WN + 16 * j + li;
+        if (n >= a.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + 16 * i + 4 * g + r;
+          if (m >= a.M) continue;
+          float* dst = a.C + (size_t)m * a.ldc + n;
+          if (single) *dst += acc[i][j][r];
+          else if (MI_TN_NOATOMIC) *dst = acc[i][j][r];
+          else atomicAdd(dst, acc[i][j][r]);
+        }
       }
     }
   }
@@ -741,6 +766,45 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) 
         const int m = m0 + wm * WM + 16 * i + 4 * g + r;
         if (m < a.M) atomicAdd(a.colsum + m, acc_cs[i][r]);
       }
+  }
+}
+
+// Sum the split-K slabs of tn_kernel<BM, BN> into C (+=).  Slab position p = ((i*NJ + j)*4 +
+// wave)*64 + lane holds D[m = 16i + 4g + r][n = 16j + li] (r = 0..3) of wave (wm, wn).  A block
+// covers 256/G consecutive positions x G split groups (thread t: position t % (256/G), group
+// t / (256/G), summing splits group, group + G, ...), so a tile with hundreds of splits is still
+// read by the whole chip; the G partials are combined in LDS in a fixed order (deterministic).
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void tn_splitk_reduce_kernel(const f32x4* __restrict__ ws, float* __restrict__ C,
+                                                               int M, int N, int ldc, int nbn, int splits,
+                                                               int log2g) {
+  constexpr int WM = BM / 2, WN = BN / 2, NJ = WN / 16;
+  constexpr int PER = BM * BN / 4;
+  __shared__ f32x4 part[256];
+  const int G = 1 << log2g, PB = 256 >> log2g;
+  const int tile = blockIdx.y;
+  const int pl = threadIdx.x & (PB - 1), grp = threadIdx.x >> (8 - log2g);
+  const int p = blockIdx.x * PB + pl;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (p < PER) {
+    const f32x4* src = ws + (size_t)tile * splits * PER + p;
+#pragma unroll 4
+    for (int s = grp; s < splits; s += G) v += src[(size_t)s * PER];
+  }
+  part[threadIdx.x] = v;
+  __syncthreads();
+  if (grp != 0 || p >= PER) return;
+  for (int g2 = 1; g2 < G; ++g2) v += part[g2 * PB + pl];
+  const int lane = p & 63, wid = (p >> 6) & 3, ij = p >> 8;
+  const int i = ij / NJ, j = ij - i * NJ;
+  const int wm = wid >> 1, wn = wid & 1, g = lane >> 4, li = lane & 15;
+  const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
+  const int n = n0 + wn * WN + 16 * j + li;
+  if (n >= N) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + wm * WM + 16 * i + 4 * g + r;
+    if (m < M) C[(size_t)m * ldc + n] += v[r];
   }
 }
 
@@ -901,6 +965,38 @@ hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
   }
 }
 
+// Split-K slab workspace of the TN kernels (fp32, per device, grown on demand and reused in stream
+// order).  Contract: the first call that needs a given size allocates (hipMalloc) -- it must not
+// run inside a HIP graph capture; GraphedStep's eager warm-up step makes every allocation first.
+// MI355X_DP_TN_SLABS=0 selects the fp32-atomic split-K path instead.
+struct SplitkWs { float* p = nullptr; size_t n = 0; };
+static SplitkWs g_splitk_ws[16];
+static float* splitk_workspace(size_t floats) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  SplitkWs& w = g_splitk_ws[dev & 15];
+  if (w.n < floats) {
+    const size_t n = std::max(floats, (size_t)16 << 20);  // >= 64 MB: every RN50 / RN152 wgrad fits
+    float* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return nullptr;  // -> atomic path
+    if (w.p) {
+      hipDeviceSynchronize();  // the old slabs may still be read by an in-flight reduce
+      hipFree(w.p);
+    }
+    w.p = p;
+    w.n = n;
+  }
+  return w.p;
+}
+static int g_tn_slabs = -1;
+static bool tn_slabs_on() {
+  if (g_tn_slabs < 0) {
+    const char* e = std::getenv("MI355X_DP_TN_SLABS");
+    g_tn_slabs = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_tn_slabs != 0;
+}
+
 template <int BM, int BN>
 hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   int tiles = cdiv(a.M, BM) * cdiv(a.N, BN);
@@ -910,10 +1006,21 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   a.k_per_split = steps_per * BK;
   splits = cdiv(a.K, a.k_per_split);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
+  a.ws = nullptr;
+  if (splits > 1 && a.colsum == nullptr && tn_slabs_on())
+    a.ws = splitk_workspace((size_t)tiles * splits * BM * BN);
   if (glds_on())
     hipLaunchKernelGGL((tn_kernel<BM, BN, 1>), dim3(tiles, splits), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((tn_kernel<BM, BN, 2>), dim3(tiles, splits), dim3(256), 0, st, a);
+  if (a.ws) {
+    // split groups per position: ~8 slab reads per thread, at most 64 groups, and enough blocks
+    int log2g = 0;
+    while (log2g < 6 && (splits >> (log2g + 3)) > 0) ++log2g;
+    const int pb = 256 >> log2g;
+    hipLaunchKernelGGL((tn_splitk_reduce_kernel<BM, BN>), dim3(cdiv(BM * BN / 4, pb), tiles), dim3(256), 0, st,
+                       (const f32x4*)a.ws, a.C, a.M, a.N, a.ldc, cdiv(a.N, BN), splits, log2g);
+  }
   return hipGetLastError();
 }
 
@@ -944,6 +1051,12 @@ hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
 // ============================================================== C ABI
 // Conv forward: x NHWC [Nb,H,W,C] bf16, w [K][R][S][C] bf16, y NHWC [Nb,P,Q,K].
 // Select direct-to-LDS (buffer_load ... lds) staging (1) or register staging (0) for all GEMM kernels.
+// Weight-gradient split-K reduction: 1 = slab workspace + reduce kernel (default), 0 = fp32 atomics.
+MI_API int mi_set_tn_slabs(int on) {
+  g_tn_slabs = on ? 1 : 0;
+  return 0;
+}
+
 MI_API int mi_set_glds(int on) {
   g_nt_glds = on ? 1 : 0;
   return 0;

@@ -65,6 +65,43 @@ def test_conv_fwd_bwd(shape):
     assert rel_err(w.grad, wr.grad) < 2e-2
 
 
+PROD_SHAPES = [
+    # ResNet-50 at batch 256: the shapes behind most of the step time
+    (256, 64, 56, 64, 3, 1, 1),     # halo 3x3 at 256 x 56^2; wgrad K = N*P*Q = 802,816 (split-K slabs)
+    (256, 256, 56, 64, 1, 1, 0),    # layer1 1x1 reduce, K = 802,816
+    (256, 256, 56, 512, 1, 2, 0),   # projection shortcut stride 2: parity-class dgrad
+    (256, 512, 7, 512, 3, 1, 1),    # layer4 3x3: few output tiles, deep reduction per tile
+]
+
+
+@pytest.mark.parametrize("shape", PROD_SHAPES)
+def test_conv_production_shapes(shape):
+    """Forward, data and weight gradient at full ResNet-50 bs256 sizes vs fp32 PyTorch, with the
+    weight gradient run twice into the same buffer (split-K reduction must ADD, deterministically)."""
+    from mi355x_dp.ops import conv2d
+    N, C, H, K, R, s, p = shape
+    torch.manual_seed(1)
+    x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL).requires_grad_()
+    w = (torch.randn(K, C, R, R, device="cuda") * (2.0 / (C * R * R)) ** 0.5).to(BF).float()
+    w = w.contiguous(memory_format=CL).requires_grad_(True)
+    y = conv2d(x, w, None, s, p)
+    yr = F.conv2d(x.detach().float(), w.detach(), None, s, p)
+    assert rel_err(y, yr) < 1e-2
+    gy = torch.randn(yr.shape, device="cuda").to(BF).contiguous(memory_format=CL)
+    del yr
+    y.backward(gy, retain_graph=True)
+    g1 = w.grad.clone()
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    F.conv2d(xr, wr, None, s, p).backward(gy.float())
+    assert rel_err(x.grad, 2 * xr.grad) < 2e-2
+    assert rel_err(g1, wr.grad) < 2e-2
+    assert torch.equal(w.grad, 2 * g1)  # second pass added exactly the same partial sums
+    del x, w, y, xr, wr, gy
+    torch.cuda.empty_cache()
+
+
 def test_conv_stem_im2col():
     from mi355x_dp.ops import conv2d
     x = torch.randn(4, 3, 64, 64, device="cuda").to(BF).contiguous(memory_format=CL)
