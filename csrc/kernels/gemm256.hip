@@ -27,6 +27,8 @@
 //    ds_read_b128 fragment reads spread over the banks;
 //  * XCD-aware, M-grouped tile order (GROUP_M 8) for L2 reuse of the B panel.
 #include "common.h"
+#include <cstdio>
+#include <cstdlib>
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
 #endif
@@ -789,6 +791,9 @@ MI_API int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, flo
   a.b_bytes = rsrc_bytes256((int64_t)N * a.K);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
   if (hipError_t e = plan_tail(a, cdiv(a.K, G_BK)); e != hipSuccess) return (int)e;
+  if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
+    fprintf(stderr, "[gemm] g256conv mode=%d M=%d N=%d K=%d Cs=%d R=%d s=%d epi=%d stats=%d blocks=%d\n", mode, a.M,
+            a.N, a.K, Cs, R, stride, epi, stats != nullptr, grid_of(a));
   if (mode == 1)
     hipLaunchKernelGGL(gemm256_nt_kernel<1>, dim3(grid_of(a)), dim3(512), 0, st, a);
   else

@@ -23,10 +23,16 @@
 #include "common.h"
 #include "epilogue.h"
 #include <algorithm>
+#include <array>
+#include <cstdio>
+#include <vector>
 #include <cstdlib>
 
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
+#endif
+#ifndef MI_NT_BLOCKS_PER_CU
+#define MI_NT_BLOCKS_PER_CU 4
 #endif
 #ifndef MI_TN_NOATOMIC
 #define MI_TN_NOATOMIC 0  // timing experiment only: split-K partials stored, not added (wrong results)
@@ -105,10 +111,17 @@ constexpr int HALO_PX = 256;
 
 template <int BM, int BN, int STAGES, bool HALO = false>
 constexpr int nt_smem_u4() {
-  // max(staging ring, epilogue C tile [BM][BN+8] bf16 + stats scratch [RPP][2][BN] fp32)
+  // max(staging ring, epilogue C tile [BM][BN+8] bf16 + stats scratch [4 waves][2][BN] fp32)
   constexpr int stage = HALO ? HALO_PX * 8 + 2 * BN * 8 : STAGES * (BM + BN) * 8;
-  constexpr int epi = (BM * (BN + 8) * 2 + (256 / (BN / 8)) * 2 * BN * 4) / 16;
+  constexpr int epi = (BM * (BN + 8) * 2 + 4 * 2 * BN * 4) / 16;
   return stage > epi ? stage : epi;
+}
+
+// blocks per CU the NT kernel is compiled for: 4 single-stage blocks (38 KB of LDS each at 128x128,
+// <= 128 VGPRs) keep more k-steps and epilogues of the short-K 1x1 convs in flight than 3 did
+template <int STAGES, bool HALO>
+constexpr int nt_occupancy() {
+  return HALO ? 2 : (STAGES == 1 ? MI_NT_BLOCKS_PER_CU : 2);
 }
 
 // STAGES = 1: one LDS buffer, load -> barrier -> MFMA -> barrier per k-step, 3 blocks per CU (the other
@@ -123,7 +136,7 @@ constexpr int nt_smem_u4() {
 // weight tile of the next tap loading into the other B buffer during each tap's MFMAs.  The
 // per-tap gather re-reads every input pixel ~9x through L2; the halo reads it ~(rp+2)/rp x.
 template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false>
-__global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) {
+__global__ __launch_bounds__(256, (nt_occupancy<STAGES, HALO>())) void nt_kernel(NTArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
   // ---- bf16 epilogue staged through LDS: full 16-byte row chunks to HBM (+ BN partial stats)
   constexpr int CST = BN + 8;                    // padded row stride (elements): 16-B aligned rows
   bf16_t* Ct = (bf16_t*)smem;                    // [BM][CST]
-  float* Sred = (float*)(smem) + (BM * CST) / 2; // [rows_par][2][BN] stats scratch
+  float* Sred = (float*)(smem) + (BM * CST) / 2; // [4 waves][2][BN] stats scratch
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int ml = wm * WM + 16 * i + fr;
@@ -538,18 +551,30 @@ __global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void nt_kernel(NTArgs a) 
     }
   }
   if (a.stats) {
-    // reduce the RPP row groups of each column chunk through LDS (Sred is disjoint from Ct)
+    // the lanes of a wave sharing a column chunk (lane mod CPR) are reduced by xor shuffles, then
+    // the 4 waves' rows through LDS (Sred is disjoint from Ct), in a fixed order
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      Sred[(rr * 2 + 0) * BN + cc * 8 + q] = s1[q];
-      Sred[(rr * 2 + 1) * BN + cc * 8 + q] = s2[q];
+    for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        s1[q] += __shfl_xor(s1[q], o, 64);
+        s2[q] += __shfl_xor(s2[q], o, 64);
+      }
+    }
+    if (lane < CPR) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        Sred[(wid * 2 + 0) * BN + cc * 8 + q] = s1[q];
+        Sred[(wid * 2 + 1) * BN + cc * 8 + q] = s2[q];
+      }
     }
     __syncthreads();
     const int prow = blockIdx.y * a.tiles_m + tm;
     for (int c = tid; c < 2 * BN; c += 256) {
       const int which = c / BN, col = c - which * BN;
       float t = 0.f;
-      for (int g = 0; g < RPP; ++g) t += Sred[(g * 2 + which) * BN + col];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) t += Sred[(w * 2 + which) * BN + col];
       if (n0 + col < a.N) a.stats[((size_t)prow * 2 + which) * a.N + n0 + col] = t;
     }
   }
@@ -946,6 +971,25 @@ static int halo_rp(int M, int N, int R, int S, int stride, int pad, int Cs, int 
   return rp;
 }
 
+// MI355X_DP_TRACE_GEMM=1: print every distinct GEMM / conv dispatch (kernel, geometry, epilogue) once
+// to stderr -- maps rocprof kernel rows (grid sizes) back to the network's layers.
+static int g_trace_gemm = -1;
+static void trace_gemm(const char* what, int mode, int M, int N, int K, int Cs, int R, int stride, int epi,
+                       int stats, int blocks, int splits) {
+  if (g_trace_gemm < 0) {
+    const char* e = std::getenv("MI355X_DP_TRACE_GEMM");
+    g_trace_gemm = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (!g_trace_gemm) return;
+  static std::vector<std::array<int, 12>> seen;
+  const std::array<int, 12> key{(int)(intptr_t)what, mode, M, N, K, Cs, R, stride, epi, stats, blocks, splits};
+  for (auto& k : seen)
+    if (k == key) return;
+  seen.push_back(key);
+  fprintf(stderr, "[gemm] %s mode=%d M=%d N=%d K=%d Cs=%d R=%d s=%d epi=%d stats=%d blocks=%d splits=%d\n", what,
+          mode, M, N, K, Cs, R, stride, epi, stats, blocks, splits);
+}
+
 hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
   if (a.mode == 1 || a.mode == 2) {
     const ConvGeom& g = a.g;
@@ -955,8 +999,17 @@ hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
       a.halo_pb = cdiv(g.P, rp);
       a.fPB = make_fastdiv((uint32_t)a.halo_pb);
       a.fHW2 = make_fastdiv((uint32_t)(g.Q + 2));
+      trace_gemm(nt_choice(a.M, a.N) == 1 ? "nt128x64-halo" : "nt128x128-halo", a.mode, a.M, a.N, a.K, g.Cs, g.R,
+                 g.stride, a.epi, a.stats != nullptr, (a.M / (g.P * g.Q)) * a.halo_pb, 1);
       return nt_choice(a.M, a.N) == 1 ? launch_nt<128, 64>(a, st) : launch_nt<128, 128>(a, st);
     }
+  }
+  {
+    static const char* names[3] = {"nt128x128", "nt128x64", "nt64x64"};
+    const int c = nt_choice(a.M, a.N);
+    const int bm = c == 2 ? 64 : 128, bn = c == 0 ? 128 : 64;
+    trace_gemm(names[c], a.mode, a.M, a.N, a.K, a.g.Cs, a.g.R, a.g.stride, a.epi, a.stats != nullptr,
+               cdiv(a.M, bm) * cdiv(a.N, bn), a.mode == 3 ? a.ncls : 1);
   }
   switch (nt_choice(a.M, a.N)) {
     case 1: return launch_nt<128, 64>(a, st);
@@ -1005,6 +1058,8 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   int steps_per = cdiv(ksteps, splits);
   a.k_per_split = steps_per * BK;
   splits = cdiv(a.K, a.k_per_split);
+  trace_gemm(BM == 128 ? (BN == 128 ? "tn128x128" : "tn128x64") : (BN == 128 ? "tn64x128" : "tn64x64"), a.mode,
+             a.M, a.N, a.K, a.g.Cs, a.g.R, a.g.stride, 0, 0, tiles, splits);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
   a.ws = nullptr;
   if (splits > 1 && a.colsum == nullptr && tn_slabs_on())

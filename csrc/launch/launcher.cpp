@@ -5,7 +5,12 @@
 //   * forks --nproc ranks, each with RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
 //     MASTER_ADDR / MASTER_PORT (torch.distributed env:// rendezvous) and
 //     OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK} for MPI-style scripts;
-//   * optional per-rank CPU affinity (contiguous equal slices of the allowed CPU set);
+//   * optional per-rank CPU affinity (--bind-cpus), GPU/NUMA-aware: local rank r drives GPU r, so
+//     it is bound to CPUs of that GPU's NUMA node (sysfs: the AMD GPUs under /sys/class/drm in
+//     PCI order -> device/numa_node; /sys/devices/system/node/nodeN/cpulist), the node's allowed
+//     CPUs split evenly among the ranks whose GPUs sit on it; contiguous equal slices of the
+//     allowed set when the topology is unreadable (the reference pinned each rank to its GPU's
+//     socket: CPU affinity ff,ffff0000,00ffffff, nb2:380).  --print-binding prints the plan.
 //   * `--tag-output` prefixes every line as "[1,mpirank:R,HOST]<stdout>:" / "<stderr>:";
 //   * abort-on-non-zero-status: the first rank that exits non-zero (or dies by a signal)
 //     makes the launcher SIGTERM (then SIGKILL after --grace seconds) every other rank,
@@ -25,6 +30,12 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <dirent.h>
+#include <fstream>
+#include <map>
+#include <set>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -44,7 +55,8 @@ void on_signal(int s) { g_signal = s; }
 void usage() {
   fprintf(stderr,
           "usage: mi355x_launch --nproc N [--node-rank R --nnodes M] [--master-addr A] [--master-port P]\n"
-          "                     [--host NAME] [--tag-output] [--bind-cpus] [--grace SEC] [-x KEY=VAL]...\n"
+          "                     [--host NAME] [--tag-output] [--bind-cpus] [--print-binding] [--grace SEC]\n"
+          "                     [-x KEY=VAL]...\n"
           "                     [--rank-env KEY=PREFIX]... -- cmd args...\n");
 }
 
@@ -73,12 +85,110 @@ std::vector<int> allowed_cpus() {
   return cpus;
 }
 
+// ------------------------------------------------------------ GPU / NUMA topology
+// MI355X_DP_TOPO_ROOT prefixes every sysfs path (tests build a fake tree).
+std::string topo_root() {
+  const char* r = getenv("MI355X_DP_TOPO_ROOT");
+  return r ? std::string(r) : std::string();
+}
+
+bool read_file(const std::string& path, std::string& out) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  out = ss.str();
+  while (!out.empty() && (out.back() == '\n' || out.back() == ' ')) out.pop_back();
+  return true;
+}
+
+std::vector<int> parse_cpulist(const std::string& s) {  // "0-3,8,10-11"
+  std::vector<int> v;
+  std::stringstream ss(s);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    if (part.empty()) continue;
+    size_t d = part.find('-');
+    int a = atoi(part.c_str()), b = d == std::string::npos ? a : atoi(part.c_str() + d + 1);
+    for (int c = a; c <= b; ++c) v.push_back(c);
+  }
+  return v;
+}
+
+// NUMA node of every AMD GPU (vendor 0x1002, display 0x03xxxx or accelerator 0x12xxxx class), in
+// PCI-address order = HIP device order; empty if sysfs is unreadable
+std::vector<int> gpu_numa_nodes() {
+  const std::string base = topo_root() + "/sys/class/drm";
+  std::vector<std::pair<std::string, int>> gpus;
+  std::set<std::string> seen;
+  DIR* d = opendir(base.c_str());
+  if (!d) return {};
+  while (dirent* e = readdir(d)) {
+    std::string n = e->d_name;
+    if (n.rfind("card", 0) != 0 || n.find('-') != std::string::npos) continue;
+    const std::string dev = base + "/" + n + "/device";
+    std::string vendor, cls, numa, link;
+    if (!read_file(dev + "/vendor", vendor) || vendor != "0x1002") continue;
+    if (!read_file(dev + "/class", cls) || !(cls.rfind("0x03", 0) == 0 || cls.rfind("0x12", 0) == 0)) continue;
+    char buf[4096];
+    ssize_t k = readlink(dev.c_str(), buf, sizeof(buf) - 1);
+    link = k > 0 ? std::string(buf, k) : n;
+    link = link.substr(link.find_last_of('/') + 1);  // PCI address, e.g. 0000:05:00.0
+    if (!seen.insert(link).second) continue;
+    int node = read_file(dev + "/numa_node", numa) ? atoi(numa.c_str()) : 0;
+    gpus.emplace_back(link, node < 0 ? 0 : node);
+  }
+  closedir(d);
+  std::sort(gpus.begin(), gpus.end());
+  std::vector<int> out;
+  for (auto& g : gpus) out.push_back(g.second);
+  return out;
+}
+
+std::vector<int> node_cpus(int node) {
+  std::string s;
+  if (!read_file(topo_root() + "/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", s)) return {};
+  return parse_cpulist(s);
+}
+
+// CPU set of every local rank: GPU/NUMA-aware when the topology is readable, else equal slices
+std::vector<std::vector<int>> plan_binding(int nproc, const std::vector<int>& allowed, std::string& how) {
+  std::vector<std::vector<int>> plan(nproc);
+  const std::vector<int> numa = gpu_numa_nodes();
+  std::set<int> allow(allowed.begin(), allowed.end());
+  bool ok = !numa.empty();
+  if (ok) {
+    std::map<int, std::vector<int>> ranks_on;  // node -> local ranks whose GPU is on it
+    for (int r = 0; r < nproc; ++r) ranks_on[numa[r % numa.size()]].push_back(r);
+    for (auto& kv : ranks_on) {
+      std::vector<int> cpus;
+      for (int c : node_cpus(kv.first))
+        if (allow.count(c)) cpus.push_back(c);
+      if (cpus.empty()) { ok = false; break; }
+      const int k = (int)kv.second.size();
+      const int per = std::max<int>(1, (int)cpus.size() / k);
+      for (int j = 0; j < k; ++j)
+        for (int c = j * per; c < (j + 1) * per && c < (int)cpus.size(); ++c) plan[kv.second[j]].push_back(cpus[c]);
+    }
+  }
+  if (ok) {
+    how = "numa";
+    return plan;
+  }
+  how = "slices";
+  plan.assign(nproc, {});
+  const int per = std::max<int>(1, (int)allowed.size() / nproc);
+  for (int r = 0; r < nproc; ++r)
+    for (int c = r * per; c < (r + 1) * per && c < (int)allowed.size(); ++c) plan[r].push_back(allowed[c]);
+  return plan;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   int nproc = 1, node_rank = 0, nnodes = 1, grace = 10;
   std::string master_addr = "127.0.0.1", master_port = "29500", host = "algo-1";
-  bool tag = false, bind = false;
+  bool tag = false, bind = false, print_binding = false;
   std::vector<std::string> extra_env, rank_env;
   int i = 1;
   for (; i < argc; ++i) {
@@ -97,14 +207,25 @@ int main(int argc, char** argv) {
     else if (a == "--grace") grace = atoi(next().c_str());
     else if (a == "--tag-output") tag = true;
     else if (a == "--bind-cpus") bind = true;
+    else if (a == "--print-binding") print_binding = true;
     else if (a == "-x") extra_env.push_back(next());
     else if (a == "--rank-env") rank_env.push_back(next());  // KEY=PREFIX -> KEY=PREFIX<rank+1>
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 2; }
   }
+  std::vector<int> cpus = allowed_cpus();
+  std::string how;
+  const std::vector<std::vector<int>> binding = plan_binding(std::max(1, nproc), cpus, how);
+  if (print_binding) {
+    for (int r = 0; r < nproc; ++r) {
+      printf("rank %d (%s):", r, how.c_str());
+      for (int c : binding[r]) printf(" %d", c);
+      printf("\n");
+    }
+    return 0;
+  }
   if (i >= argc || nproc < 1) { usage(); return 2; }
   char** cmd = argv + i;
   const int world = nproc * nnodes;
-  std::vector<int> cpus = allowed_cpus();
 
   struct sigaction sa;
   memset(&sa, 0, sizeof(sa));
@@ -146,13 +267,12 @@ int main(int argc, char** argv) {
         if (eq != std::string::npos)
           setenv(kv.substr(0, eq).c_str(), (kv.substr(eq + 1) + std::to_string(rank + 1)).c_str(), 1);
       }
-      if (bind && !cpus.empty()) {
-        const int per = std::max<int>(1, (int)cpus.size() / nproc);
+      if (bind && !binding[lr].empty()) {
         cpu_set_t set_;
         CPU_ZERO(&set_);
-        for (int c = lr * per; c < (lr + 1) * per && c < (int)cpus.size(); ++c) CPU_SET(cpus[c], &set_);
+        for (int c : binding[lr]) CPU_SET(c, &set_);
         sched_setaffinity(0, sizeof(set_), &set_);
-        set("OMP_NUM_THREADS", std::to_string(per));
+        set("OMP_NUM_THREADS", std::to_string(binding[lr].size()));
       }
       execvp(cmd[0], cmd);
       fprintf(stderr, "mi355x_launch: exec %s failed: %s\n", cmd[0], strerror(errno));

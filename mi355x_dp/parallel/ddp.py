@@ -123,6 +123,7 @@ class DataParallel(nn.Module):
         self.comm_on = self.distributed and (self.world_size > 1 or force_comm)
         self.check_stream_order = bool(check_stream_order)
         self.order_violations = []
+        self._buf_works = []
 
         params = [p for p in module.parameters() if p.requires_grad]
         params = list(reversed(params))  # approximate backward order
@@ -306,12 +307,26 @@ class DataParallel(nn.Module):
     # ------------------------------------------------------------ public
     def forward(self, *args, **kwargs):
         self._reset()
+        self._wait_buffer_sync()
+        out = self.module(*args, **kwargs)
         if self.broadcast_buffers and self.buffers.buffers and self.module.training:
-            dist.broadcast(self.buffers.data, 0, group=self.process_group)
-        return self.module(*args, **kwargs)
+            # torch DDP broadcasts rank 0's buffers synchronously BEFORE every training forward
+            # (SURVEY.md X4), on the critical path.  Same values, off the critical path: broadcast
+            # AFTER this forward's BN kernels (which update the running statistics) are enqueued;
+            # the comm stream runs it behind backward, and it is waited for before the next
+            # forward -- when every rank again starts from rank 0's buffers.  Backward never
+            # touches the buffers, and the broadcast precedes every bucket collective on all ranks.
+            self._buf_works.append(dist.broadcast(self.buffers.data, 0, group=self.process_group, async_op=True))
+        return out
+
+    def _wait_buffer_sync(self):
+        for w in self._buf_works:
+            w.wait()
+        self._buf_works = []
 
     def finish_gradient_sync(self, average: bool = False):
         """Launch any bucket not yet launched (unused params), then wait for all."""
+        self._wait_buffer_sync()
         if self.reducer is not None:
             self.reducer.finish()
             if average and self.world_size > 1:
@@ -338,6 +353,7 @@ class DataParallel(nn.Module):
         self.flat.zero_grad()
 
     def state_dict(self, *args, **kwargs):
+        self._wait_buffer_sync()
         return super().state_dict(*args, **kwargs)
 
 

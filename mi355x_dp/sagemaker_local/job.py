@@ -134,7 +134,11 @@ class TrainingJob:
         print("Invoking script with the following command:\n" + " ".join(cmd), flush=True)
         t_train = time.time()
         rank_env = {"SM_CURRENT_HOST": "algo-"} if per_host and len(hosts) > 1 else None
-        rc = launch(cmd, nproc=nproc, env=env, tag_output=nproc > 1, rank_env=rank_env, cwd=self.code_dir)
+        # multi-rank jobs pin each rank to CPUs of its GPU's NUMA node (the reference's mpirun bound
+        # ranks to their GPU's socket, nb2:380); MI355X_DP_BIND_CPUS=0 turns it off
+        bind = nproc > 1 and os.environ.get("MI355X_DP_BIND_CPUS", "1") != "0"
+        rc = launch(cmd, nproc=nproc, env=env, tag_output=nproc > 1, rank_env=rank_env, cwd=self.code_dir,
+                    bind_cpus=bind)
         self.exit_code = rc
         self.training_seconds = int(round(time.time() - t_train))
         if rc != 0:

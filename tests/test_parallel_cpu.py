@@ -303,3 +303,56 @@ def test_force_comm_world1():
     from mi355x_dp.parallel import _reducer_native
     if _reducer_native.load() is not None:
         assert trace[:nb] == list(range(nb)) and trace[-1] == -1
+
+
+class _BNNet(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.c = torch.nn.Conv2d(3, 8, 3)
+        self.bn = torch.nn.BatchNorm2d(8)
+        self.fc = torch.nn.Linear(8, 10)
+
+    def forward(self, x):
+        return self.fc(torch.relu(self.bn(self.c(x))).mean((2, 3)))
+
+
+def _worker_buffers(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        torch.manual_seed(0)
+        m = DataParallel(_BNNet(), min_bucket_mb=0)
+        opt = FlatSGD(m, lr=0.05, momentum=0.9)
+        x, y = _data()
+        shard = slice(rank * 8, (rank + 1) * 8)
+        seen = []
+        for _ in range(3):
+            opt.zero_grad()
+            out = m(x[shard] * (1 + rank))  # different batch statistics per rank
+            torch.nn.functional.cross_entropy(out, y[shard]).backward()
+            opt.step()
+            seen.append(m.module.bn.running_mean.clone().numpy())
+        q.put((rank, seen, int(m.module.bn.num_batches_tracked)))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None))
+        raise
+
+
+def test_buffer_broadcast_async():
+    """BN buffers are broadcast from rank 0 asynchronously behind backward (not before every
+    forward): after each optimizer step every rank holds rank 0's post-forward running stats."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_buffers, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (s, n) for r, s, n in [q.get(timeout=120) for _ in ps]}
+    for p in ps:
+        p.join(60)
+    for r, (s, n) in res.items():
+        assert not isinstance(s, Exception), repr(s)
+        assert n == 3
+    for a, b in zip(res[0][0], res[1][0]):
+        assert (a == b).all()

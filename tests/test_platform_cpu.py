@@ -140,3 +140,68 @@ def test_model_archive_path_traversal_refused(tmp_path):
         tf.addfile(ti, io.BytesIO(data))
     with pytest.raises(ValueError):
         extract_model(str(evil))
+
+
+def _fake_topology(root, gpus, nodes):
+    """gpus: [(pci_address, numa_node)]; nodes: {node: cpulist}"""
+    for i, (pci, node) in enumerate(gpus):
+        dev = root / "pci" / pci
+        dev.mkdir(parents=True)
+        (dev / "vendor").write_text("0x1002\n")
+        (dev / "class").write_text("0x120000\n")
+        (dev / "numa_node").write_text(f"{node}\n")
+        card = root / "sys" / "class" / "drm" / f"card{i}"
+        card.mkdir(parents=True)
+        (card / "device").symlink_to(dev)
+        (root / "sys" / "class" / "drm" / f"card{i}-DP-1").mkdir()  # connector entries are skipped
+    other = root / "pci" / "0000:ff:00.0"  # a non-AMD display device is ignored
+    other.mkdir(parents=True)
+    (other / "vendor").write_text("0x10de\n")
+    (other / "class").write_text("0x030000\n")
+    (root / "sys" / "class" / "drm" / "card99").mkdir()
+    (root / "sys" / "class" / "drm" / "card99" / "device").symlink_to(other)
+    for n, cpus in nodes.items():
+        d = root / "sys" / "devices" / "system" / "node" / f"node{n}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cpus + "\n")
+
+
+def _binding(root, nproc):
+    from mi355x_dp.launch import ensure_launcher
+    r = subprocess.run([ensure_launcher(), "--nproc", str(nproc), "--print-binding"], capture_output=True, text=True,
+                       env={**os.environ, "MI355X_DP_TOPO_ROOT": str(root)}, timeout=30)
+    assert r.returncode == 0, r.stderr
+    plan = {}
+    for line in r.stdout.splitlines():
+        head, cpus = line.split(":")
+        plan[int(head.split()[1])] = (head.split("(")[1].rstrip(")"), [int(c) for c in cpus.split()])
+    return plan
+
+
+def test_launcher_numa_binding(tmp_path):
+    """--bind-cpus pins local rank r (driving GPU r) to CPUs of GPU r's NUMA node; GPUs are taken in
+    PCI order (= HIP device order) and alternate between two nodes here, so ranks 0,2,4,6 share
+    node 0's CPUs and 1,3,5,7 node 1's.  Without a readable topology: equal slices."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 4:
+        pytest.skip("needs >= 4 allowed CPUs")
+    half = len(allowed) // 2
+    n0, n1 = allowed[:half], allowed[half:2 * half]
+    gpus = [(f"0000:{0x05 + 0x10 * i:02x}:00.0", i % 2) for i in range(8)]
+    import random
+    random.Random(0).shuffle(gpus)  # directory order must not matter, PCI order does
+    _fake_topology(tmp_path, gpus, {0: ",".join(map(str, n0)), 1: ",".join(map(str, n1))})
+    plan = _binding(tmp_path, 8)
+    assert all(how == "numa" for how, _ in plan.values())
+    for r in range(8):
+        node_cpus = n0 if r % 2 == 0 else n1
+        assert plan[r][1] and set(plan[r][1]) <= set(node_cpus), (r, plan[r])
+    # the 4 ranks of a node get disjoint, equal shares of it
+    for node_ranks in ((0, 2, 4, 6), (1, 3, 5, 7)):
+        sets = [set(plan[r][1]) for r in node_ranks]
+        assert len(set(map(len, sets))) == 1
+        assert sum(map(len, sets)) == len(set().union(*sets))
+    # unreadable topology -> contiguous equal slices of the allowed set
+    plan = _binding(tmp_path / "missing", 4)
+    assert all(how == "slices" for how, _ in plan.values())
+    assert plan[0][1][0] == allowed[0]
