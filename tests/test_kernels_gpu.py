@@ -24,6 +24,12 @@ def rel_err(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-6))
 
 
+def rel_l2(a, b):
+    a = a.detach().float()
+    b = b.detach().float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
 CONV_SHAPES = [
     # N, C, H, K, R, stride, pad
     (4, 64, 56, 64, 1, 1, 0),
@@ -293,9 +299,12 @@ def test_resnet18_train_step_matches_fp32():
     F.cross_entropy(st(x.to(BF).contiguous(memory_format=CL)).float(), y).backward()
     assert abs(float(loss.detach()) - float(loss_r.detach())) < 0.05 * max(1.0, abs(float(loss_r.detach())))
     pn, pr, ps = dict(m.named_parameters()), dict(ref.named_parameters()), dict(st.named_parameters())
+    # norm-wise relative error: the max-element metric of a BN affine gradient at batch 8 is
+    # dominated by single cancellation-heavy channels and swings run to run with stock MIOpen's
+    # own nondeterminism (its error on layer2.1.bn1.weight alone: 0.25 .. 0.30)
     for n in pr:
-        e_native = rel_err(pn[n].grad, pr[n].grad)
-        e_stock = rel_err(ps[n].grad, pr[n].grad)
+        e_native = rel_l2(pn[n].grad, pr[n].grad)
+        e_stock = rel_l2(ps[n].grad, pr[n].grad)
         assert e_native <= 1.5 * e_stock + 0.02, (n, e_native, e_stock)
 
 
