@@ -34,6 +34,12 @@
 #ifndef MI_NT_BLOCKS_PER_CU
 #define MI_NT_BLOCKS_PER_CU 4
 #endif
+#ifndef MI_NT64_BLOCKS_PER_CU
+#define MI_NT64_BLOCKS_PER_CU 4  // BN = 64 tiles (24.6 KB of LDS)
+#endif
+#ifndef MI_TN_BLOCKS_PER_CU
+#define MI_TN_BLOCKS_PER_CU 3
+#endif
 #ifndef MI_TN_NOATOMIC
 #define MI_TN_NOATOMIC 0  // timing experiment only: split-K partials stored, not added (wrong results)
 #endif
@@ -119,9 +125,9 @@ constexpr int nt_smem_u4() {
 
 // blocks per CU the NT kernel is compiled for: 4 single-stage blocks (38 KB of LDS each at 128x128,
 // <= 128 VGPRs) keep more k-steps and epilogues of the short-K 1x1 convs in flight than 3 did
-template <int STAGES, bool HALO>
+template <int BN, int STAGES, bool HALO>
 constexpr int nt_occupancy() {
-  return HALO ? 2 : (STAGES == 1 ? MI_NT_BLOCKS_PER_CU : 2);
+  return HALO ? 2 : (STAGES == 1 ? (BN == 64 ? MI_NT64_BLOCKS_PER_CU : MI_NT_BLOCKS_PER_CU) : 2);
 }
 
 // STAGES = 1: one LDS buffer, load -> barrier -> MFMA -> barrier per k-step, 3 blocks per CU (the other
@@ -136,7 +142,7 @@ constexpr int nt_occupancy() {
 // weight tile of the next tap loading into the other B buffer during each tap's MFMAs.  The
 // per-tap gather re-reads every input pixel ~9x through L2; the halo reads it ~(rp+2)/rp x.
 template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false>
-__global__ __launch_bounds__(256, (nt_occupancy<STAGES, HALO>())) void nt_kernel(NTArgs a) {
+__global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_kernel(NTArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
@@ -589,7 +595,7 @@ __device__ __forceinline__ int tr_swz(int k) {
 }
 
 template <int BM, int BN, int STAGES>
-__global__ __launch_bounds__(256, STAGES == 1 ? 3 : 2) void tn_kernel(TNArgs a) {
+__global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn_kernel(TNArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int AU = BM / 4, BU = BN / 4;            // 8-byte units per LDS row
