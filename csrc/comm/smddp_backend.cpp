@@ -22,6 +22,11 @@
 //   * allreduce AVG maps to ncclAvg; large all-reduces can be split into link-sized
 //     chunks queued back to back (MI355X_DP_SMDDP_CHUNK_MB) so a long bucket does not
 //     hold the comm stream in one monolithic kernel;
+//   * MI355X_DP_SMDDP_IPC_ONLY=1: no RCCL communicator at all -- every all-reduce (fp32 SUM/AVG
+//     through the one/two-shot kernels in slot-sized chunks, other dtypes / MAX / MIN through a
+//     generic one-shot kernel), broadcast (copy from the root's slot) and barrier (a flag round)
+//     runs over the IPC buffers: a single-node xGMI backend, and the only way several ranks can
+//     share one GPU (RCCL refuses that) for multi-rank rehearsals with real comm kernels;
 //   * MI355X_DP_SMDDP_IPC=1: fp32 SUM/AVG all-reduces up to MI355X_DP_SMDDP_IPC_MB (default 4)
 //     take a one-shot (<= MI355X_DP_SMDDP_IPC_ONESHOT_KB, default 256) or two-shot
 //     (reduce-scatter + all-gather) path over IPC peer pointers instead of RCCL (latency-bound buckets,
@@ -186,8 +191,13 @@ class SmddpBackend : public c10d::Backend {
     if (const char* c = std::getenv("MI355X_DP_SMDDP_CHUNK_MB")) chunk_bytes_ = (size_t)(atof(c) * (1 << 20));
     if (const char* c = std::getenv("MI355X_DP_SMDDP_ABORT_ON_ERROR")) abort_on_error_ = c[0] != '0';
     const char* ipc = std::getenv("MI355X_DP_SMDDP_IPC");
-    if (ipc && ipc[0] == '1' && size > 1) setup_ipc();
-    if (!ipc_on_) comm();  // eager RCCL bootstrap unless the IPC path may serve the first collectives
+    const char* only = std::getenv("MI355X_DP_SMDDP_IPC_ONLY");
+    ipc_only_ = only && only[0] == '1';
+    if ((ipc && ipc[0] == '1') || ipc_only_) {
+      if (size > 1) setup_ipc();
+      TORCH_CHECK(!ipc_only_ || size == 1 || ipc_on_, "smddp: MI355X_DP_SMDDP_IPC_ONLY=1 but the IPC path is unavailable");
+    }
+    if (!ipc_on_ && !(ipc_only_ && size == 1)) comm();  // eager RCCL bootstrap unless IPC may serve the collectives
     watchdog_ = std::thread([this] { watchdog_loop(); });
     std::lock_guard<std::mutex> lk(g_live_mu);
     g_live.push_back(this);
@@ -214,6 +224,8 @@ class SmddpBackend : public c10d::Backend {
   // RCCL communicator, created on first use (ncclCommInitRank is collective: every rank reaches
   // it in the same collective because the RCCL / IPC choice depends only on the op's shape)
   ncclComm_t comm() {
+    TORCH_CHECK(!ipc_only_, "smddp: this collective needs RCCL, but MI355X_DP_SMDDP_IPC_ONLY=1 "
+                            "(IPC-only mode supports all-reduce, broadcast and barrier)");
     std::lock_guard<std::mutex> lk(init_mu_);
     if (!comm_) NCCLCHECK(ncclCommInitRank(&comm_, size_, uid_, rank_));
     return comm_;
@@ -236,14 +248,17 @@ class SmddpBackend : public c10d::Backend {
  private:
   using IpcFn = int (*)(const float* const*, uint32_t* const*, int, int, float*, int64_t, uint32_t, float, int*,
                         uint32_t, hipStream_t);
+  using Ipc1Fn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int, int, int, uint32_t, int*,
+                         uint32_t, hipStream_t);
 
   void setup_ipc() {
     const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
     void* h = lib ? dlopen(lib, RTLD_NOW | RTLD_GLOBAL) : nullptr;
     ipc_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce_f32") : nullptr;
     ipc2_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce2_f32") : nullptr;
+    ipc1_fn_ = h ? (Ipc1Fn)dlsym(h, "mi_ipc_oneshot") : nullptr;
     auto flag_bytes = h ? (int64_t (*)())dlsym(h, "mi_ipc_flag_bytes") : nullptr;
-    if (!ipc_fn_ || !ipc2_fn_ || !flag_bytes || size_ > 8) {
+    if (!ipc_fn_ || !ipc2_fn_ || !ipc1_fn_ || !flag_bytes || size_ > 8) {
       fprintf(stderr, "smddp: IPC all-reduce unavailable (kernel library %s); using RCCL only\n", lib ? lib : "unset");
       return;
     }
@@ -269,36 +284,104 @@ class SmddpBackend : public c10d::Backend {
       memcpy(&ph, v.data(), sizeof(ph));
       HIPCHECK(hipIpcOpenMemHandle(&ipc_base_[q], ph, hipIpcMemLazyEnablePeerAccess));
     }
+    // peers' flag waits are bounded spins (never a hang): long enough to absorb the host-side skew
+    // between ranks (start-up, Python), MI355X_DP_SMDDP_IPC_SPIN overrides the count (x s_sleep 8)
+    if (const char* c = std::getenv("MI355X_DP_SMDDP_IPC_SPIN")) ipc_spin_limit_ = (uint32_t)std::atoll(c);
+    else if (ipc_only_) ipc_spin_limit_ = 60000000u;
     HIPCHECK(hipHostMalloc((void**)&ipc_err_, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
     *ipc_err_ = 0;
     HIPCHECK(hipHostGetDevicePointer((void**)&ipc_err_dev_, ipc_err_, 0));
     ipc_on_ = true;
+    // start-up rendezvous through the store: every rank has opened every peer's buffer before any
+    // rank's first flag wait starts its bounded spin
+    store_->set("smddp/ipc_ready/" + std::to_string(rank_), std::vector<uint8_t>{1});
+    for (int q = 0; q < size_; ++q) store_->get("smddp/ipc_ready/" + std::to_string(q));
   }
 
   bool ipc_eligible(const std::vector<at::Tensor>& ts, const c10d::AllreduceOptions& opts) const {
     if (!ipc_on_ || ts.size() != 1) return false;
     const auto& t = ts[0];
-    return t.scalar_type() == at::kFloat && t.is_contiguous() && (size_t)t.numel() * 4 <= ipc_cap_ &&
+    return t.scalar_type() == at::kFloat && t.is_contiguous() && (ipc_only_ || (size_t)t.numel() * 4 <= ipc_cap_) &&
            (opts.reduceOp == c10d::ReduceOp::SUM || opts.reduceOp == c10d::ReduceOp::AVG);
   }
 
-  void ipc_allreduce(at::Tensor& t, bool avg, hipStream_t s) {
-    const uint32_t epoch = ++ipc_epoch_;
+  // the slots of call `epoch` in every rank's buffer
+  void ipc_slots(uint32_t epoch, const void** data, uint32_t** flags) const {
     const size_t slot = (epoch & 1) * ipc_cap_;
-    const float* data[8];
-    uint32_t* flags[8];
     for (int q = 0; q < size_; ++q) {
-      data[q] = (const float*)((char*)ipc_base_[q] + slot);
+      data[q] = (const char*)ipc_base_[q] + slot;
       flags[q] = (uint32_t*)((char*)ipc_base_[q] + 2 * ipc_cap_);
     }
-    HIPCHECK(hipMemcpyAsync((char*)ipc_base_[rank_] + slot, t.data_ptr(), t.numel() * 4, hipMemcpyDeviceToDevice, s));
-    // one-shot (one flag round, every peer's whole bucket read) for latency-bound sizes, two-shot
-    // (reduce-scatter + all-gather, 2/world of the bucket per link) above the threshold
-    IpcFn fn = (size_t)t.numel() * 4 <= ipc_oneshot_bytes_ ? ipc_fn_ : ipc2_fn_;
-    const int rc = fn(data, flags, rank_, size_, (float*)t.data_ptr(), t.numel(), epoch,
-                      avg ? 1.f / size_ : 1.f, ipc_err_dev_, ipc_spin_limit_, s);
-    TORCH_CHECK(rc == 0, "smddp: IPC all-reduce launch failed with hipError ", rc);
   }
+
+  // fp32 SUM / AVG of any size: slot-sized chunks, each one call of the one-shot (latency-bound
+  // sizes) or two-shot (reduce-scatter into the own slot + all-gather: 2/world of the chunk per
+  // xGMI link) kernel; chunks pipeline through the two alternating slots on the comm stream
+  void ipc_allreduce(at::Tensor& t, bool avg, hipStream_t s) {
+    const int64_t n = t.numel(), per = (int64_t)(ipc_cap_ / 4);
+    for (int64_t off = 0; off < n || (n == 0 && off == 0); off += per) {
+      const int64_t cnt = std::min(per, n - off);
+      const uint32_t epoch = ++ipc_epoch_;
+      const void* data[8];
+      uint32_t* flags[8];
+      ipc_slots(epoch, data, flags);
+      float* src = (float*)t.data_ptr() + off;
+      if (cnt > 0) HIPCHECK(hipMemcpyAsync((void*)data[rank_], src, cnt * 4, hipMemcpyDeviceToDevice, s));
+      IpcFn fn = (size_t)cnt * 4 <= ipc_oneshot_bytes_ ? ipc_fn_ : ipc2_fn_;
+      if (ipc_trace_)
+        fprintf(stderr, "[smddp ipc] rank %d epoch %u allreduce%s f32 n=%lld\n", rank_, epoch,
+                fn == ipc_fn_ ? "1" : "2", (long long)cnt);
+      const int rc = fn((const float* const*)data, flags, rank_, size_, src, cnt, epoch, avg ? 1.f / size_ : 1.f,
+                        ipc_err_dev_, ipc_spin_limit_, s);
+      TORCH_CHECK(rc == 0, "smddp: IPC all-reduce launch failed with hipError ", rc);
+      if (n == 0) break;
+    }
+  }
+
+  // IPC-only mode: any dtype / op through the generic one-shot kernel (op 3 = copy from root,
+  // nbytes 0 = barrier), chunked like ipc_allreduce
+  void ipc_generic(void* ptr, int64_t nbytes, int dtype, int op, int root, hipStream_t s) {
+    const int64_t per = (int64_t)ipc_cap_;
+    for (int64_t off = 0; off < nbytes || (nbytes == 0 && off == 0); off += per) {
+      const int64_t cnt = std::min(per, nbytes - off);
+      const uint32_t epoch = ++ipc_epoch_;
+      const void* data[8];
+      uint32_t* flags[8];
+      ipc_slots(epoch, data, flags);
+      char* p = (char*)ptr + off;
+      if (ipc_trace_)
+        fprintf(stderr, "[smddp ipc] rank %d epoch %u generic op=%d dtype=%d root=%d bytes=%lld\n", rank_, epoch, op,
+                dtype, root, (long long)cnt);
+      if (cnt > 0 && (op != 3 || rank_ == root))
+        HIPCHECK(hipMemcpyAsync((void*)data[rank_], p, cnt, hipMemcpyDeviceToDevice, s));
+      const int rc = ipc1_fn_(data, flags, rank_, size_, p, std::max<int64_t>(cnt, 0), dtype, op, root, epoch,
+                              ipc_err_dev_, ipc_spin_limit_, s);
+      TORCH_CHECK(rc == 0, "smddp: IPC collective launch failed with hipError ", rc);
+      if (nbytes == 0) break;
+    }
+  }
+
+  static int ipc_dtype(at::ScalarType t) {
+    switch (t) {
+      case at::kFloat: return 0;
+      case at::kDouble: return 1;
+      case at::kInt: return 2;
+      case at::kLong: return 3;
+      default: return -1;
+    }
+  }
+
+  static int ipc_op(const c10d::ReduceOp& op) {
+    switch (op) {
+      case c10d::ReduceOp::SUM: return 0;
+      case c10d::ReduceOp::MAX: return 1;
+      case c10d::ReduceOp::MIN: return 2;
+      default: return -1;
+    }
+  }
+
+  // single rank in IPC-only mode (no RCCL): every collective is the identity
+  bool solo() const { return ipc_only_ && size_ == 1; }
 
  public:
 
@@ -340,9 +423,21 @@ class SmddpBackend : public c10d::Backend {
   // ------------------------------------------------------------ collectives
   c10::intrusive_ptr<c10d::Work> allreduce(std::vector<at::Tensor>& tensors,
                                            const c10d::AllreduceOptions& opts) override {
+    if (solo()) return run(c10d::OpType::ALLREDUCE, tensors, tensors, [](hipStream_t) {});
     if (ipc_eligible(tensors, opts)) {
       const bool avg = opts.reduceOp == c10d::ReduceOp::AVG;
       return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) { ipc_allreduce(tensors[0], avg, s); });
+    }
+    if (ipc_only_) {
+      for (auto& t : tensors) {
+        const int dt = ipc_dtype(t.scalar_type()), op = ipc_op(opts.reduceOp);
+        TORCH_CHECK(dt >= 0 && op >= 0 && t.is_contiguous(), "smddp IPC-only all-reduce: unsupported dtype / op");
+      }
+      return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) {
+        for (auto& t : tensors)
+          ipc_generic(t.data_ptr(), t.numel() * t.element_size(), ipc_dtype(t.scalar_type()), ipc_op(opts.reduceOp), 0,
+                      s);
+      });
     }
     auto op = to_nccl(opts.reduceOp);
     return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) {
@@ -364,6 +459,13 @@ class SmddpBackend : public c10d::Backend {
 
   c10::intrusive_ptr<c10d::Work> broadcast(std::vector<at::Tensor>& tensors,
                                            const c10d::BroadcastOptions& opts) override {
+    if (solo()) return run(c10d::OpType::BROADCAST, tensors, tensors, [](hipStream_t) {});
+    if (ipc_only_) {
+      for (auto& t : tensors) TORCH_CHECK(t.is_contiguous(), "smddp IPC-only broadcast: tensor must be contiguous");
+      return run(c10d::OpType::BROADCAST, tensors, tensors, [&](hipStream_t s) {
+        for (auto& t : tensors) ipc_generic(t.data_ptr(), t.numel() * t.element_size(), 0, 3, (int)opts.rootRank, s);
+      });
+    }
     return run(c10d::OpType::BROADCAST, tensors, tensors, [&](hipStream_t s) {
       NCCLCHECK(ncclGroupStart());
       for (auto& t : tensors)
@@ -456,6 +558,10 @@ class SmddpBackend : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> barrier(const c10d::BarrierOptions&) override {
     auto t = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(c10::Device(c10::DeviceType::CUDA,
                                                                                       (c10::DeviceIndex)device_)));
+    if (solo()) return run(c10d::OpType::BARRIER, {t}, {t}, [](hipStream_t) {}, /*blocking=*/true);
+    if (ipc_only_)
+      return run(c10d::OpType::BARRIER, {t}, {t}, [&](hipStream_t s) { ipc_generic(nullptr, 0, 0, 0, 0, s); },
+                 /*blocking=*/true);
     return run(c10d::OpType::BARRIER, {t}, {t}, [&](hipStream_t s) {
       NCCLCHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), 1, ncclFloat32, ncclSum, comm(), s));
     }, /*blocking=*/true);
@@ -535,6 +641,9 @@ class SmddpBackend : public c10d::Backend {
   bool ipc_on_ = false;
   IpcFn ipc_fn_ = nullptr;
   IpcFn ipc2_fn_ = nullptr;
+  Ipc1Fn ipc1_fn_ = nullptr;
+  bool ipc_only_ = false;
+  bool ipc_trace_ = std::getenv("MI355X_DP_SMDDP_IPC_TRACE") != nullptr;
   size_t ipc_cap_ = 4u << 20;
   size_t ipc_oneshot_bytes_ = 256u << 10;  // MI355X_DP_SMDDP_IPC_ONESHOT_KB
   std::vector<void*> ipc_base_;

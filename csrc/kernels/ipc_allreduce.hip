@@ -18,6 +18,15 @@
 // finishing its own call e (stream order).
 #include "common.h"
 
+// Grid cap of every IPC collective kernel.  Their blocks spin on peer flags, and the dispatcher
+// spreads a grid one block per CU: a 256-block spinner leaves no CU whose register file can take a
+// full-CU compute block (gemm256: 8 waves x 256 VGPRs), so backward on the same GPU stalls behind
+// the collective -- and with two ranks sharing a GPU the peer's backward never reaches its
+// collective at all (a deadlock until the spin bound).  64 blocks keep 3/4 of the CUs free.
+#ifndef MI_IPC_MAX_GRID
+#define MI_IPC_MAX_GRID 64
+#endif
+
 namespace {
 
 constexpr int IPC_MAX_PEERS = 8;
@@ -189,7 +198,8 @@ MI_API int mi_ipc_allreduce2_f32(const float* const* data, uint32_t* const* flag
     vec = vec && ((uintptr_t)data[q] & 15) == 0;
   }
   const int64_t shard = ((n + world - 1) / world + 3) & ~(int64_t)3;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(IPC_MAX_BLOCKS2, (shard + 2047) / 2048));
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(IPC_MAX_BLOCKS2, MI_IPC_MAX_GRID),
+                                                                  (shard + 2047) / 2048));
   const int64_t chunk = ((shard + blocks - 1) / blocks + 3) & ~(int64_t)3;
   if (vec)
     hipLaunchKernelGGL(ipc_allreduce2_kernel<true>, dim3(blocks), dim3(256), 0, st, p, rank, world, out, n, shard,
@@ -207,8 +217,121 @@ MI_API int mi_ipc_allreduce_f32(const float* const* data, uint32_t* const* flags
   if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || n < 0) return (int)hipErrorInvalidValue;
   IpcPeers p{};
   for (int q = 0; q < world; ++q) { p.data[q] = data[q]; p.flags[q] = flags[q]; }
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(256, (n + 255) / 256));
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(MI_IPC_MAX_GRID, (n + 255) / 256));
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(blocks), dim3(256), 0, st, p, rank, world, out, n, epoch, scale, err,
                      spin_limit);
   return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic one-shot collective over the same slots / flags, for the smddp backend's IPC-only mode
+// (MI355X_DP_SMDDP_IPC_ONLY=1: no RCCL communicator at all -- single-node xGMI, and several ranks
+// may share one GPU for rehearsals): op SUM / MAX / MIN over f32 / f64 / i32 / i64, COPY = every
+// rank takes the root's slot (broadcast), and a zero-byte call is a barrier (flag round only).
+namespace {
+
+enum { IPC_SUM = 0, IPC_MAX = 1, IPC_MIN = 2, IPC_COPY = 3 };
+
+struct IpcRaw {
+  const void* data[IPC_MAX_PEERS];
+  uint32_t* flags[IPC_MAX_PEERS];
+};
+
+__device__ __forceinline__ bool ipc_handshake(const IpcRaw& p, int rank, int world, uint32_t epoch, int* err,
+                                              uint32_t spin_limit) {
+  __shared__ int ok;
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)world) {
+    __threadfence_system();
+    __hip_atomic_store(p.flags[threadIdx.x] + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    bool good = true;
+    for (int q = 0; q < world && good; ++q) good = ipc_wait_ge(p.flags[rank] + q, epoch, spin_limit, spins);
+    if (!good) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ok = good;
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ T ipc_combine(T a, T b) {
+  if (OP == IPC_SUM) return a + b;
+  if (OP == IPC_MAX) return a > b ? a : b;
+  return a < b ? a : b;
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void ipc_oneshot_kernel(IpcRaw p, int rank, int world, T* __restrict__ out,
+                                                          int64_t n, int root, uint32_t epoch, int* err,
+                                                          uint32_t spin_limit) {
+  if (!ipc_handshake(p, rank, world, epoch, err, spin_limit)) return;
+  if (OP == IPC_COPY && rank == root) return;  // the root's tensor is the source
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (OP == IPC_COPY) {
+      out[i] = __builtin_nontemporal_load((const T*)p.data[root] + i);
+    } else {
+      T v = __builtin_nontemporal_load((const T*)p.data[0] + i);
+#pragma unroll 1
+      for (int q = 1; q < world; ++q) v = ipc_combine<T, OP>(v, __builtin_nontemporal_load((const T*)p.data[q] + i));
+      out[i] = v;
+    }
+  }
+}
+
+template <typename T, int OP>
+void launch_oneshot(const IpcRaw& p, int rank, int world, void* out, int64_t n, int root, uint32_t epoch, int* err,
+                    uint32_t spin_limit, hipStream_t st) {
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(MI_IPC_MAX_GRID, (n + 255) / 256));
+  hipLaunchKernelGGL((ipc_oneshot_kernel<T, OP>), dim3(blocks), dim3(256), 0, st, p, rank, world, (T*)out, n, root,
+                     epoch, err, spin_limit);
+}
+
+template <typename T>
+int dispatch_oneshot(int op, const IpcRaw& p, int rank, int world, void* out, int64_t n, int root, uint32_t epoch,
+                     int* err, uint32_t spin_limit, hipStream_t st) {
+  switch (op) {
+    case IPC_SUM: launch_oneshot<T, IPC_SUM>(p, rank, world, out, n, root, epoch, err, spin_limit, st); break;
+    case IPC_MAX: launch_oneshot<T, IPC_MAX>(p, rank, world, out, n, root, epoch, err, spin_limit, st); break;
+    case IPC_MIN: launch_oneshot<T, IPC_MIN>(p, rank, world, out, n, root, epoch, err, spin_limit, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// dtype: 0 f32, 1 f64, 2 i32, 3 i64 (ignored for COPY); op: 0 SUM, 1 MAX, 2 MIN, 3 COPY (root's slot);
+// nbytes: bytes of this call's slot payload (0 = barrier).  Same slot / flag protocol and epochs as
+// mi_ipc_allreduce_f32.
+MI_API int mi_ipc_oneshot(const void* const* data, uint32_t* const* flags, int rank, int world, void* out,
+                          int64_t nbytes, int dtype, int op, int root, uint32_t epoch, int* err, uint32_t spin_limit,
+                          hipStream_t st) {
+  if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || nbytes < 0 || root < 0 || root >= world ||
+      op < 0 || op > IPC_COPY)
+    return (int)hipErrorInvalidValue;
+  IpcRaw p{};
+  bool al16 = ((uintptr_t)out & 15) == 0;
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = data[q];
+    p.flags[q] = flags[q];
+    al16 = al16 && ((uintptr_t)data[q] & 15) == 0;
+  }
+  if (op == IPC_COPY) {
+    if (al16 && nbytes % 16 == 0)
+      launch_oneshot<u32x4, IPC_COPY>(p, rank, world, out, nbytes / 16, root, epoch, err, spin_limit, st);
+    else if (nbytes % 4 == 0)
+      launch_oneshot<uint32_t, IPC_COPY>(p, rank, world, out, nbytes / 4, root, epoch, err, spin_limit, st);
+    else
+      launch_oneshot<uint8_t, IPC_COPY>(p, rank, world, out, nbytes, root, epoch, err, spin_limit, st);
+    return (int)hipGetLastError();
+  }
+  switch (dtype) {
+    case 0: return dispatch_oneshot<float>(op, p, rank, world, out, nbytes / 4, root, epoch, err, spin_limit, st);
+    case 1: return dispatch_oneshot<double>(op, p, rank, world, out, nbytes / 8, root, epoch, err, spin_limit, st);
+    case 2: return dispatch_oneshot<int32_t>(op, p, rank, world, out, nbytes / 4, root, epoch, err, spin_limit, st);
+    case 3: return dispatch_oneshot<int64_t>(op, p, rank, world, out, nbytes / 8, root, epoch, err, spin_limit, st);
+    default: return (int)hipErrorInvalidValue;
+  }
 }

@@ -183,6 +183,61 @@ def test_smddp_ipc_oneshot_allreduce_two_ranks(tmp_path, oneshot_kb):
     assert r.stdout.count("IPC_OK") == 2
 
 
+def test_smddp_ipc_only_two_ranks(tmp_path):
+    """IPC-only smddp (MI355X_DP_SMDDP_IPC_ONLY=1: no RCCL communicator): 2 ranks sharing cuda:0.
+    fp32 SUM/AVG all-reduces far larger than the 1 MB slot (chunked two-shot), fp64 MAX, int64 SUM,
+    fp32 MIN (generic one-shot), broadcasts of fp32 / odd-sized uint8 / int64 from either root, a
+    barrier -- then the DP engine's bucketed ResNet-18 training over it with bit-identical replicas."""
+    script = tmp_path / "ipc_only.py"
+    script.write_text(
+        "import os, sys, torch, torch.distributed as dist\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.append({os.path.join(ROOT, 'compat')!r})\n"
+        "import smdistributed.dataparallel.torch.torch_smddp\n"
+        "dist.init_process_group(backend='smddp')\n"
+        "r, w = dist.get_rank(), dist.get_world_size()\n"
+        "n = 3_000_001\n"
+        "for op in (dist.ReduceOp.SUM, dist.ReduceOp.AVG):\n"
+        "    t = torch.arange(n, device='cuda', dtype=torch.float32) * (r + 1)\n"
+        "    dist.all_reduce(t, op=op)\n"
+        "    ref = torch.arange(n, device='cuda', dtype=torch.float32) * 3 / (2 if op == dist.ReduceOp.AVG else 1)\n"
+        "    assert torch.allclose(t, ref, rtol=1e-6), (op, (t - ref).abs().max().item())\n"
+        "d = torch.tensor([1.5 + r, -r], device='cuda', dtype=torch.float64); dist.all_reduce(d, op=dist.ReduceOp.MAX)\n"
+        "assert d.tolist() == [2.5, 0.0], d\n"
+        "i = torch.full((300_001,), r + 1, device='cuda', dtype=torch.int64); dist.all_reduce(i)\n"
+        "assert int(i.min()) == 3 and int(i.max()) == 3\n"
+        "f = torch.full((5,), float(r), device='cuda'); dist.all_reduce(f, op=dist.ReduceOp.MIN)\n"
+        "assert float(f.max()) == 0.0\n"
+        "b = torch.arange(2_000_003, device='cuda', dtype=torch.float32) * (r + 7); dist.broadcast(b, 1)\n"
+        "assert torch.equal(b, torch.arange(2_000_003, device='cuda', dtype=torch.float32) * 8)\n"
+        "u = torch.full((1001,), 10 + r, device='cuda', dtype=torch.uint8); dist.broadcast(u, 0)\n"
+        "assert int(u.min()) == 10 and int(u.max()) == 10\n"
+        "l = torch.tensor([r * 100 + 1], device='cuda', dtype=torch.int64); dist.broadcast(l, 1)\n"
+        "assert int(l) == 101\n"
+        "dist.barrier()\n"
+        "from mi355x_dp.models import resnet18\n"
+        "from mi355x_dp.ops import cross_entropy\n"
+        "from mi355x_dp.parallel import DataParallel, FlatSGD\n"
+        "from mi355x_dp.parallel.health import ReplicaChecker\n"
+        "torch.manual_seed(r)\n"
+        "eng = DataParallel(resnet18(num_classes=10).cuda(), bucket_cap_mb=8, min_bucket_mb=0)\n"
+        "opt = FlatSGD(eng, lr=0.05, momentum=0.9)\n"
+        "g = torch.Generator(device='cuda').manual_seed(r)\n"
+        "for _ in range(3):\n"
+        "    x = torch.randn(16, 3, 32, 32, device='cuda', generator=g); y = torch.randint(0, 10, (16,), device='cuda', generator=g)\n"
+        "    eng.zero_grad(); cross_entropy(eng(x), y).backward(); opt.step()\n"
+        "assert ReplicaChecker(eng)(force=True)\n"
+        "assert eng.comm_calls >= 3 * len(eng.buckets), eng.comm_calls\n"
+        "torch.cuda.synchronize()\n"
+        "print('IPC_ONLY_OK', r, len(eng.buckets), flush=True)\n"
+        "dist.destroy_process_group()\n")
+    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC_ONLY": "1", "MI355X_DP_SMDDP_DEVICE": "0",
+           "MI355X_DP_SMDDP_IPC_MB": "1", "MI355X_DP_SMDDP_TERMINATE_TRACE": "1"}
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2", str(script)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("IPC_ONLY_OK") == 2
+
+
 @pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "mi355x_dp", "_native", "libmi355x_kernels_debug.so")),
                     reason="debug kernel library not built (python -m mi355x_dp.build kernels --debug)")
 def test_debug_kernels_training_step_clean(tmp_path):
