@@ -58,6 +58,13 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(1, torch.cuda.device_count()):
+        # ranks share GPUs (multi-rank rehearsal on a small box): with the default 4 hardware queues
+        # per process, 3+ processes oversubscribe the GPU's queue slots and the scheduler time-slices
+        # them -- gloo's host-synchronised copies then crawl (profiles/multirank_rehearsal.md).
+        # Must be set before the first HIP call (device_count() does not initialise HIP here).
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
