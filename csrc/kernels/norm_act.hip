@@ -10,6 +10,7 @@
 // The ReLU mask is recovered from the saved output y, so no mask tensor exists.
 // All loads/stores are 16-byte vectors (8 bf16 per lane).
 #include "common.h"
+#include <mutex>
 #include <algorithm>
 
 namespace {
@@ -856,31 +857,44 @@ inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const f
   return S;
 }
 
-// per-device arrival counters of slab_split_fin_kernel (one per 64-channel group, self-resetting)
-struct FinCounters { int* cnt = nullptr; int n = 0; };
+// Arrival counters of slab_split_fin_kernel (one per 64-channel group, reset by the finalizing
+// block).  Two finalizes in flight on DIFFERENT streams must not share counters, so every (device,
+// stream) gets its own slot of a table allocated up front by mi_bn_init_counters() (called when
+// the library is loaded -- never lazily, which would break a HIP graph capture).  A stream beyond
+// the table, or a device that was never initialised, takes the two-launch split + finalize path,
+// which needs no counters (same results, deterministic either way).
+constexpr int FIN_STREAM_SLOTS = 16, FIN_GROUPS = 128;  // 128 x 64 = 8192 channels
+struct FinCounters {
+  int* cnt = nullptr;  // [FIN_STREAM_SLOTS][FIN_GROUPS]
+  hipStream_t owner[FIN_STREAM_SLOTS] = {};
+  bool used[FIN_STREAM_SLOTS] = {};
+};
 static FinCounters g_fin_cnt[16];
-static int* fin_counters(int groups) {
+static std::mutex g_fin_mu;
+
+static int* fin_counters(int groups, hipStream_t st) {
+  if (groups > FIN_GROUPS) return nullptr;
   int dev = 0;
-  hipGetDevice(&dev);
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_fin_mu);
   FinCounters& w = g_fin_cnt[dev & 15];
-  if (w.n < groups) {
-    const int n = std::max(groups, 128);
-    int* p = nullptr;
-    if (hipMalloc(&p, sizeof(int) * n) != hipSuccess) return nullptr;
-    hipMemset(p, 0, sizeof(int) * n);
-    hipDeviceSynchronize();
-    if (w.cnt) hipFree(w.cnt);
-    w.cnt = p;
-    w.n = n;
-  }
-  return w.cnt;
+  if (!w.cnt) return nullptr;
+  for (int i = 0; i < FIN_STREAM_SLOTS; ++i)
+    if (w.used[i] && w.owner[i] == st) return w.cnt + i * FIN_GROUPS;
+  for (int i = 0; i < FIN_STREAM_SLOTS; ++i)
+    if (!w.used[i]) {
+      w.used[i] = true;
+      w.owner[i] = st;
+      return w.cnt + i * FIN_GROUPS;
+    }
+  return nullptr;
 }
 
 // finalize a [nblk][2][C] partial slab: one launch (finalize, or split + finalize for tall slabs)
 template <bool BWD>
 inline void slab_finalize(float* part, int nblk, const FinArgs& f, hipStream_t st) {
   const int C = f.C;
-  int* cnt = nblk > 256 ? fin_counters(cdiv(C, 64)) : nullptr;
+  int* cnt = nblk > 256 ? fin_counters(cdiv(C, 64), st) : nullptr;
   if (cnt) {
     const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, 128));
     const int rows_per = cdiv(nblk, S);
@@ -916,6 +930,23 @@ inline FinArgs fin_bwd_args(int M, int C, const float* gamma, const float* mean,
 }  // namespace
 
 MI_API int mi_bn_slab_extra_rows() { return SLAB_EXTRA_ROWS; }
+
+// Allocate the current device's finalize-counter table (zeroed, synchronously).  Idempotent; call
+// before any graph capture (the Python loader does, at library load).
+MI_API int mi_bn_init_counters() {
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return (int)e;
+  std::lock_guard<std::mutex> lk(g_fin_mu);
+  FinCounters& w = g_fin_cnt[dev & 15];
+  if (w.cnt) return 0;
+  int* p = nullptr;
+  const size_t bytes = sizeof(int) * FIN_STREAM_SLOTS * FIN_GROUPS;
+  if (hipError_t e = hipMalloc(&p, bytes); e != hipSuccess) return (int)e;
+  if (hipError_t e = hipMemset(p, 0, bytes); e != hipSuccess) return (int)e;
+  if (hipError_t e = hipDeviceSynchronize(); e != hipSuccess) return (int)e;
+  w.cnt = p;
+  return 0;
+}
 
 MI_API int mi_bn_partial_rows(int M, int C) {
   int nblk, rpb; dim3 grid;

@@ -3,6 +3,8 @@
 // fp32 statistics / parameters / gradients.  The GEMMs themselves (QKV, projections, MLP with
 // fused GELU and residual epilogues) are the MFMA kernels of gemm_conv.hip.
 #include "common.h"
+#include <map>
+#include <mutex>
 #include <algorithm>
 #include <cstdlib>
 
@@ -222,7 +224,11 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
   // Grid-stride kernel: launch at most one resident wave of blocks (CUs x occupancy, per LN_V
   // instantiation), so no block waits for a slot while the others already stride past its rows.
   // MI355X_DP_LN_BWD_BLOCKS overrides (rows in flight vs dW/dB atomics per block).
-  static int env_blocks = -2, resident[LN_MAXV + 1] = {0};
+  static int env_blocks = -2;
+  // resident-block count per (device, dynamic LDS bytes): the occupancy depends on the LDS size
+  // (4 * D floats), which differs between D values of one LN_V instantiation (e.g. 640 vs 768)
+  static std::mutex res_mu;
+  static std::map<std::pair<int, size_t>, int> resident;
   if (env_blocks == -2) {
     const char* e = std::getenv("MI355X_DP_LN_BWD_BLOCKS");
     env_blocks = e ? std::max(1, std::atoi(e)) : -1;
@@ -231,16 +237,16 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
   const int nvec = cdiv(D, 256);
   auto cap = [&](const void* fn) {
     if (env_blocks > 0) return env_blocks;
-    if (resident[nvec] == 0) {
-      int dev = 0, cus = 256, per_cu = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu <= 0)
-        per_cu = 2;
-      resident[nvec] = cus * per_cu;
-    }
-    return resident[nvec];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(res_mu);
+    auto it = resident.find({dev, lds});
+    if (it != resident.end()) return it->second;
+    int cus = 256, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 2;
+    resident[{dev, lds}] = cus * per_cu;
+    return cus * per_cu;
   };
   const int rw = nvec <= 4 ? MI_LN_BWD_RW : 1;
 #define MI_LN_BWD(V)                                                                                    \

@@ -153,11 +153,13 @@ def build_all(force=False, verbose=True):
     return [o for o in outs if o]
 
 
-if __name__ == "__main__":
-    what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    force = "--force" in sys.argv
+def main(argv=None):
+    """`mi355x-build [all|kernels|launcher|comm|reducer] [--force] [--debug]`"""
+    argv = sys.argv[1:] if argv is None else argv
+    what = next((a for a in argv if not a.startswith("-")), "all")
+    force = "--force" in argv
     if what == "kernels":
-        build_kernels(force, debug="--debug" in sys.argv)
+        build_kernels(force, debug="--debug" in argv)
     elif what == "launcher":
         build_launcher(force)
     elif what == "comm":
@@ -166,3 +168,8 @@ if __name__ == "__main__":
         build_reducer(force)
     else:
         build_all(force)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -18,7 +18,11 @@ import sys
 from typing import Dict, List, Optional
 
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# import-path compat packages: the source tree's compat/ (editable / in-tree use), else the copy a
+# wheel ships inside the package (mi355x_dp/_compat)
 COMPAT_DIR = os.path.join(REPO_ROOT, "compat")
+if not os.path.isdir(COMPAT_DIR):
+    COMPAT_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_compat")
 NATIVE_LAUNCHER = os.path.join(REPO_ROOT, "mi355x_dp", "_native", "mi355x_launch")
 
 

@@ -98,8 +98,19 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+# BatchNorm entry points whose tall-slab finalize uses the per-stream arrival counters of
+# mi_bn_init_counters(): the table is allocated on the first such call (the GPU is initialised by
+# then, and GraphedStep's eager warm-up makes it happen before any capture).  A process that later
+# uses another device simply takes the counter-free two-launch path there.
+_BN_COUNTER_USERS = frozenset(("mi_bn_fwd_train", "mi_bn_bwd_train", "mi_bn_bwd_train_pre"))
+_bn_counters_pending = [True]
+
+
 def call(name, *args):
     lib = load(True)
+    if _bn_counters_pending[0] and name in _BN_COUNTER_USERS:
+        _bn_counters_pending[0] = False
+        check(lib.mi_bn_init_counters(), "mi_bn_init_counters")
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")

@@ -29,3 +29,23 @@ def test_kernels_compile_without_scratch(src, tmp_path):
             assert vg <= 256, f"{n} uses {vg} VGPRs (> 2 waves/SIMD budget)"
         elif "nt_kernel" in n or "tn_kernel" in n:
             assert vg <= 168, f"{n} uses {vg} VGPRs (> 3 waves/SIMD budget)"
+
+
+def test_package_installs(tmp_path):
+    """`pip install` of the source tree (no network, no build isolation) yields an importable
+    mi355x_dp with its native components and the compat packages shipped inside (SURVEY.md C78:
+    the reference had only a pin list)."""
+    import subprocess
+    import sys
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    target = tmp_path / "site"
+    r = subprocess.run([sys.executable, "-m", "pip", "install", "--no-deps", "--no-build-isolation", "--no-index",
+                        "--target", str(target), ROOT], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert (target / "mi355x_dp" / "_compat" / "smdistributed" / "dataparallel" / "torch" / "torch_smddp.py").exists()
+    assert any(p.name.startswith("mi355x_dp-") and p.name.endswith(".dist-info") for p in target.iterdir())
+    code = ("import mi355x_dp.launch as l, mi355x_dp.build as b, os; "
+            "print(os.path.isdir(l.COMPAT_DIR), callable(b.main), callable(l.main))")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=str(tmp_path),
+                       env={**os.environ, "PYTHONPATH": str(target)})
+    assert r.returncode == 0 and r.stdout.split() == ["True", "True", "True"], r.stdout + r.stderr

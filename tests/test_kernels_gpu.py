@@ -193,6 +193,36 @@ def test_batchnorm_production_shapes(N, H, C):
         torch.cuda.empty_cache()
 
 
+def test_batchnorm_tall_slabs_two_streams():
+    """Two tall-slab BN forwards in flight on different streams at once: each stream has its own
+    finalize arrival counters (one process-global counter array mixed their arrivals)."""
+    from mi355x_dp.ops import batch_norm_act
+    torch.manual_seed(3)
+    C = 64
+    xs = [(torch.randn(64, C, 56, 56, device="cuda") * (1 + i) + i).to(BF).contiguous(memory_format=CL)
+          for i in range(2)]
+    outs, stats = [None, None], []
+    for i in range(2):
+        stats.append((torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"),
+                      torch.zeros((), dtype=torch.long, device="cuda")))
+    g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i in range(2):
+            with torch.cuda.stream(streams[i]):
+                outs[i] = batch_norm_act(xs[i], g, b, stats[i][0], stats[i][1], stats[i][2], True, 0.1, 1e-5,
+                                         relu=False)
+    torch.cuda.synchronize()
+    for i in range(2):
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        for rep in range(3):
+            ref = F.batch_norm(xs[i].float(), rm, rv, g, b, True, 0.1, 1e-5)
+        assert rel_err(outs[i], ref) < 1e-2
+        assert torch.allclose(stats[i][0], rm, rtol=1e-3, atol=1e-3) and torch.allclose(stats[i][1], rv, rtol=1e-3)
+        assert int(stats[i][2]) == 3
+
+
 def test_maxpool_gap():
     from mi355x_dp.ops import global_avg_pool, max_pool2d
     x = torch.randn(4, 64, 56, 56, device="cuda").to(BF).contiguous(memory_format=CL).requires_grad_()

@@ -1,0 +1,3 @@
+bash tools/gpu_steps.sh \
+  all_gpu_tests 900 "python -u -m pytest -q --timeout 200 --timeout-method thread tests/ -m gpu" \
+  bench 300 "python bench.py --steps 20 --warmup 5"
