@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--force-comm", action="store_true",
                    help="create the process group and issue every bucket collective even at N=1 "
                         "(comm-stream / overlap traces on one GPU); the headline N=1 run leaves it off")
+    p.add_argument("--grad-comm", default=os.environ.get("MI355X_DP_GRAD_COMM", "fp32"), choices=("fp32", "bf16"),
+                   help="gradient all-reduce dtype (bf16: half the bytes; fp32 master weights either way)")
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as one captured HIP graph (launch-bound small-batch configs)")
@@ -98,6 +100,7 @@ def main():
         kw["bucket_cap_mb"] = args.bucket_mb
     if args.force_comm:
         kw["force_comm"] = True
+    kw["grad_comm"] = args.grad_comm
     engine = DataParallel(model, **kw)
     opt = FlatSGD(engine, lr=args.lr, momentum=0.9, weight_decay=1e-4)
 
@@ -195,6 +198,7 @@ def main():
                 "backend": args.backend if use_pg else "none",
                 "comm_forced_at_world1": bool(args.force_comm and world == 1),
                 "buckets": len(engine.buckets),
+                "grad_comm": args.grad_comm,
                 "hip_graph": bool(args.graph),
             },
             "loss_first_warmup": round(first_loss, 4),

@@ -367,6 +367,7 @@ class SmddpBackend : public c10d::Backend {
       case at::kDouble: return 1;
       case at::kInt: return 2;
       case at::kLong: return 3;
+      case at::kBFloat16: return 4;
       default: return -1;
     }
   }

@@ -108,10 +108,18 @@ class Reducer {
  public:
   Reducer(at::Tensor flat_grad, std::vector<int64_t> offsets, std::vector<int64_t> numels,
           std::vector<std::vector<int64_t>> buckets, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t align,
-          bool force_comm)
+          bool force_comm, c10::optional<at::Tensor> comm_buf)
       : grad_(std::move(flat_grad)), offsets_(std::move(offsets)), numels_(std::move(numels)),
         buckets_(std::move(buckets)), pg_(std::move(pg)), force_comm_(force_comm) {
     TORCH_CHECK(offsets_.size() == numels_.size(), "offsets / numels mismatch");
+    if (comm_buf.has_value() && comm_buf->defined()) {
+      // reduced-precision gradient exchange: each bucket is cast into this buffer on the producing
+      // stream, all-reduced there (half the bytes over xGMI for bf16), and cast back into the fp32
+      // gradient in finish() -- every rank receives the identical reduced values, so replicas stay
+      // bit-identical; the fp32 master weights and optimizer are unchanged
+      comm_ = *comm_buf;
+      TORCH_CHECK(comm_.numel() >= grad_.numel() && comm_.device() == grad_.device(), "bad comm buffer");
+    }
     const int64_t np = (int64_t)offsets_.size();
     bucket_of_.assign(np, -1);
     for (size_t b = 0; b < buckets_.size(); ++b) {
@@ -138,6 +146,7 @@ class Reducer {
     param_ready_.assign(offsets_.size(), false);
     works_.clear();
     next_ = 0;
+    sent_.assign(buckets_.size(), false);
     trace_.clear();
     t0_ = std::chrono::steady_clock::now();
   }
@@ -164,6 +173,12 @@ class Reducer {
     }
     for (auto& w : works) w->wait();
     std::lock_guard<std::mutex> g(mu_);
+    if (comm_.defined())
+      for (int64_t b = 0; b < (int64_t)ranges_.size(); ++b)
+        if (sent_[b]) {
+          const auto& r = ranges_[b];
+          grad_.narrow(0, r.first, r.second - r.first).copy_(comm_.narrow(0, r.first, r.second - r.first));
+        }
     trace_.emplace_back(-1, 0, since_reset_us());
   }
 
@@ -188,14 +203,22 @@ class Reducer {
   void launch_ready_locked() {
     while (next_ < (int64_t)buckets_.size() && ready_[next_]) {
       const auto& r = ranges_[next_];
-      trace_.emplace_back(next_, (r.second - r.first) * grad_.element_size(), since_reset_us());
+      const at::Tensor& buf = comm_.defined() ? comm_ : grad_;
+      trace_.emplace_back(next_, (r.second - r.first) * buf.element_size(), since_reset_us());
       if (pg_ && (pg_->getSize() > 1 || force_comm_)) {
-        std::vector<at::Tensor> ts{grad_.narrow(0, r.first, r.second - r.first)};
+        at::Tensor slice = grad_.narrow(0, r.first, r.second - r.first);
+        if (comm_.defined()) {
+          at::Tensor c = comm_.narrow(0, r.first, r.second - r.first);
+          c.copy_(slice);  // cast on the caller's (producing) stream, ordered before the collective
+          slice = c;
+          sent_[next_] = true;
+        }
+        std::vector<at::Tensor> ts{slice};
         c10d::AllreduceOptions opts;
         opts.reduceOp = c10d::ReduceOp::SUM;
         works_.push_back(pg_->allreduce(ts, opts));
         ++comm_calls_;
-        comm_bytes_ += (r.second - r.first) * grad_.element_size();
+        comm_bytes_ += (r.second - r.first) * slice.element_size();
       }
       ++next_;
     }
@@ -207,7 +230,8 @@ class Reducer {
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   std::vector<std::pair<int64_t, int64_t>> ranges_;
   std::vector<int64_t> bucket_of_, pending_;
-  std::vector<bool> ready_, param_ready_;
+  std::vector<bool> ready_, param_ready_, sent_;
+  at::Tensor comm_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
   bool force_comm_ = false;
   std::vector<std::tuple<int64_t, int64_t, double>> trace_;
@@ -228,9 +252,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("min_bytes") = 0);
   py::class_<mi_ddp::Reducer>(m, "Reducer")
       .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>, std::vector<std::vector<int64_t>>,
-                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t, bool>(),
+                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t, bool, c10::optional<at::Tensor>>(),
            py::arg("flat_grad"), py::arg("offsets"), py::arg("numels"), py::arg("buckets"), py::arg("process_group"),
-           py::arg("align") = 64, py::arg("force_comm") = false)
+           py::arg("align") = 64, py::arg("force_comm") = false, py::arg("comm_buf") = py::none())
       .def("reset", &mi_ddp::Reducer::reset)
       .def("mark_ready", &mi_ddp::Reducer::mark_ready, py::call_guard<py::gil_scoped_release>())
       .def("finish", &mi_ddp::Reducer::finish, py::call_guard<py::gil_scoped_release>())

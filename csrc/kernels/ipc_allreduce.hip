@@ -262,6 +262,18 @@ __device__ __forceinline__ T ipc_combine(T a, T b) {
   return a < b ? a : b;
 }
 
+// bf16 elements (raw bits): combined in fp32, rounded once per step in rank order -- identical on
+// every rank
+struct Bf16 {
+  uint16_t v;
+};
+template <>
+__device__ __forceinline__ Bf16 ipc_combine<Bf16, IPC_SUM>(Bf16 a, Bf16 b) { return {f2bf(bf2f(a.v) + bf2f(b.v))}; }
+template <>
+__device__ __forceinline__ Bf16 ipc_combine<Bf16, IPC_MAX>(Bf16 a, Bf16 b) { return bf2f(a.v) >= bf2f(b.v) ? a : b; }
+template <>
+__device__ __forceinline__ Bf16 ipc_combine<Bf16, IPC_MIN>(Bf16 a, Bf16 b) { return bf2f(a.v) <= bf2f(b.v) ? a : b; }
+
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void ipc_oneshot_kernel(IpcRaw p, int rank, int world, T* __restrict__ out,
                                                           int64_t n, int root, uint32_t epoch, int* err,
@@ -269,8 +281,13 @@ __global__ __launch_bounds__(256) void ipc_oneshot_kernel(IpcRaw p, int rank, in
   if (!ipc_handshake(p, rank, world, epoch, err, spin_limit)) return;
   if (OP == IPC_COPY && rank == root) return;  // the root's tensor is the source
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (OP == IPC_COPY) {
+    if constexpr (OP == IPC_COPY) {
       out[i] = __builtin_nontemporal_load((const T*)p.data[root] + i);
+    } else if constexpr (sizeof(T) == 2) {  // Bf16: plain loads (no 2-byte non-temporal struct load)
+      T v = ((const T*)p.data[0])[i];
+#pragma unroll 1
+      for (int q = 1; q < world; ++q) v = ipc_combine<T, OP>(v, ((const T*)p.data[q])[i]);
+      out[i] = v;
     } else {
       T v = __builtin_nontemporal_load((const T*)p.data[0] + i);
 #pragma unroll 1
@@ -302,7 +319,7 @@ int dispatch_oneshot(int op, const IpcRaw& p, int rank, int world, void* out, in
 
 }  // namespace
 
-// dtype: 0 f32, 1 f64, 2 i32, 3 i64 (ignored for COPY); op: 0 SUM, 1 MAX, 2 MIN, 3 COPY (root's slot);
+// dtype: 0 f32, 1 f64, 2 i32, 3 i64, 4 bf16 (ignored for COPY); op: 0 SUM, 1 MAX, 2 MIN, 3 COPY (root's slot);
 // nbytes: bytes of this call's slot payload (0 = barrier).  Same slot / flag protocol and epochs as
 // mi_ipc_allreduce_f32.
 MI_API int mi_ipc_oneshot(const void* const* data, uint32_t* const* flags, int rank, int world, void* out,
@@ -332,6 +349,7 @@ MI_API int mi_ipc_oneshot(const void* const* data, uint32_t* const* flags, int r
     case 1: return dispatch_oneshot<double>(op, p, rank, world, out, nbytes / 8, root, epoch, err, spin_limit, st);
     case 2: return dispatch_oneshot<int32_t>(op, p, rank, world, out, nbytes / 4, root, epoch, err, spin_limit, st);
     case 3: return dispatch_oneshot<int64_t>(op, p, rank, world, out, nbytes / 8, root, epoch, err, spin_limit, st);
+    case 4: return dispatch_oneshot<Bf16>(op, p, rank, world, out, nbytes / 2, root, epoch, err, spin_limit, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -46,6 +46,9 @@ FORCE_COMM = os.environ.get("MI355X_DP_FORCE_COMM", "0") == "1"
 # debug: stage each bucket through a copy taken where its collective starts, and check at the end
 # of backward that no gradient was written after its bucket was launched (parallel/health.py)
 CHECK_STREAM_ORDER = os.environ.get("MI355X_DP_CHECK_STREAM_ORDER", "0") == "1"
+# dtype of the gradient exchange: "fp32" (default) or "bf16" (half the bytes on the wire; the sums
+# are rounded to bf16 once, identically on every rank, then cast back into the fp32 gradient)
+GRAD_COMM = os.environ.get("MI355X_DP_GRAD_COMM", "fp32")
 
 
 def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int, last_cap_bytes: int = None,
@@ -111,7 +114,7 @@ class DataParallel(nn.Module):
                  first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB, broadcast_buffers: bool = True,
                  bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
-                 check_stream_order: bool = CHECK_STREAM_ORDER):
+                 check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -166,13 +169,19 @@ class DataParallel(nn.Module):
 
         self.reducer = None
         self._staging = {}
+        if grad_comm not in ("fp32", "bf16"):
+            raise ValueError(f"grad_comm must be 'fp32' or 'bf16', not {grad_comm!r}")
+        self.grad_comm = grad_comm
+        self._comm_buf = (torch.empty(self.flat.grad.numel(), dtype=torch.bfloat16, device=self.flat.grad.device)
+                          if grad_comm == "bf16" and self.comm_on and not self.check_stream_order else None)
+        self._sent = set()
         if native is not None and not self.check_stream_order:
             pg = None
             if self.comm_on:
                 pg = process_group if process_group is not None else dist.distributed_c10d._get_default_group()
             self.reducer = native.Reducer(self.flat.grad, [int(o) for o in self.flat.offsets],
                                           [p.numel() for p in self.flat.params], self.buckets, pg, 64,
-                                          bool(force_comm))
+                                          bool(force_comm), self._comm_buf)
         for i, p in enumerate(self.flat.params):
             cb = functools.partial(self.reducer.mark_ready, i) if self.reducer is not None \
                 else self._make_ready_cb(i)
@@ -225,6 +234,7 @@ class DataParallel(nn.Module):
             self._ready[b] = False
         self._param_ready = [False] * len(self.flat.params)
         self._works = []
+        self._sent = set()
         self._next = 0
 
     def _mark_ready(self, i):
@@ -249,7 +259,12 @@ class DataParallel(nn.Module):
             return
         if not self.comm_on:
             return
-        w = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+        buf = self.flat.grad[lo:hi]
+        if self._comm_buf is not None:
+            self._comm_buf[lo:hi].copy_(buf)
+            buf = self._comm_buf[lo:hi]
+            self._sent.add(b)
+        w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
         self._works.append(w)
         self._py_comm_calls += 1
 
@@ -341,6 +356,10 @@ class DataParallel(nn.Module):
             for w in self._works:
                 w.wait()
             self._works = []
+            for b in sorted(self._sent):
+                lo, hi = self.bucket_ranges[b]
+                self.flat.grad[lo:hi].copy_(self._comm_buf[lo:hi])
+            self._sent = set()
         if average and self.world_size > 1:
             self.flat.grad.mul_(1.0 / self.world_size)
 

@@ -206,6 +206,8 @@ def test_smddp_ipc_only_two_ranks(tmp_path):
         "i = torch.full((300_001,), r + 1, device='cuda', dtype=torch.int64); dist.all_reduce(i)\n"
         "assert int(i.min()) == 3 and int(i.max()) == 3\n"
         "f = torch.full((5,), float(r), device='cuda'); dist.all_reduce(f, op=dist.ReduceOp.MIN)\n"
+        "h = torch.full((700_001,), 1.5 + r, device='cuda', dtype=torch.bfloat16); dist.all_reduce(h)\n"
+        "assert float(h.float().min()) == 4.0 and float(h.float().max()) == 4.0\n"
         "assert float(f.max()) == 0.0\n"
         "b = torch.arange(2_000_003, device='cuda', dtype=torch.float32) * (r + 7); dist.broadcast(b, 1)\n"
         "assert torch.equal(b, torch.arange(2_000_003, device='cuda', dtype=torch.float32) * 8)\n"
@@ -219,7 +221,7 @@ def test_smddp_ipc_only_two_ranks(tmp_path):
         "from mi355x_dp.parallel import DataParallel, FlatSGD\n"
         "from mi355x_dp.parallel.health import ReplicaChecker\n"
         "torch.manual_seed(r)\n"
-        "eng = DataParallel(resnet18(num_classes=10).cuda(), bucket_cap_mb=8, min_bucket_mb=0)\n"
+        "eng = DataParallel(resnet18(num_classes=10).cuda(), bucket_cap_mb=8, min_bucket_mb=0, grad_comm='bf16')\n"
         "opt = FlatSGD(eng, lr=0.05, momentum=0.9)\n"
         "g = torch.Generator(device='cuda').manual_seed(r)\n"
         "for _ in range(3):\n"

@@ -356,3 +356,51 @@ def test_buffer_broadcast_async():
         assert n == 3
     for a, b in zip(res[0][0], res[1][0]):
         assert (a == b).all()
+
+
+def _worker_bf16_comm(rank, world, port, q, py, comm):
+    try:
+        if py:
+            os.environ["MI355X_DP_PY_REDUCER"] = "1"
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0, grad_comm=comm)
+        opt = FlatSGD(m, lr=0.1, momentum=0.9)
+        x, y = _data()
+        shard = slice(rank * 8, (rank + 1) * 8)
+        for _ in range(3):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x[shard]), y[shard]).backward()
+            opt.step()
+        q.put((rank, m.flat.data.clone().numpy(), m.native_reducer, m.reducer.comm_bytes if m.reducer else -1))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, None))
+        raise
+
+
+def test_bf16_gradient_allreduce():
+    """grad_comm='bf16': buckets are exchanged as bf16 (half the bytes), summed identically on every
+    rank (replicas bit-identical) and cast back into the fp32 gradient; the trajectory stays within
+    bf16 rounding of the fp32 exchange.  Native and Python reducers agree."""
+    out = {}
+    for py, comm in ((False, "fp32"), (False, "bf16"), (True, "bf16")):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _port()
+        ps = [ctx.Process(target=_worker_bf16_comm, args=(r, 2, port, q, py, comm)) for r in range(2)]
+        for p in ps:
+            p.start()
+        res = {r: (d, nat, nb) for r, d, nat, nb in [q.get(timeout=120) for _ in ps]}
+        for p in ps:
+            p.join(60)
+        for r, (d, nat, nb) in res.items():
+            assert not isinstance(d, Exception), repr(d)
+        assert (res[0][0] == res[1][0]).all(), (py, comm)
+        out[(py, comm)] = res[0]
+    f32, b16, b16py = out[(False, "fp32")], out[(False, "bf16")], out[(True, "bf16")]
+    assert b16[1] is True and b16py[1] is False
+    assert b16[2] * 2 == f32[2] > 0  # half the bytes on the wire
+    assert (b16[0] == b16py[0]).all()
+    assert abs(b16[0] - f32[0]).max() < 2e-3
+    assert (b16[0] != f32[0]).any()  # the exchange really was rounded
