@@ -844,12 +844,17 @@ inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3&
 
 // Tall slabs (e.g. one row per conv M-tile) are first reduced by a (C/64) x S grid into S rows
 // written just past the slab (callers allocate SLAB_EXTRA_ROWS spare rows), then finalized.
-constexpr int SLAB_EXTRA_ROWS = 64;
+// split rows: the split stage is latency-bound (a 6272-row x 256-channel slab is 12.8 MB read by
+// S x C/64 blocks), so tall slabs are cut into more, shorter splits (MI_SLAB_SPLIT_ROWS rows each)
+#ifndef MI_SLAB_SPLIT_ROWS
+#define MI_SLAB_SPLIT_ROWS 32
+#endif
+constexpr int SLAB_EXTRA_ROWS = 256;
 
 inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const float*& fin) {
   fin = part;
   if (nblk <= 256) return nblk;
-  const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, 128));
+  const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, MI_SLAB_SPLIT_ROWS));
   const int rows_per = cdiv(nblk, S);
   float* out = part + (size_t)nblk * 2 * C;
   hipLaunchKernelGGL(slab_split_kernel, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, C, rows_per, out);
@@ -896,7 +901,7 @@ inline void slab_finalize(float* part, int nblk, const FinArgs& f, hipStream_t s
   const int C = f.C;
   int* cnt = nblk > 256 ? fin_counters(cdiv(C, 64), st) : nullptr;
   if (cnt) {
-    const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, 128));
+    const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, MI_SLAB_SPLIT_ROWS));
     const int rows_per = cdiv(nblk, S);
     float* out = part + (size_t)nblk * 2 * C;
     hipLaunchKernelGGL(slab_split_fin_kernel<BWD>, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, rows_per,

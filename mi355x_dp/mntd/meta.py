@@ -5,7 +5,8 @@ MI355X-first changes to the hot loop (which in the reference is dominated by
 ``torch.load`` of a ~1.1 MB checkpoint per model per step): a
 ``CheckpointBank`` loads every shadow/target state_dict ONCE (``weights_only=True``) and
 keeps them resident on the device; each step swaps parameters with
-``torch.func.functional_call`` (no copies, no file I/O).  Semantics -- per-model
+``torch.func.functional_call`` (no copies, no file I/O); evaluation runs all models of a split in ONE ``torch.func.vmap``
+forward over the bank's stacked parameters (``_eval_scores_batched``).  Semantics -- per-model
 forward of the learnable queries, BCE / one-class loss, per-model optimizer step,
 AUC via sklearn, 'half' = median threshold -- are unchanged.  ``np.asscalar`` (gone
 in numpy 2) is replaced by ``float``.
@@ -19,7 +20,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
-from torch.func import functional_call
+from torch.func import functional_call, stack_module_state, vmap
 
 from .models import TASK_MODELS
 
@@ -108,6 +109,16 @@ class CheckpointBank:
     def __len__(self):
         return len(self.params)
 
+    def stacked(self, paths: Sequence[str]) -> Dict[str, torch.Tensor]:
+        """{name: [len(paths), *shape]} of the models in ``paths`` (cached per path tuple): the
+        whole evaluation set as one batch of parameter tensors for a vmapped forward."""
+        key = tuple(paths)
+        cache = self.__dict__.setdefault("_stacked", {})
+        if key not in cache:
+            names = list(self.params[paths[0]].keys())
+            cache[key] = {n: torch.stack([self.params[p][n] for p in paths]) for n in names}
+        return cache[key]
+
 
 class _EmbForward(nn.Module):
     """Routes forward() to the wrapped model's emb_forward() so functional_call can drive it."""
@@ -158,8 +169,37 @@ def epoch_meta_train(meta_model, basic_model, optimizer, dataset, is_discrete, t
     return cum_loss / len(dataset), auc, acc
 
 
+# MI355X_DP_MNTD_BATCHED=0 falls back to the reference's one-model-at-a-time evaluation
+BATCHED_EVAL = os.environ.get("MI355X_DP_MNTD_BATCHED", "1") != "0"
+
+
+@torch.no_grad()
+def _eval_scores_batched(meta_model, basic_model, dataset, is_discrete, bank):
+    """Every model of ``dataset`` in ONE vmapped forward over the bank's stacked parameters, then
+    the meta-classifier over all of them at once -- no per-model launches or host syncs (the
+    reference: one torch.load + forward + .item() per model, utils_meta.py:74-104).  Shadow models
+    stay in train mode like the reference; dropout (CIFAR CNN) draws per model."""
+    paths = [x for x, _ in dataset]
+    labs = np.array([y for _, y in dataset])
+    stacked = bank.stacked(paths)
+    fn = "emb_forward" if is_discrete else "forward"
+    outs = vmap(lambda p: _call_method(basic_model, p, fn, meta_model.inp), randomness="different")(stacked)
+    if isinstance(meta_model, MetaClassifier):
+        emb = F.relu(meta_model.fc(outs.reshape(len(paths), meta_model.N_in * meta_model.class_num)))
+        scores = meta_model.output(emb).reshape(-1)
+        target = torch.as_tensor(labs, dtype=scores.dtype, device=scores.device)
+        losses = F.binary_cross_entropy_with_logits(scores, target, reduction="none").tolist()
+    else:
+        emb = F.relu(meta_model.fc(outs.reshape(len(paths), meta_model.N_in * meta_model.class_num)))
+        scores = emb @ meta_model.w
+        losses = []
+    return scores.detach().cpu().numpy().astype(np.float64), labs, losses
+
+
 @torch.no_grad()
 def _eval_scores(meta_model, basic_model, dataset, is_discrete, bank):
+    if bank is not None and BATCHED_EVAL and len(dataset) > 0:
+        return _eval_scores_batched(meta_model, basic_model, dataset, is_discrete, bank)
     preds, labs, losses = [], [], []
     for x, y in dataset:
         if bank is not None:

@@ -126,3 +126,26 @@ def test_shadow_generation_serial_equals_task_parallel(tmp_path):
         for k in a:
             assert torch.allclose(a[k], b[k], atol=1e-6), (i, k)
     assert os.path.exists(os.path.join(root, "par", "mnist", "jumbo.log"))
+
+
+@pytest.mark.skipif(not os.path.isdir(CKPT), reason="reference checkpoints not mounted")
+def test_batched_meta_eval_matches_sequential():
+    """The vmapped evaluation over the stacked checkpoint bank gives the per-model scores and losses
+    of the reference's one-model-at-a-time loop (shipped MNIST checkpoints, both meta models)."""
+    import mi355x_dp.mntd.meta as M
+    from mi355x_dp.mntd import MNISTCNN
+    d = os.path.join(CKPT, "mnist", "models")
+    ds = [(os.path.join(d, f"shadow_jumbo_{i}.model"), 1) for i in range(6)] + \
+         [(os.path.join(d, f"shadow_benign_{i}.model"), 0) for i in range(6)]
+    bank = M.CheckpointBank([ds])
+    torch.manual_seed(0)
+    for meta in (M.MetaClassifier((1, 28, 28), 10), M.MetaClassifierOC((1, 28, 28), 10)):
+        basic = MNISTCNN()
+        p1, l1, loss1 = M._eval_scores_batched(meta, basic, ds, False, bank)
+        M.BATCHED_EVAL = False
+        try:
+            p2, l2, loss2 = M._eval_scores(meta, basic, ds, False, bank)
+        finally:
+            M.BATCHED_EVAL = True
+        assert np.allclose(p1, p2, rtol=1e-4, atol=1e-5), (p1, p2)
+        assert (l1 == l2).all() and np.allclose(loss1, loss2, rtol=1e-4, atol=1e-6)
