@@ -44,6 +44,8 @@ def parse():
                         "(comm-stream / overlap traces on one GPU); the headline N=1 run leaves it off")
     p.add_argument("--grad-comm", default=os.environ.get("MI355X_DP_GRAD_COMM", "fp32"), choices=("fp32", "bf16"),
                    help="gradient all-reduce dtype (bf16: half the bytes; fp32 master weights either way)")
+    p.add_argument("--wgrad-stream", type=int, default=int(os.environ.get("MI355X_DP_WGRAD_STREAM", "1")),
+                   choices=(0, 1), help="conv weight gradients on a side HIP stream (overlap with data gradients)")
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as one captured HIP graph (launch-bound small-batch configs)")
@@ -101,6 +103,7 @@ def main():
     if args.force_comm:
         kw["force_comm"] = True
     kw["grad_comm"] = args.grad_comm
+    kw["wgrad_stream"] = bool(args.wgrad_stream)
     engine = DataParallel(model, **kw)
     opt = FlatSGD(engine, lr=args.lr, momentum=0.9, weight_decay=1e-4)
 
@@ -199,6 +202,7 @@ def main():
                 "comm_forced_at_world1": bool(args.force_comm and world == 1),
                 "buckets": len(engine.buckets),
                 "grad_comm": args.grad_comm,
+                "wgrad_stream": bool(args.wgrad_stream),
                 "hip_graph": bool(args.graph),
             },
             "loss_first_warmup": round(first_loss, 4),

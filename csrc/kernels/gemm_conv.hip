@@ -26,6 +26,7 @@
 #include <array>
 #include <cstdio>
 #include <vector>
+#include <mutex>
 #include <cstdlib>
 
 #ifndef MI_CONV_NTSTORE
@@ -1024,16 +1025,22 @@ hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
   }
 }
 
-// Split-K slab workspace of the TN kernels (fp32, per device, grown on demand and reused in stream
-// order).  Contract: the first call that needs a given size allocates (hipMalloc) -- it must not
-// run inside a HIP graph capture; GraphedStep's eager warm-up step makes every allocation first.
+// Split-K slab workspace of the TN kernels (fp32, grown on demand and reused in stream order).  One
+// per device for every stream, plus one for the device's registered weight-gradient side stream
+// (mi_register_wgrad_stream): side-stream weight gradients run concurrently with compute-stream
+// TN work and must not share slabs with it.  Contract: the first call that needs a given size
+// allocates (hipMalloc) -- it must not run inside a HIP graph capture; GraphedStep's eager warm-up
+// step makes every allocation first (capture streams use the shared slot, like the warm-up).
 // MI355X_DP_TN_SLABS=0 selects the fp32-atomic split-K path instead.
 struct SplitkWs { float* p = nullptr; size_t n = 0; };
-static SplitkWs g_splitk_ws[16];
-static float* splitk_workspace(size_t floats) {
+static SplitkWs g_splitk_ws[16][2];
+static hipStream_t g_wgrad_stream[16];
+static std::mutex g_splitk_mu;
+static float* splitk_workspace(size_t floats, hipStream_t st) {
   int dev = 0;
   hipGetDevice(&dev);
-  SplitkWs& w = g_splitk_ws[dev & 15];
+  std::lock_guard<std::mutex> lk(g_splitk_mu);
+  SplitkWs& w = g_splitk_ws[dev & 15][st != nullptr && st == g_wgrad_stream[dev & 15] ? 1 : 0];
   if (w.n < floats) {
     const size_t n = std::max(floats, (size_t)16 << 20);  // >= 64 MB: every RN50 / RN152 wgrad fits
     float* p = nullptr;
@@ -1069,7 +1076,7 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
   a.ws = nullptr;
   if (splits > 1 && a.colsum == nullptr && tn_slabs_on())
-    a.ws = splitk_workspace((size_t)tiles * splits * BM * BN);
+    a.ws = splitk_workspace((size_t)tiles * splits * BM * BN, st);
   if (glds_on())
     hipLaunchKernelGGL((tn_kernel<BM, BN, 1>), dim3(tiles, splits), dim3(256), 0, st, a);
   else
@@ -1113,6 +1120,15 @@ hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
 // Conv forward: x NHWC [Nb,H,W,C] bf16, w [K][R][S][C] bf16, y NHWC [Nb,P,Q,K].
 // Select direct-to-LDS (buffer_load ... lds) staging (1) or register staging (0) for all GEMM kernels.
 // Weight-gradient split-K reduction: 1 = slab workspace + reduce kernel (default), 0 = fp32 atomics.
+// The current device's weight-gradient side stream (its own split-K slab workspace).
+MI_API int mi_register_wgrad_stream(hipStream_t st) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_splitk_mu);
+  g_wgrad_stream[dev & 15] = st;
+  return 0;
+}
+
 MI_API int mi_set_tn_slabs(int on) {
   g_tn_slabs = on ? 1 : 0;
   return 0;

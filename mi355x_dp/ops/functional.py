@@ -17,6 +17,8 @@ through autograd as usual (works with stock ``torch.nn.parallel.DDP``).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
@@ -83,14 +85,111 @@ def _grad_buffer(p: torch.Tensor) -> torch.Tensor:
     return torch.zeros_like(p, dtype=torch.float32)
 
 
+class WgradStream:
+    """Weight gradients on a side HIP stream (owned by the flat-buffer engine, one per device).
+
+    A conv's weight gradient is needed by nothing but the optimizer, while its data gradient is
+    the critical path of backward; on one stream every kernel's tail (its last, partly filled
+    wave of workgroups) and every small split-K reduce / BN finalize idles most of the 256 CUs.
+    With the weight gradients on their own stream the two chains overlap and fill each other's
+    tails.  Ordering rules (no host synchronisation anywhere):
+
+    * ``run``: the side stream waits for the compute stream (the kernel's operands were produced
+      there), the weight-gradient kernels run on it, their operands are ``record_stream``-ed so
+      the caching allocator does not recycle them early, and the parameter is marked ready ON
+      the side stream -- so a bucket's collective (which waits on the current stream) waits for
+      the side stream, which itself has waited for everything the compute stream did before;
+    * marks of gradients produced on the compute stream (BN affine) while side work is pending
+      are deferred and issued on the side stream at its next ``run`` (or ``join``), for the same
+      reason: a bucket may mix both kinds;
+    * ``join`` (engine: before the optimizer / reducer finish, at forward, at zero_grad) makes
+      the compute stream wait for the side stream.
+    Disabled inside HIP graph capture (the captured step stays single-stream)."""
+
+    _streams = {}  # device index -> the side stream (shared by every engine on that device)
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        if idx not in WgradStream._streams:
+            st = torch.cuda.Stream(device=self.device)
+            with torch.cuda.device(idx):  # its own split-K slab workspace (gemm_conv.hip)
+                _lib.call("mi_register_wgrad_stream", ctypes.c_void_p(st.cuda_stream))
+            WgradStream._streams[idx] = st
+        self.stream = WgradStream._streams[idx]
+        self.dirty = False
+        self.deferred = []
+        self.runs = 0
+
+    def active(self) -> bool:
+        return not torch.cuda.is_current_stream_capturing()
+
+    def run(self, fn, tensors=(), cb=None):
+        main = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(main)
+        with torch.cuda.stream(self.stream):
+            out = fn()
+            for t in tensors:
+                if t is not None:
+                    t.record_stream(self.stream)
+            self.dirty = True
+            self.runs += 1
+            self._flush_locked()
+            if cb is not None:
+                cb()
+        return out
+
+    def _flush_locked(self):
+        pending, self.deferred = self.deferred, []
+        for d in pending:
+            d()
+
+    def mark(self, cb):
+        if self.dirty:
+            self.deferred.append(cb)
+        else:
+            cb()
+
+    def join(self):
+        if self.deferred:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                self._flush_locked()
+        if self.dirty:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            self.dirty = False
+
+
+def _side(p):
+    """the engine's weight-gradient stream for parameter p, if it should be used now"""
+    s = getattr(p, "_mi_side", None)
+    if s is None or not _flat(p) or not s.active():
+        return None
+    return s
+
+
 def _finish_grad(p: torch.Tensor, g: torch.Tensor):
     """Return value for autograd: None if accumulated in place (flat engine)."""
     if _flat(p):
         cb = getattr(p, "_mi_on_grad_ready", None)
         if cb is not None:
-            cb()
+            s = getattr(p, "_mi_side", None)
+            if s is not None:
+                s.mark(cb)
+            else:
+                cb()
         return None
     return g.to(p.dtype) if g.dtype != p.dtype else g
+
+
+def run_wgrad(p: torch.Tensor, fn, tensors=()):
+    """Run ``fn`` (which writes p's fp32 gradient into the flat buffer) on the engine's weight-
+    gradient stream when there is one, else inline; then signal the engine (see WgradStream)."""
+    s = _side(p)
+    if s is None:
+        fn()
+        return
+    s.run(fn, tensors, getattr(p, "_mi_on_grad_ready", None))
 
 
 def _conv_out(h, r, stride, pad):
@@ -176,7 +275,12 @@ class _Conv2d(torch.autograd.Function):
             _lib.call("mi_conv2d_dgrad", ptr(dy), ptr(wt), ptr(dx), N, H, W, C, K, R, S, stride, padding, P, Q, st)
         if ctx.needs_input_grad[1]:
             g = _grad_buffer(weight)
-            if ctx.mode == "direct":
+            on_side = ctx.mode == "direct" and _side(weight) is not None
+            if on_side:
+                # flat engine with a weight-gradient stream: kernels + ready signal on the side stream
+                run_wgrad(weight, lambda: _lib.call("mi_conv2d_wgrad", ptr(xs), ptr(dy), ptr(g), N, H, W, C, K, R,
+                                                    S, stride, padding, P, Q, stream_of(dy)), (xs, dy))
+            elif ctx.mode == "direct":
                 _lib.call("mi_conv2d_wgrad", ptr(xs), ptr(dy), ptr(g), N, H, W, C, K, R, S, stride, padding, P, Q, st)
             elif ctx.mode == "c8":
                 gp = torch.zeros((K, R, S, 8), dtype=torch.float32, device=dy.device)
@@ -189,7 +293,8 @@ class _Conv2d(torch.autograd.Function):
                 gp = torch.zeros((K, Kp), dtype=torch.float32, device=dy.device)
                 _lib.call("mi_gemm_tn", ptr(dy), ptr(xs), ptr(gp), K, Kp, N * P * Q, K, Kp, Kp, st)
                 g.add_(gp[:, :Kr].reshape(K, R, S, C).permute(0, 3, 1, 2))
-            dw = _finish_grad(weight, g)
+            if not on_side:
+                dw = _finish_grad(weight, g)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             bias = ctx.bias_param
             gb = _grad_buffer(bias)

@@ -34,7 +34,7 @@ import torch
 from . import _lib
 from . import kernels as _k  # noqa: F401
 from ._lib import ptr, stream_of
-from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, weight_bf16, weight_bf16_t
+from .functional import BF16, CL, _finish_grad, _grad_buffer, _nhwc, _side, run_wgrad, weight_bf16, weight_bf16_t
 
 F32 = torch.float32
 EPI_ACCUM, EPI_BN_BWD, EPI_ACCUM_BN_BWD = 3, 4, 5
@@ -121,12 +121,20 @@ def _bn_fwd_dual(c, slab, rows, bn, cd, slabd, rowsd, bnd):
 
 # ---------------------------------------------------------------------- backward pieces
 def _wgrad(x, dy, spec):
+    """weight gradient into the flat buffer -- on the engine's weight-gradient stream when it has
+    one (overlapping this block's data-gradient chain, see functional.WgradStream)"""
     N, C, H, W = x.shape
     K, _, R, S = spec.w.shape
     P, Q = dy.shape[2], dy.shape[3]
     g = _grad_buffer(spec.w)
-    _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dy), ptr(g), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
-              stream_of(dy))
+
+    def launch():
+        _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dy), ptr(g), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
+                  stream_of(dy))
+    if _side(spec.w) is not None:
+        run_wgrad(spec.w, launch, (x, dy))
+        return None
+    launch()
     return _finish_grad(spec.w, g)
 
 

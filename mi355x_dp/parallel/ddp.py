@@ -49,6 +49,9 @@ CHECK_STREAM_ORDER = os.environ.get("MI355X_DP_CHECK_STREAM_ORDER", "0") == "1"
 # dtype of the gradient exchange: "fp32" (default) or "bf16" (half the bytes on the wire; the sums
 # are rounded to bf16 once, identically on every rank, then cast back into the fp32 gradient)
 GRAD_COMM = os.environ.get("MI355X_DP_GRAD_COMM", "fp32")
+# run conv weight gradients on a side HIP stream, overlapping the data-gradient chain
+# (mi355x_dp.ops.functional.WgradStream); CUDA engines only
+WGRAD_STREAM = os.environ.get("MI355X_DP_WGRAD_STREAM", "1") == "1"
 
 
 def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int, last_cap_bytes: int = None,
@@ -114,7 +117,8 @@ class DataParallel(nn.Module):
                  first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB, broadcast_buffers: bool = True,
                  bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
-                 check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM):
+                 check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM,
+                 wgrad_stream: bool = WGRAD_STREAM):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -182,11 +186,17 @@ class DataParallel(nn.Module):
             self.reducer = native.Reducer(self.flat.grad, [int(o) for o in self.flat.offsets],
                                           [p.numel() for p in self.flat.params], self.buckets, pg, 64,
                                           bool(force_comm), self._comm_buf)
+        self.wgrad_stream = None
+        if wgrad_stream and self.flat.grad.is_cuda:
+            from mi355x_dp.ops.functional import WgradStream
+            self.wgrad_stream = WgradStream(self.flat.grad.device)
         for i, p in enumerate(self.flat.params):
             cb = functools.partial(self.reducer.mark_ready, i) if self.reducer is not None \
                 else self._make_ready_cb(i)
             p._mi_on_grad_ready = cb
-            p.register_post_accumulate_grad_hook(self._make_hook(i, cb))
+            p._mi_side = self.wgrad_stream
+            hook_cb = functools.partial(self.wgrad_stream.mark, cb) if self.wgrad_stream is not None else cb
+            p.register_post_accumulate_grad_hook(self._make_hook(i, hook_cb))
 
         if self.distributed and self.world_size > 1:
             # one broadcast of the whole flat parameter buffer (+ buffers) from rank 0
@@ -320,7 +330,12 @@ class DataParallel(nn.Module):
                 f"bucket(s) affected)")
 
     # ------------------------------------------------------------ public
+    def _join_side(self):
+        if self.wgrad_stream is not None:
+            self.wgrad_stream.join()
+
     def forward(self, *args, **kwargs):
+        self._join_side()  # a backward whose sync was skipped (no_sync / accumulation) left side work
         self._reset()
         self._wait_buffer_sync()
         out = self.module(*args, **kwargs)
@@ -341,6 +356,7 @@ class DataParallel(nn.Module):
 
     def finish_gradient_sync(self, average: bool = False):
         """Launch any bucket not yet launched (unused params), then wait for all."""
+        self._join_side()
         self._wait_buffer_sync()
         if self.reducer is not None:
             self.reducer.finish()
@@ -368,6 +384,7 @@ class DataParallel(nn.Module):
         return 1.0 / self.world_size
 
     def zero_grad(self, set_to_none: bool = False):
+        self._join_side()
         self.flat.reattach_grads()
         self.flat.zero_grad()
 

@@ -43,6 +43,65 @@ def test_stream_order_checker_native_step():
     assert torch.allclose(grads[False], grads[True], rtol=1e-4, atol=1e-6)
 
 
+def test_wgrad_stream_bitwise_and_ordered():
+    """Weight gradients on the side stream (DataParallel(wgrad_stream=True)): ResNet-50's fused
+    bottleneck blocks give bit-identical gradients to the single-stream engine (same kernels, same
+    reduction order), and the stream-order checker -- whose bucket snapshot waits on whatever
+    stream the ready-mark ran on -- finds no bucket written after its launch."""
+    sys.path.insert(0, ROOT)
+    from mi355x_dp.models import resnet50
+    from mi355x_dp.ops import cross_entropy
+    from mi355x_dp.parallel import DataParallel
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(8, 3, 64, 64, device=dev, generator=g)
+    y = torch.randint(0, 1000, (8,), device=dev, generator=g)
+    grads = {}
+    for side, check in ((False, False), (False, False), (True, False), (True, True)):
+        torch.manual_seed(0)
+        m = resnet50().to(dev)
+        names = {id(p): n for n, p in m.named_parameters()}
+        e = DataParallel(m, bucket_cap_mb=8, first_bucket_mb=1, min_bucket_mb=0,
+                         check_stream_order=check, wgrad_stream=side)
+        for _ in range(2):
+            e.zero_grad()
+            cross_entropy(e(x), y).backward()
+            e.finish_gradient_sync()
+        torch.cuda.synchronize()
+        assert e.order_violations == []
+        if side:
+            assert e.wgrad_stream is not None and e.wgrad_stream.runs >= 2 * 52
+            assert not e.wgrad_stream.dirty and not e.wgrad_stream.deferred
+        if (side, check) in grads:
+            grads["repeat"] = e.flat.grad.clone()
+        else:
+            grads[(side, check)] = e.flat.grad.clone()
+    spans = [(names[id(p)], int(o), int(o) + p.numel()) for p, o in zip(e.flat.params, e.flat.offsets)]
+
+    def differing(a, b):
+        return [n for n, lo, hi in spans if not torch.equal(a[lo:hi], b[lo:hi])]
+    # the stem's weight-gradient kernel and the fc layer's split-K (with bias column sums) add with
+    # fp32 atomics: non-deterministic even on a single stream; every other conv / BN gradient is
+    # bit-reproducible, and must stay so with the side stream
+    atomic = lambda n: n == "conv1.weight" or n.startswith("fc.")  # noqa: E731
+    base = differing(grads[(False, False)], grads["repeat"])
+    assert all(atomic(n) for n in base), base
+    side_diff = differing(grads[(False, False)], grads[(True, False)])
+    assert all(atomic(n) for n in side_diff), side_diff
+    def rel(a, b, names):
+        out = {}
+        for n, lo, hi in spans:
+            if n in names:
+                out[n] = float((a[lo:hi] - b[lo:hi]).norm() / b[lo:hi].norm().clamp_min(1e-30))
+        return out
+    # the atomically summed gradients differ by summation order only: relative L2 at fp32 rounding
+    for other in (grads["repeat"], grads[(True, False)], grads[(True, True)]):
+        d = rel(other, grads[(False, False)], [n for n, _, _ in spans if atomic(n)])
+        assert max(d.values()) < 1e-5, d
+    assert differing(grads[(False, False)], grads[(True, True)]) == side_diff or \
+        all(atomic(n) for n in differing(grads[(False, False)], grads[(True, True)]))
+
+
 def _bench(args, env=None):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
                        timeout=300, cwd=ROOT, env={**os.environ, **(env or {})})
@@ -51,14 +110,18 @@ def _bench(args, env=None):
     return json.loads(line)
 
 
-@pytest.mark.parametrize("backend", ["smddp", "nccl"])
-def test_force_comm_world1_bench(backend):
+@pytest.mark.parametrize("backend,wgrad_stream", [("smddp", 0), ("nccl", 0), ("nccl", 1)])
+def test_force_comm_world1_bench(backend, wgrad_stream):
     """bench.py --force-comm: a real process group at N=1 (native smddp or ProcessGroupNCCL) and
-    one collective per bucket, launched in bucket order while backward runs."""
-    out = _bench(["--model", "resnet18", "--batch", "32", "--image-size", "64", "--steps", "3", "--warmup", "1",
-                  "--force-comm", "--backend", backend], {"MASTER_PORT": str(29600 + (backend == "nccl"))})
+    one collective per bucket, launched in bucket order while backward runs (also with the weight
+    gradients on the side stream, whose ready-marks then trigger the launches)."""
+    out = _bench(["--model", "resnet18" if not wgrad_stream else "resnet50", "--batch", "32", "--image-size", "64",
+                  "--steps", "3", "--warmup", "1", "--force-comm", "--backend", backend,
+                  "--wgrad-stream", str(wgrad_stream)],
+                 {"MASTER_PORT": str(29600 + (backend == "nccl") + 2 * wgrad_stream)})
     cfg = out["config"]
     assert cfg["backend"] == backend and cfg["comm_forced_at_world1"] is True
+    assert cfg["wgrad_stream"] is bool(wgrad_stream)
     trace = out["bucket_launch_ms"]
     assert [t[0] for t in trace[:-1]] == list(range(cfg["buckets"])) and trace[-1][0] == -1
     launch_ms = [t[2] for t in trace[:-1]]
