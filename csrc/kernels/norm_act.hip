@@ -75,7 +75,10 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const bf16_t* __restrict__
 // Reduce the [nblk][2][C] partial slab for 64 consecutive channels per block:
 // 1024 threads = 64 channel lanes x 16 row groups, coalesced 256-B row reads,
 // fp64 accumulation, LDS tree over the 16 groups.  Result in (s, q) of tid<64.
-constexpr int FIN_T = 1024, FIN_G = FIN_T / 64;
+#ifndef MI_FIN_T
+#define MI_FIN_T 1024
+#endif
+constexpr int FIN_T = MI_FIN_T, FIN_G = FIN_T / 64;
 
 __device__ __forceinline__ bool slab_reduce64(const float* __restrict__ part, int nblk, int C, double& s, double& q) {
   __shared__ double red[2][FIN_G][64];
