@@ -43,17 +43,17 @@ c_float = ctypes.c_float
 _SIGNATURES = {}
 
 
-def signature(name, *argtypes):
-    _SIGNATURES[name] = list(argtypes)
+def signature(name, *argtypes, restype=None):
+    _SIGNATURES[name] = (list(argtypes), restype if restype is not None else c_int)
 
 
 def _bind(lib):
-    for name, argtypes in _SIGNATURES.items():
+    for name, (argtypes, restype) in _SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None:
             raise RuntimeError(f"native kernel library is stale: missing symbol {name}; rebuild with `python -m mi355x_dp.build`")
         fn.argtypes = argtypes
-        fn.restype = c_int
+        fn.restype = restype
 
 
 def load(required: bool = True):

@@ -18,6 +18,7 @@ through autograd as usual (works with stock ``torch.nn.parallel.DDP``).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -112,8 +113,12 @@ class WgradStream:
         self.device = torch.device(device)
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         if idx not in WgradStream._streams:
-            st = torch.cuda.Stream(device=self.device)
-            with torch.cuda.device(idx):  # its own split-K slab workspace (gemm_conv.hip)
+            # MI355X_DP_WGRAD_PRIORITY=-1: the side stream's workgroups are dispatched ahead of the
+            # compute stream's (default 0: equal priority; profiles/rn50_bs256_wgrad_stream.md)
+            with torch.cuda.device(idx):
+                st = torch.cuda.Stream(device=self.device,
+                                       priority=int(os.environ.get("MI355X_DP_WGRAD_PRIORITY", "0")))
+                # its own split-K slab workspace (gemm_conv.hip)
                 _lib.call("mi_register_wgrad_stream", ctypes.c_void_p(st.cuda_stream))
             WgradStream._streams[idx] = st
         self.stream = WgradStream._streams[idx]

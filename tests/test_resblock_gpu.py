@@ -184,3 +184,44 @@ def _chain_handoff(R, BatchNorm2d, resblock):
     assert rel_err(dx1, dx0) < 2e-2
     for n in g0:
         assert rel_err(g1[n], g0[n]) < 2e-2, n
+
+
+def test_abandoned_handoff_no_double_count():
+    """A block output with a second consumer: the next block's conv1 dgrad still finalizes the
+    previous block's last BatchNorm into scratch (hand-off), but the previous block receives the
+    SUM of both consumers' gradients -- a different buffer -- so it must drop the hand-off and
+    recompute; its affine gradients are then counted once (matches the per-op path)."""
+    import mi355x_dp.models.resnet as R
+    from mi355x_dp.ops import resblock
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x0 = torch.randn(8, 256, 28, 28, device="cuda", generator=g).to(torch.bfloat16)
+    x0 = x0.contiguous(memory_format=torch.channels_last)
+    d_out = torch.randn(8, 256, 28, 28, device="cuda", generator=g).to(torch.bfloat16)
+    d_mid = torch.randn(8, 256, 28, 28, device="cuda", generator=g).to(torch.bfloat16)
+    res = {}
+    for fused in (False, True):
+        torch.manual_seed(6)
+        b0, b1 = R.Bottleneck(256, 64).cuda(), R.Bottleneck(256, 64).cuda()
+        with torch.no_grad():
+            for mod in list(b0.modules()) + list(b1.modules()):
+                if isinstance(mod, torch.nn.BatchNorm2d):
+                    mod.weight.uniform_(0.5, 1.5)
+                    mod.bias.uniform_(-0.2, 0.2)
+        old = R.FUSED_BLOCKS
+        R.FUSED_BLOCKS = fused
+        used0 = resblock.HANDOFF_USED[0]
+        try:
+            x = x0.clone().requires_grad_()
+            h = b0(x)
+            out = b1(h)
+            torch.autograd.backward([out, h], [d_out.contiguous(memory_format=torch.channels_last),
+                                               d_mid.contiguous(memory_format=torch.channels_last)])
+        finally:
+            R.FUSED_BLOCKS = old
+        torch.cuda.synchronize()
+        if fused:
+            assert resblock.HANDOFF_USED[0] == used0  # the hand-off was abandoned
+        resblock._HANDOFF.clear()
+        res[fused] = {n: p.grad.float() for n, p in list(b0.named_parameters()) + list(b1.named_parameters())}
+    for n in res[False]:
+        assert rel_err(res[True][n], res[False][n]) < 2e-2, n
