@@ -1092,20 +1092,26 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   return hipGetLastError();
 }
 
-// split-K block target of the TN (weight-gradient) kernels: every split adds its tile into the
-// fp32 gradient with atomics, whose chip-wide rate (~1.3 TB/s of added bytes) makes the atomic
-// volume ~ blocks x tile area the cost to balance against occupancy (MI355X_DP_TN_BLOCKS)
-static int g_tn_blocks = -1;
-static int tn_target_blocks() {
+// split-K block target of the TN (weight-gradient) kernels: more splits fill the chip, but every
+// split adds a partial tile of slab traffic and a longer reduce (MI355X_DP_TN_BLOCKS, default 768).
+// On the weight-gradient side stream the TN kernels share the CUs with the data-gradient chain and
+// a smaller grid is better (MI355X_DP_TN_BLOCKS_SIDE, default 384: RN50 bs256 12.56k img/s vs 12.32k
+// at 768, 12.21k at 256; RN152 5463 vs 5295 -- profiles/rn50_bs256_wgrad_stream.md).
+static int g_tn_blocks = -1, g_tn_blocks_side = -1;
+static int tn_target_blocks(hipStream_t st) {
   if (g_tn_blocks < 0) {
     const char* e = std::getenv("MI355X_DP_TN_BLOCKS");
     g_tn_blocks = e ? std::max(64, std::atoi(e)) : 768;
+    const char* es = std::getenv("MI355X_DP_TN_BLOCKS_SIDE");
+    g_tn_blocks_side = es ? std::max(64, std::atoi(es)) : (e ? g_tn_blocks : 384);
   }
-  return g_tn_blocks;
+  int dev = 0;
+  hipGetDevice(&dev);
+  return (st != nullptr && st == g_wgrad_stream[dev & 15]) ? g_tn_blocks_side : g_tn_blocks;
 }
 
 hipError_t dispatch_tn(TNArgs& a, hipStream_t st) {
-  const int target = tn_target_blocks();
+  const int target = tn_target_blocks(st);
   bool n64 = a.N <= 64;
   bool m64 = a.M <= 64;
   if (m64 && n64) return launch_tn<64, 64>(a, st, target);

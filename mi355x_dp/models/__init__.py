@@ -11,7 +11,7 @@ _REGISTRY = {
 
 def get_model(name: str, **kw):
     name = name.lower().replace("-", "").replace("_", "")
-    if name in ("vitb16", "vitb16"):
+    if name == "vitb16":
         from .vit import vit_b_16
         return vit_b_16(**kw)
     if name not in _REGISTRY:

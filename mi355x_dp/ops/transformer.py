@@ -30,7 +30,7 @@ import torch.nn.functional as F
 from . import _lib
 from . import kernels as _k  # noqa: F401
 from ._lib import ptr, stream_of
-from .functional import BF16, _finish_grad, _grad_buffer, linear_weight_t, weight_bf16
+from .functional import BF16, _finish_grad, _grad_buffer, _side, linear_weight_t, weight_bf16
 
 F32 = torch.float32
 EPI_NONE, EPI_GELU, EPI_GELU_BWD, EPI_RESIDUAL = 0, 1, 2, 3
@@ -70,11 +70,26 @@ def _gemm(a2, w16, bias=None, epi=EPI_NONE, aux=None):
 
 
 def _wbgrad(weight, bias, dy2, x2):
-    """weight AND bias gradient from one TN GEMM (the bias column sums ride on its A fragments)."""
+    """weight AND bias gradient from one TN GEMM (the bias column sums ride on its A fragments) --
+    on the engine's weight-gradient stream when it has one (functional.WgradStream), overlapping
+    the layer's data-gradient chain."""
     g, gb = _grad_buffer(weight), _grad_buffer(bias)
     M, N = dy2.shape
     K = x2.shape[1]
-    _lib.call("mi_gemm_tn_bias", ptr(dy2), ptr(x2), ptr(g), ptr(gb), N, K, M, N, K, K, stream_of(dy2))
+
+    def launch():
+        _lib.call("mi_gemm_tn_bias", ptr(dy2), ptr(x2), ptr(g), ptr(gb), N, K, M, N, K, K, stream_of(dy2))
+    side = _side(weight)
+    if side is not None and _side(bias) is not None:
+        cw, cb = getattr(weight, "_mi_on_grad_ready", None), getattr(bias, "_mi_on_grad_ready", None)
+
+        def ready():
+            for c in (cw, cb):
+                if c is not None:
+                    c()
+        side.run(launch, (dy2, x2), ready)
+        return None, None
+    launch()
     return _finish_grad(weight, g), _finish_grad(bias, gb)
 
 

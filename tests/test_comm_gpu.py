@@ -162,3 +162,35 @@ os._exit(0)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "RAISED True" in r.stdout and "RAISED2" in r.stdout, r.stdout + r.stderr
+
+
+def test_wgrad_stream_vit_layers():
+    """ViT encoder layers: the Linear weight + bias gradients (one TN GEMM with column sums each)
+    run on the side stream; gradients match the single-stream engine up to fp32 atomic order, and
+    no bucket is written after its launch."""
+    sys.path.insert(0, ROOT)
+    from mi355x_dp.models.vit import VisionTransformer
+    from mi355x_dp.ops import cross_entropy
+    from mi355x_dp.parallel import DataParallel
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(8, 3, 64, 64, device=dev, generator=g)
+    y = torch.randint(0, 10, (8,), device=dev, generator=g)
+    grads = {}
+    for side, check in ((False, False), (True, False), (True, True)):
+        torch.manual_seed(0)
+        m = VisionTransformer(image_size=64, patch_size=16, num_layers=2, num_heads=4, hidden_dim=256, mlp_dim=512,
+                              num_classes=10).to(dev)
+        e = DataParallel(m, bucket_cap_mb=1, first_bucket_mb=0.5, min_bucket_mb=0, check_stream_order=check,
+                         wgrad_stream=side)
+        e.zero_grad()
+        cross_entropy(e(x), y).backward()
+        e.finish_gradient_sync()
+        torch.cuda.synchronize()
+        assert e.order_violations == []
+        if side:
+            assert e.wgrad_stream.runs >= 2 * 4
+        grads[(side, check)] = e.flat.grad.clone()
+    base = grads[(False, False)]
+    for k in ((True, False), (True, True)):
+        assert float((grads[k] - base).norm() / base.norm()) < 1e-5, k
