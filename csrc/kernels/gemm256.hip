@@ -37,6 +37,7 @@
 #endif
 #include "epilogue.h"
 #include <algorithm>
+#include <mutex>
 #include <cstdlib>
 
 namespace {
@@ -649,20 +650,27 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
 
 // Tail split-K planning: with 1 block per CU, a grid of `tiles` runs in ceil(tiles / CUs) waves;
 // when the last wave is at most 3/4 full its tiles are split along K so it fills the chip.
+// Per (device, stream) -- the forward / data-gradient convs of a projection shortcut run on an
+// auxiliary stream concurrently with the main chain (ops/resblock.py), so two streams must not
+// share the partials or the arrival counters.  A stream beyond the table runs without tail split.
 struct TailWs {
+  hipStream_t st = nullptr;
+  bool used = false;
   float* ws = nullptr;
   size_t ws_floats = 0;
   int* cnt = nullptr;
   int cnt_n = 0;
 };
-static TailWs g_tail_ws[16];
+constexpr int TAIL_WS_STREAMS = 4;
+static TailWs g_tail_ws[16][TAIL_WS_STREAMS];
+static std::mutex g_tail_mu;
 static int g_num_cus = 0;
 static int g_tail_split_env = -1;
 static int g_tail_min_kt = 12;
 
 MI_API void mi_set_tail_split(int on) { g_tail_split_env = on ? 1 : 0; }
 
-static hipError_t plan_tail(G256Args& a, int nk) {
+static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
   if (g_num_cus == 0) {
     int dev = 0;
     hipGetDevice(&dev);
@@ -681,12 +689,22 @@ static hipError_t plan_tail(G256Args& a, int nk) {
     // split still runs >= g_tail_min_kt k-tiles (ViT K=768 GEMMs measured slower when split)
     while (split > 1 && nk / split < g_tail_min_kt) --split;
   }
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_tail_mu);
+  TailWs* wp = nullptr;
+  if (split > 1) {
+    for (auto& e : g_tail_ws[dev & 15])
+      if (e.used && e.st == st) { wp = &e; break; }
+    if (!wp)
+      for (auto& e : g_tail_ws[dev & 15])
+        if (!e.used) { e.used = true; e.st = st; wp = &e; break; }
+    if (!wp) split = 1;
+  }
   a.full_blocks = split > 1 ? full : tiles;
   a.tail_split = split;
   if (split <= 1) return hipSuccess;
-  int dev = 0;
-  hipGetDevice(&dev);
-  TailWs& w = g_tail_ws[dev & 15];
+  TailWs& w = *wp;
   const size_t need = (size_t)tail * split * G_BM * G_BN;
   if (w.ws_floats < need) {
     if (w.ws) hipFree(w.ws);
@@ -726,7 +744,7 @@ MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bia
   a.a_bytes = rsrc_bytes256((int64_t)M * lda);
   a.b_bytes = rsrc_bytes256((int64_t)N * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
-  if (hipError_t e = plan_tail(a, cdiv(K, G_BK)); e != hipSuccess) return (int)e;
+  if (hipError_t e = plan_tail(a, cdiv(K, G_BK), st); e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(gemm256_nt_kernel<0>, dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
@@ -790,7 +808,7 @@ MI_API int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, flo
   a.a_bytes = rsrc_bytes256((int64_t)Nb * H * W * Cs);
   a.b_bytes = rsrc_bytes256((int64_t)N * a.K);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
-  if (hipError_t e = plan_tail(a, cdiv(a.K, G_BK)); e != hipSuccess) return (int)e;
+  if (hipError_t e = plan_tail(a, cdiv(a.K, G_BK), st); e != hipSuccess) return (int)e;
   if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
     fprintf(stderr, "[gemm] g256conv mode=%d M=%d N=%d K=%d Cs=%d R=%d s=%d epi=%d stats=%d blocks=%d\n", mode, a.M,
             a.N, a.K, Cs, R, stride, epi, stats != nullptr, grid_of(a));

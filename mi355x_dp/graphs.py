@@ -30,7 +30,9 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # capture on the warm-up stream: the native library keys lazily allocated workspaces (split-K
+        # partials, BN finalize counters) by stream, and the warm-up allocated this stream's
+        with torch.cuda.graph(self.graph, stream=side):
             self.out = fn()
         torch.cuda.synchronize()
         self.replays = 0
