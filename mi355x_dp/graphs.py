@@ -21,19 +21,26 @@ import torch
 
 class GraphedStep:
     def __init__(self, fn, warmup: int = 2):
+        from mi355x_dp.ops.functional import WgradStream
         self.fn = fn
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                fn()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        # capture on the warm-up stream: the native library keys lazily allocated workspaces (split-K
-        # partials, BN finalize counters) by stream, and the warm-up allocated this stream's
-        with torch.cuda.graph(self.graph, stream=side):
-            self.out = fn()
+        # warm-up and capture run single-stream (no weight-gradient / shortcut side streams) and on
+        # ONE stream: the native library keys lazily allocated workspaces (split-K partials, tail
+        # split, BN finalize counters) by stream, so the warm-up allocates exactly what the
+        # captured kernels use -- nothing may be allocated inside the capture
+        WgradStream.suspended += 1
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    fn()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=side):
+                self.out = fn()
+        finally:
+            WgradStream.suspended -= 1
         torch.cuda.synchronize()
         self.replays = 0
 

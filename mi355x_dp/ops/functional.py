@@ -126,8 +126,13 @@ class WgradStream:
         self.deferred = []
         self.runs = 0
 
+    # > 0 while a GraphedStep warms up / captures: the captured step is single-stream, and its
+    # warm-up must run the same kernels on the same stream so the native library's lazily sized
+    # workspaces exist before capture (no allocation may happen inside it)
+    suspended = 0
+
     def active(self) -> bool:
-        return not torch.cuda.is_current_stream_capturing()
+        return WgradStream.suspended == 0 and not torch.cuda.is_current_stream_capturing()
 
     def run(self, fn, tensors=(), cb=None):
         main = torch.cuda.current_stream(self.device)

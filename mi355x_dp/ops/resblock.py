@@ -63,7 +63,8 @@ _AUX_STREAMS = {}
 
 
 def _aux_stream(dev):
-    if not DS_STREAM or dev.type != "cuda" or torch.cuda.is_current_stream_capturing():
+    from .functional import WgradStream
+    if not DS_STREAM or dev.type != "cuda" or WgradStream.suspended or torch.cuda.is_current_stream_capturing():
         return None
     s = _AUX_STREAMS.get(dev.index)
     if s is None:

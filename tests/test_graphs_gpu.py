@@ -46,3 +46,21 @@ def test_graphed_step_matches_eager():
     assert loss_graph == pytest.approx(loss_eager, rel=1e-3)
     step_eager = (p_eager - snap[0]).abs().max()
     assert float((eng.flat.data - p_eager).abs().max()) <= 1e-2 * float(step_eager)
+
+
+def test_bench_graph_fresh_process():
+    """bench.py --graph in a fresh process: the eager steps before capture run with the weight-
+    gradient side stream, the graph warm-up / capture single-stream on one stream -- every lazily
+    sized native workspace must exist before the capture (regression: a capture-time allocation
+    invalidated the capture when only the side stream's workspace had been sized)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--model", "resnet18", "--batch", "32",
+                        "--image-size", "32", "--num-classes", "10", "--steps", "5", "--warmup", "2", "--graph"],
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["hip_graph"] is True and out["value"] > 0
