@@ -404,3 +404,56 @@ def test_bf16_gradient_allreduce():
     assert (b16[0] == b16py[0]).all()
     assert abs(b16[0] - f32[0]).max() < 2e-3
     assert (b16[0] != f32[0]).any()  # the exchange really was rounded
+
+
+def _big_model():
+    torch.manual_seed(0)
+    # ~12.6 M fp32 parameters (50 MB of gradient): the DEFAULT planner splits it into several buckets
+    return torch.nn.Sequential(torch.nn.Linear(256, 4096), torch.nn.ReLU(), torch.nn.Linear(4096, 2048),
+                               torch.nn.ReLU(), torch.nn.Linear(2048, 1024), torch.nn.ReLU(),
+                               torch.nn.Linear(1024, 10))
+
+
+def _worker_default_plan(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_big_model())  # default bucket plan (link-aware cap, min-size merge)
+        opt = FlatSGD(m, lr=0.05, momentum=0.9)
+        g = torch.Generator().manual_seed(10 + rank)
+        for _ in range(3):
+            x, y = torch.randn(32, 256, generator=g), torch.randint(0, 10, (32,), generator=g)
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            opt.step()
+        q.put((rank, m.flat.data.clone().numpy(), [len(b) for b in m.buckets], m.comm_calls))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, -1))
+        raise
+
+
+def test_four_ranks_default_plan():
+    """4 gloo ranks with the default bucket planner (a 4-rank default-plan run had
+    stalled on a GPU box -- root-caused to hardware-queue oversubscription of ranks sharing one GPU,
+    profiles/multirank_rehearsal.md): every rank finishes, launches the same number of bucket
+    collectives, and ends with bit-identical replicas."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_default_plan, args=(r, 4, port, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in ps:
+        r, d, plan, calls = q.get(timeout=240)
+        res[r] = (d, plan, calls)
+    for p in ps:
+        p.join(60)
+    for r, (d, _, _) in res.items():
+        assert not isinstance(d, Exception), f"rank {r}: {d!r}"
+    plans = {tuple(v[1]) for v in res.values()}
+    assert len(plans) == 1 and len(next(iter(plans))) >= 2, plans
+    assert len({v[2] for v in res.values()}) == 1
+    for r in range(1, 4):
+        assert (res[r][0] == res[0][0]).all(), f"rank {r} diverged"
