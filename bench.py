@@ -46,6 +46,8 @@ def parse():
                    help="gradient all-reduce dtype (bf16: half the bytes; fp32 master weights either way)")
     p.add_argument("--wgrad-stream", type=int, default=int(os.environ.get("MI355X_DP_WGRAD_STREAM", "1")),
                    choices=(0, 1), help="conv weight gradients on a side HIP stream (overlap with data gradients)")
+    p.add_argument("--calibrate-comm", action="store_true",
+                   help="size gradient buckets from an all-reduce alpha-beta fit measured at start-up")
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as one captured HIP graph (launch-bound small-batch configs)")
@@ -104,6 +106,8 @@ def main():
         kw["force_comm"] = True
     kw["grad_comm"] = args.grad_comm
     kw["wgrad_stream"] = bool(args.wgrad_stream)
+    if args.calibrate_comm:
+        kw["calibrate"] = True
     engine = DataParallel(model, **kw)
     opt = FlatSGD(engine, lr=args.lr, momentum=0.9, weight_decay=1e-4)
 
@@ -209,6 +213,7 @@ def main():
             "loss_last": round(last_loss, 4),
             "warmup_s": round(t_w1 - t_w0, 2),
             "replicas_identical": replicas_ok,
+            "comm_calibration": engine.calibration,
             "bucket_launch_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
         }
         print(json.dumps(out), flush=True)

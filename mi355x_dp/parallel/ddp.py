@@ -49,6 +49,9 @@ CHECK_STREAM_ORDER = os.environ.get("MI355X_DP_CHECK_STREAM_ORDER", "0") == "1"
 # dtype of the gradient exchange: "fp32" (default) or "bf16" (half the bytes on the wire; the sums
 # are rounded to bf16 once, identically on every rank, then cast back into the fp32 gradient)
 GRAD_COMM = os.environ.get("MI355X_DP_GRAD_COMM", "fp32")
+# measure the all-reduce alpha-beta model on the actual fabric at construction (world > 1, planner
+# cap not given explicitly) instead of assuming 7 x 153 GB/s xGMI rings with a 25 us launch cost
+CALIBRATE = os.environ.get("MI355X_DP_CALIBRATE", "0") == "1"
 # run conv weight gradients on a side HIP stream, overlapping the data-gradient chain
 # (mi355x_dp.ops.functional.WgradStream); CUDA engines only
 WGRAD_STREAM = os.environ.get("MI355X_DP_WGRAD_STREAM", "1") == "1"
@@ -82,6 +85,48 @@ def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int, l
         buckets.append(cur)
     buckets.append(list(range(tail_begin, n)))
     return merge_small_buckets(buckets, sizes_bytes, min_bytes)
+
+
+def calibrate_allreduce(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32.0), iters=5, warmup=2):
+    """Fit T(S) = alpha + S / B (one all-reduce of S bytes of fp32) on the live process group:
+    a few timed all-reduces per size, least squares over sizes, then the MAX of each parameter
+    over ranks (every rank must plan the same buckets).  Returns (alpha_us, B_GBps)."""
+    import time
+    dev = device if device is not None else torch.device("cpu")
+    cuda = dev.type == "cuda"
+    buf = torch.zeros(int(max(sizes_mb) * 2**20) // 4, dtype=torch.float32, device=dev)
+    xs, ys = [], []
+    for mb in sizes_mb:
+        t = buf[:int(mb * 2**20) // 4]
+        for _ in range(warmup):
+            dist.all_reduce(t, group=process_group)
+        if cuda:
+            torch.cuda.synchronize(dev)
+        dist.barrier(group=process_group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(t, group=process_group)
+        if cuda:
+            torch.cuda.synchronize(dev)
+        xs.append(t.numel() * 4.0)
+        ys.append((time.perf_counter() - t0) / iters)
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    sxx = sum((x - mx) ** 2 for x in xs)
+    slope = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx if sxx > 0 else 0.0
+    slope = max(slope, 1e-15)
+    alpha = max(my - slope * mx, 1e-6)
+    # worst rank: largest latency and largest per-byte time
+    v = torch.tensor([alpha, slope], dtype=torch.float64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=process_group)
+    alpha, slope = float(v[0]), float(v[1])
+    return alpha * 1e6, 1.0 / slope / 1e9
+
+
+def calibrated_cap(alpha_us, bw_gbps, overhead=0.1, min_bytes=4 << 20, max_bytes=64 << 20):
+    """bucket size whose all-reduce spends `overhead` of its time in the fixed latency alpha"""
+    s = alpha_us * 1e-6 * (1.0 - overhead) / overhead * bw_gbps * 1e9
+    return int(max(min_bytes, min(max_bytes, s)))
 
 
 def merge_small_buckets(buckets: List[List[int]], sizes_bytes: List[int], min_bytes: int) -> List[List[int]]:
@@ -118,7 +163,7 @@ class DataParallel(nn.Module):
                  bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
                  check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM,
-                 wgrad_stream: bool = WGRAD_STREAM):
+                 wgrad_stream: bool = WGRAD_STREAM, calibrate: bool = CALIBRATE):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -142,7 +187,13 @@ class DataParallel(nn.Module):
         from . import _reducer_native
         native = _reducer_native.load()
         sizes = [p.numel() * 4 for p in self.flat.params]
-        if bucket_cap_mb is None:
+        self.calibration = None
+        if bucket_cap_mb is None and calibrate and self.distributed and self.world_size > 1:
+            dev = params[0].device if params else torch.device("cpu")
+            a_us, bw = calibrate_allreduce(process_group, dev)
+            cap = calibrated_cap(a_us, bw)
+            self.calibration = {"alpha_us": round(a_us, 2), "algbw_GBps": round(bw, 2), "cap_mb": round(cap / 2**20, 2)}
+        elif bucket_cap_mb is None:
             cap = (native.link_aware_cap(self.world_size) if native is not None
                    else int(32 * 2**20))
         else:

@@ -457,3 +457,37 @@ def test_four_ranks_default_plan():
     assert len({v[2] for v in res.values()}) == 1
     for r in range(1, 4):
         assert (res[r][0] == res[0][0]).all(), f"rank {r} diverged"
+
+
+def _worker_calibrate(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel
+        from mi355x_dp.parallel.ddp import calibrated_cap
+        m = DataParallel(_big_model(), calibrate=True)
+        c = m.calibration
+        assert c is not None and c["alpha_us"] > 0 and c["algbw_GBps"] > 0
+        assert int(c["cap_mb"] * 2**20) in range(4 << 20, (64 << 20) + 1)
+        assert calibrated_cap(c["alpha_us"], c["algbw_GBps"]) >= 4 << 20
+        q.put((rank, c, [len(b) for b in m.buckets]))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None))
+        raise
+
+
+def test_calibrated_bucket_plan_agrees_across_ranks():
+    """DataParallel(calibrate=True): the all-reduce alpha-beta fit is reduced (MAX) over ranks, so
+    every rank derives the same bucket cap and plan (a rank-dependent plan would deadlock)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_calibrate, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (c, plan)) for r, c, plan in [q.get(timeout=180) for _ in ps])
+    for p in ps:
+        p.join(60)
+    for r, (c, _) in res.items():
+        assert not isinstance(c, Exception), f"rank {r}: {c!r}"
+    assert res[0] == res[1]
