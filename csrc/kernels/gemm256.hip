@@ -366,7 +366,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 v = acc[mq * 4 + i][j];
-        *(uint2*)&Ct[(i * 16 + fr) * CST + j * 16 + 4 * fq] =
+        // 8-B slot XOR-swizzled by row bit 3 (conflict-free ds_write_b64 groups, see gemm_conv.hip)
+        *(uint2*)&Ct[(i * 16 + fr) * CST + ((j * 16 + 4 * fq) ^ (((fr >> 3) & 1) << 2))] =
             make_uint2(pack2bf(v[0] + bv[j][0], v[1] + bv[j][1]), pack2bf(v[2] + bv[j][2], v[3] + bv[j][3]));
       }
     lgkm_wait0();
@@ -402,7 +403,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
       for (int u = 0; u < EPI_U; ++u) {
         const int rl = (s0 + u) * 8 + (lane >> 3);
-        const uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
+        uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
+        if ((rl >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // undo the write swizzle
         if (!ok[u]) continue;
         const size_t off = offs[u];
         MI_ASSERT(n + 8 <= a.N, n);

@@ -463,7 +463,10 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       if (a.bias && n0 + nl < a.N) {
         v0 += a.bias[n0 + nl]; v1 += a.bias[n0 + nl + 1]; v2 += a.bias[n0 + nl + 2]; v3 += a.bias[n0 + nl + 3];
       }
-      *(uint2*)&Ct[ml * CST + nl] = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+      // 8-B slot XOR-swizzled by row bit 3: the 16 contiguous lanes of a ds_write_b64 group (rows
+      // fr = 0..15, row stride 4 banks mod 32) hit 16 distinct bank pairs instead of 2-way
+      // conflicting rows fr / fr + 8; the swap stays inside the 16-B chunk the reads fetch
+      *(uint2*)&Ct[ml * CST + (nl ^ (((ml >> 3) & 1) << 2))] = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
     }
   }
   __syncthreads();
@@ -514,7 +517,8 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
     for (int u = 0; u < EU; ++u) {
       if (!ok[u]) continue;
       const int ml = rr + (s0 + u) * RPP;
-      const uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
+      uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
+      if ((ml >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // undo the write swizzle
       const size_t off = offs[u];
       MI_ASSERT(off + 8 <= (size_t)(a.mode == 3 ? a.M : Mrows) * a.ldc, (long long)off);
       uint4 o = v;
