@@ -613,9 +613,17 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
   uint2* Bs = smem + STAGES * BK * AU;     // [STAGES][BK][BU]
 
   const int nbn = (a.N + BN - 1) / BN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // 1-D grid of tiles x splits, XCD-aware: each XCD owns a contiguous run of (split, tile) work
+  // items with the tiles of one split adjacent, so the blocks that read the same reduction rows
+  // (one split's k-range of dY and of the gathered input, shared by all its output tiles) run
+  // together on one XCD and share its L2 -- with the splits as blockIdx.y and XCD = block id % 8
+  // they landed on different XCDs and every tile re-fetched the rows from HBM
+  const int tiles = ((a.M + BM - 1) / BM) * nbn;
+  const int nsplit = gridDim.x / tiles;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = w / tiles, tile = w - split * tiles;
   const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
-  const int kbeg = blockIdx.y * a.k_per_split;
+  const int kbeg = split * a.k_per_split;
   const int kend = min(a.K, kbeg + a.k_per_split);
   if (kbeg >= kend) return;
 
@@ -765,12 +773,12 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
   }
 
   // epilogue: lane holds D[m = 16i + 4g + r][n = 16j + li]
-  const bool single = (gridDim.y == 1);
+  const bool single = (nsplit == 1);
   if (!single && a.ws) {
     // split-K: this block's partial tile goes to its own slab in fragment order -- every store is one
     // fully coalesced 1 KB wave-instruction (64 lanes x float4) -- and tn_splitk_reduce_kernel sums
     // the splits into C: deterministic, and no fp32 atomics (~1.3 TB/s chip-wide) on the hot path
-    f32x4* slab = (f32x4*)a.ws + ((size_t)tile * gridDim.y + blockIdx.y) * (BM * BN / 4);
+    f32x4* slab = (f32x4*)a.ws + ((size_t)tile * nsplit + split) * (BM * BN / 4);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1082,9 +1090,9 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   if (splits > 1 && a.colsum == nullptr && tn_slabs_on())
     a.ws = splitk_workspace((size_t)tiles * splits * BM * BN, st);
   if (glds_on())
-    hipLaunchKernelGGL((tn_kernel<BM, BN, 1>), dim3(tiles, splits), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((tn_kernel<BM, BN, 1>), dim3(tiles * splits), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((tn_kernel<BM, BN, 2>), dim3(tiles, splits), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((tn_kernel<BM, BN, 2>), dim3(tiles * splits), dim3(256), 0, st, a);
   if (a.ws) {
     // split groups per position: ~8 slab reads per thread, at most 64 groups, and enough blocks
     int log2g = 0;
