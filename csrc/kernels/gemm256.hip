@@ -308,13 +308,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     }
     __syncthreads();
     if (!flag[0]) return;
+    // sum the partials in split order 0, 1, ... -- this block's own one re-read from the workspace
+    // -- so the result does not depend on which split arrived last (fp32 adds do not associate)
     for (int q = 0; q < a.tail_split; ++q) {
-      if (q == split) continue;
-      const f32x4* other = (const f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + q) * tile_f) + tid;
+      const f32x4* part = (const f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + q) * tile_f) + tid;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += __builtin_nontemporal_load(other + (i * 4 + j) * 512);
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 v = __builtin_nontemporal_load(part + (i * 4 + j) * 512);
+          acc[i][j] = q == 0 ? v : acc[i][j] + v;
+        }
     }
     if (tid == 0) a.counters[tail_tile] = 0;  // ready for the next launch (stream order)
     __syncthreads();
@@ -654,7 +658,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
 // when the last wave is at most 3/4 full its tiles are split along K so it fills the chip.
 // Per (device, stream) -- the forward / data-gradient convs of a projection shortcut run on an
 // auxiliary stream concurrently with the main chain (ops/resblock.py), so two streams must not
-// share the partials or the arrival counters.  A stream beyond the table runs without tail split.
+// share the partials or the arrival counters.  A stream beyond the table takes over a slot
+// round-robin after a device synchronisation (never inside a graph capture: the capture's warm-up
+// on the same stream claimed its slot), so the split -- and the numerics -- never depend on
+// which streams ran before.
 struct TailWs {
   hipStream_t st = nullptr;
   bool used = false;
@@ -665,6 +672,7 @@ struct TailWs {
 };
 constexpr int TAIL_WS_STREAMS = 4;
 static TailWs g_tail_ws[16][TAIL_WS_STREAMS];
+static int g_tail_evict[16];
 static std::mutex g_tail_mu;
 static int g_num_cus = 0;
 static int g_tail_split_env = -1;
@@ -701,7 +709,11 @@ static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
     if (!wp)
       for (auto& e : g_tail_ws[dev & 15])
         if (!e.used) { e.used = true; e.st = st; wp = &e; break; }
-    if (!wp) split = 1;
+    if (!wp) {
+      wp = &g_tail_ws[dev & 15][g_tail_evict[dev & 15]++ % TAIL_WS_STREAMS];
+      hipDeviceSynchronize();  // its previous owner may still have partials in flight
+      wp->st = st;
+    }
   }
   a.full_blocks = split > 1 ? full : tiles;
   a.tail_split = split;

@@ -152,7 +152,10 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   uint4* Bs = smem + STAGES * BM * 8;    // [STAGES][BN][8]
 
   const int nbn = (a.N + BN - 1) / BN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // mode 3: one parity class per grid row (blockIdx.y).  Folding the classes into an XCD-aware
+  // 1-D grid with a tile's classes adjacent cut a stride-2 3x3 dgrad's HBM fetch from 107 to
+  // 28 MB but made it slower (0.148 vs 0.118 ms): this launch is not fetch-bound
+  const int tile = xcd_remap(blockIdx.x, gridDim.x), cy = blockIdx.y;
   const int tm = tile / nbn;
   int m0 = tm * BM;
   const int n0 = (tile % nbn) * BN;
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   int Mrows = a.M;
   FastDiv fPQ = a.g.fPQ, fQ = a.g.fQ;
   if (a.mode == 3) {
-    cls = a.cls_map[blockIdx.y];
+    cls = a.cls_map[cy];
     ph = cls / a.g.stride; pw = cls - ph * a.g.stride;
     r0 = (ph + a.g.pad) % a.g.stride; s0 = (pw + a.g.pad) % a.g.stride;
     nr = r0 < a.g.R ? (a.g.R - r0 + a.g.stride - 1) / a.g.stride : 0;
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   if (m0 >= Mrows) {
     // empty tile of a parity class: its statistics rows still have to be defined
     if (a.stats) {
-      const int prow = blockIdx.y * a.tiles_m + tm;
+      const int prow = cy * a.tiles_m + tm;
       for (int c = threadIdx.x; c < 2 * BN; c += 256) {
         const int which = c / BN, col = c - which * BN;
         if (n0 + col < a.N) a.stats[((size_t)prow * 2 + which) * a.N + n0 + col] = 0.f;
@@ -580,7 +583,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       }
     }
     __syncthreads();
-    const int prow = blockIdx.y * a.tiles_m + tm;
+    const int prow = cy * a.tiles_m + tm;
     for (int c = tid; c < 2 * BN; c += 256) {
       const int which = c / BN, col = c - which * BN;
       float t = 0.f;

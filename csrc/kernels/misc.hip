@@ -158,8 +158,23 @@ __global__ __launch_bounds__(NT) void ce_fwd_kernel(const float* __restrict__ lo
     const float tot = red[0] + red[1] + red[2] + red[3];
     const float ls = m + __logf(tot);
     lse[row] = ls;
-    atomicAdd(loss, (ls - l[y[row]]) * inv_n);
+    lse[gridDim.x + row] = ls - l[y[row]];  // per-row loss, summed in row order by ce_sum_kernel
   }
+}
+
+// mean of the per-row losses in a fixed order (the loss is bit-reproducible, unlike an atomic sum)
+__global__ __launch_bounds__(NT) void ce_sum_kernel(const float* __restrict__ rowloss, float* __restrict__ loss, int n,
+                                                    float inv_n) {
+  __shared__ float red[NT];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += NT) s += rowloss[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = NT / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] * inv_n;
 }
 
 // dlogits[n][c] = g * inv_n * (softmax - onehot), bf16 [N][ldo] (zero in padding columns)
@@ -335,9 +350,11 @@ MI_API int mi_gap_bwd(const void* dy, void* dx, int Nb, int HW, int C, hipStream
   return (int)hipGetLastError();
 }
 
+// lse: fp32 [2 * N] workspace -- log-sum-exp per row (read by mi_ce_bwd), then the per-row losses.
 MI_API int mi_ce_fwd(const float* logits, const int64_t* y, float* lse, float* loss, int N, int ncls, int ld,
                      hipStream_t st) {
   hipLaunchKernelGGL(ce_fwd_kernel, dim3(N), dim3(NT), 0, st, logits, y, lse, loss, ncls, ld, 1.f / N);
+  hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(NT), 0, st, lse + N, loss, N, 1.f / N);
   return (int)hipGetLastError();
 }
 

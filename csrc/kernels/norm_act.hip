@@ -879,6 +879,7 @@ struct FinCounters {
   bool used[FIN_STREAM_SLOTS] = {};
 };
 static FinCounters g_fin_cnt[16];
+static int g_fin_evict[16];
 static std::mutex g_fin_mu;
 
 static int* fin_counters(int groups, hipStream_t st) {
@@ -896,7 +897,13 @@ static int* fin_counters(int groups, hipStream_t st) {
       w.owner[i] = st;
       return w.cnt + i * FIN_GROUPS;
     }
-  return nullptr;
+  // table full (streams come and go): take over a slot round-robin once its owner's finalizes
+  // have drained, so the one-launch path -- and its reduction order -- never depends on how many
+  // streams the process used before (never inside a capture: the warm-up claimed the slot)
+  const int i = g_fin_evict[dev & 15]++ % FIN_STREAM_SLOTS;
+  hipDeviceSynchronize();
+  w.owner[i] = st;
+  return w.cnt + i * FIN_GROUPS;
 }
 
 // finalize a [nblk][2][C] partial slab: one launch (finalize, or split + finalize for tall slabs)

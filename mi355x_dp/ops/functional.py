@@ -568,8 +568,8 @@ class _CrossEntropy(torch.autograd.Function):
         lg = logits.float().contiguous()
         N, ncls = lg.shape
         tgt = target.to(torch.int64).contiguous()
-        lse = torch.empty(N, dtype=torch.float32, device=lg.device)
-        loss = torch.zeros((), dtype=torch.float32, device=lg.device)
+        lse = torch.empty(2 * N, dtype=torch.float32, device=lg.device)  # [lse rows | per-row losses]
+        loss = torch.empty((), dtype=torch.float32, device=lg.device)
         _lib.call("mi_ce_fwd", ptr(lg), ptr(tgt), ptr(lse), ptr(loss), N, ncls, ncls, stream_of(lg))
         ctx.save_for_backward(lg, tgt, lse)
         ctx.in_dtype = logits.dtype
