@@ -244,6 +244,16 @@ __global__ __launch_bounds__(NT) void augment_kernel(const uint8_t* __restrict__
     const int sw0 = fl ? (W - 1 - w) : w;
     const int sw = sw0 + dx;
     const bool ok = (unsigned)sh < (unsigned)H && (unsigned)sw < (unsigned)W;
+    if (Cout == 8 && C <= 8) {
+      // one 16-byte store per pixel (the stem's 8-channel layout) instead of eight 2-byte ones
+      float f[8];
+      const uint8_t* sp = src + (((size_t)n * H + sh) * W + sw) * C;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        f[c] = (c < C && ok) ? ((float)sp[c] * (1.f / 255.f) - mean[c]) * stdinv[c] : 0.f;
+      *(uint4*)(dst + (size_t)t * 8) = pack8(f);
+      continue;
+    }
     bf16_t* o = dst + (size_t)t * Cout;
     for (int c = 0; c < Cout; ++c) {
       float v = 0.f;

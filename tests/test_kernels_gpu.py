@@ -304,6 +304,10 @@ def test_augment_pipeline():
     xa = augment(u8, 3, mean, std, pad=4, flip=True, seed=3)
     xb = augment(u8, 3, mean, std, pad=4, flip=True, seed=3)
     assert torch.equal(xa, xb)  # deterministic per seed
+    # the stem's 8-channel layout (one 16-byte store per pixel): channels 0-2 as above, 3-7 zero
+    x8 = augment(u8, 8, mean, std, pad=4, flip=True, seed=3)
+    assert x8.shape[1] == 8
+    assert torch.equal(x8[:, :3].float(), xa.float()) and not x8[:, 3:].any()
 
 
 def test_resnet18_train_step_matches_fp32():
