@@ -29,6 +29,9 @@
 #include <mutex>
 #include <cstdlib>
 
+#ifndef MI_NT_PROBE
+#define MI_NT_PROBE 0  // timing probes (wrong results): 1 = no output stores, 2 = no operand loads
+#endif
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
 #endif
@@ -402,7 +405,11 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
     }
   } else if constexpr (STAGES == 1) {
     for (int kt = 0; kt < nk; ++kt) {
+#if MI_NT_PROBE == 2  // timing probe only: no operand loads (LDS left as is)
+      if (kt < 0) issue_loads(kt, 0);
+#else
       issue_loads(kt, 0);
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       compute(0);
@@ -558,10 +565,14 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
           for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
         }
       }
+#if MI_NT_PROBE == 1  // timing probe only: output stores dropped (kept alive, never taken)
+      if (o.x == 0x7fc17fc1u && o.y == 0x7fc27fc2u) *(uint4*)((bf16_t*)a.C + off) = o;
+#else
       if (MI_CONV_NTSTORE)
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16_t*)a.C + off));
       else
         *(uint4*)((bf16_t*)a.C + off) = o;
+#endif
     }
   }
   if (a.stats) {
