@@ -91,7 +91,15 @@ def main():
         if args.backend == "smddp":
             sys.path.append(os.path.join(ROOT, "compat"))
             import smdistributed.dataparallel.torch.torch_smddp  # noqa: F401  (registers 'smddp')
-        dist.init_process_group(backend=args.backend, device_id=dev if args.backend == "nccl" else None)
+        pg_options = None
+        if args.backend == "nccl":
+            # RCCL kernels on a high-priority stream (as the native smddp backend does): with the
+            # compute and weight-gradient streams filling the CUs, the bucket all-reduces are
+            # dispatched first instead of queueing behind backward kernels
+            pg_options = dist.ProcessGroupNCCL.Options()
+            pg_options.is_high_priority_stream = True
+        dist.init_process_group(backend=args.backend, device_id=dev if args.backend == "nccl" else None,
+                                pg_options=pg_options)
 
     from mi355x_dp.models import get_model
     from mi355x_dp.ops import augment, cross_entropy
