@@ -46,6 +46,9 @@ def parse():
                    help="gradient all-reduce dtype (bf16: half the bytes; fp32 master weights either way)")
     p.add_argument("--wgrad-stream", type=int, default=int(os.environ.get("MI355X_DP_WGRAD_STREAM", "1")),
                    choices=(0, 1), help="conv weight gradients on a side HIP stream (overlap with data gradients)")
+    p.add_argument("--shard-optimizer", action="store_true",
+                   default=os.environ.get("MI355X_DP_SHARD_OPTIMIZER", "0") == "1",
+                   help="SMDDP balanced shards: reduce-scatter gradients, shard-local SGD, all-gather parameters")
     p.add_argument("--calibrate-comm", action="store_true",
                    help="size gradient buckets from an all-reduce alpha-beta fit measured at start-up")
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
@@ -116,6 +119,7 @@ def main():
     kw["wgrad_stream"] = bool(args.wgrad_stream)
     if args.calibrate_comm:
         kw["calibrate"] = True
+    kw["shard_optimizer"] = bool(args.shard_optimizer)
     engine = DataParallel(model, **kw)
     opt = FlatSGD(engine, lr=args.lr, momentum=0.9, weight_decay=1e-4)
 
@@ -214,6 +218,7 @@ def main():
                 "comm_forced_at_world1": bool(args.force_comm and world == 1),
                 "buckets": len(engine.buckets),
                 "grad_comm": args.grad_comm,
+                "shard_optimizer": bool(args.shard_optimizer),
                 "wgrad_stream": bool(args.wgrad_stream),
                 "hip_graph": bool(args.graph),
             },

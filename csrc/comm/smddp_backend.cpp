@@ -250,6 +250,10 @@ class SmddpBackend : public c10d::Backend {
                         uint32_t, hipStream_t);
   using Ipc1Fn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int, int, int, uint32_t, int*,
                          uint32_t, hipStream_t);
+  using IpcRsFn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int, float, uint32_t, int*,
+                          uint32_t, hipStream_t);
+  using IpcAgFn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int64_t, uint32_t, int*,
+                          uint32_t, hipStream_t);
 
   void setup_ipc() {
     const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
@@ -257,6 +261,8 @@ class SmddpBackend : public c10d::Backend {
     ipc_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce_f32") : nullptr;
     ipc2_fn_ = h ? (IpcFn)dlsym(h, "mi_ipc_allreduce2_f32") : nullptr;
     ipc1_fn_ = h ? (Ipc1Fn)dlsym(h, "mi_ipc_oneshot") : nullptr;
+    ipc_rs_fn_ = h ? (IpcRsFn)dlsym(h, "mi_ipc_reduce_scatter") : nullptr;
+    ipc_ag_fn_ = h ? (IpcAgFn)dlsym(h, "mi_ipc_all_gather") : nullptr;
     auto flag_bytes = h ? (int64_t (*)())dlsym(h, "mi_ipc_flag_bytes") : nullptr;
     if (!ipc_fn_ || !ipc2_fn_ || !ipc1_fn_ || !flag_bytes || size_ > 8) {
       fprintf(stderr, "smddp: IPC all-reduce unavailable (kernel library %s); using RCCL only\n", lib ? lib : "unset");
@@ -359,6 +365,60 @@ class SmddpBackend : public c10d::Backend {
       TORCH_CHECK(rc == 0, "smddp: IPC collective launch failed with hipError ", rc);
       if (nbytes == 0) break;
     }
+  }
+
+  // balanced-shard reduce-scatter over the mesh (mi_ipc_reduce_scatter): per call every rank
+  // packs `cnt` elements of each rank's piece into its slot with one strided copy and pulls its own
+  // piece from every peer's slot; chunked so world * cnt fits a slot
+  void ipc_reduce_scatter(at::Tensor& out, at::Tensor& in, bool avg, hipStream_t s) {
+    const int64_t S = out.numel();
+    const size_t esz = in.element_size();
+    const int dt = in.scalar_type() == at::kFloat ? 0 : 4;
+    const int64_t per = std::max<int64_t>(1, (int64_t)(ipc_cap_ / esz / size_) & ~(int64_t)3);
+    for (int64_t off = 0; off < S || (S == 0 && off == 0); off += per) {
+      const int64_t cnt = std::min(per, S - off);
+      const uint32_t epoch = ++ipc_epoch_;
+      const void* data[8];
+      uint32_t* flags[8];
+      ipc_slots(epoch, data, flags);
+      if (cnt > 0)
+        HIPCHECK(hipMemcpy2DAsync((void*)data[rank_], cnt * esz, (const char*)in.data_ptr() + off * esz, S * esz,
+                                  cnt * esz, size_, hipMemcpyDeviceToDevice, s));
+      if (ipc_trace_)
+        fprintf(stderr, "[smddp ipc] rank %d epoch %u reduce_scatter dtype=%d n=%lld\n", rank_, epoch, dt,
+                (long long)cnt);
+      const int rc = ipc_rs_fn_(data, flags, rank_, size_, (char*)out.data_ptr() + off * esz, std::max<int64_t>(cnt, 0),
+                                dt, avg ? 1.f / size_ : 1.f, epoch, ipc_err_dev_, ipc_spin_limit_, s);
+      TORCH_CHECK(rc == 0, "smddp: IPC reduce-scatter launch failed with hipError ", rc);
+      if (S == 0) break;
+    }
+  }
+
+  // all-gather over the mesh (mi_ipc_all_gather): any dtype, chunked by the slot size
+  void ipc_all_gather(at::Tensor& out, at::Tensor& in, hipStream_t s) {
+    const int64_t nb = in.numel() * (int64_t)in.element_size();
+    const int64_t per = (int64_t)ipc_cap_ & ~(int64_t)15;
+    for (int64_t off = 0; off < nb || (nb == 0 && off == 0); off += per) {
+      const int64_t cnt = std::min(per, nb - off);
+      const uint32_t epoch = ++ipc_epoch_;
+      const void* data[8];
+      uint32_t* flags[8];
+      ipc_slots(epoch, data, flags);
+      if (cnt > 0)
+        HIPCHECK(hipMemcpyAsync((void*)data[rank_], (const char*)in.data_ptr() + off, cnt, hipMemcpyDeviceToDevice, s));
+      if (ipc_trace_)
+        fprintf(stderr, "[smddp ipc] rank %d epoch %u all_gather bytes=%lld\n", rank_, epoch, (long long)cnt);
+      const int rc = ipc_ag_fn_(data, flags, rank_, size_, (char*)out.data_ptr() + off, std::max<int64_t>(cnt, 0), nb,
+                                epoch, ipc_err_dev_, ipc_spin_limit_, s);
+      TORCH_CHECK(rc == 0, "smddp: IPC all-gather launch failed with hipError ", rc);
+      if (nb == 0) break;
+    }
+  }
+
+  bool ipc_rs_eligible(const at::Tensor& out, const at::Tensor& in, const c10d::ReduceOp& op) const {
+    return ipc_on_ && ipc_rs_fn_ && out.is_contiguous() && in.is_contiguous() &&
+           (in.scalar_type() == at::kFloat || in.scalar_type() == at::kBFloat16) &&
+           out.scalar_type() == in.scalar_type() && (op == c10d::ReduceOp::SUM || op == c10d::ReduceOp::AVG);
   }
 
   static int ipc_dtype(at::ScalarType t) {
@@ -487,6 +547,14 @@ class SmddpBackend : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> _allgather_base(at::Tensor& out, at::Tensor& in,
                                                  const c10d::AllgatherOptions&) override {
     TORCH_CHECK(out.numel() == in.numel() * size_, "smddp _allgather_base: size mismatch");
+    if (solo())
+      return run(c10d::OpType::_ALLGATHER_BASE, {out, in}, {out}, [&](hipStream_t s) {
+        if (out.data_ptr() != in.data_ptr())
+          HIPCHECK(hipMemcpyAsync(out.data_ptr(), in.data_ptr(), in.numel() * in.element_size(),
+                                  hipMemcpyDeviceToDevice, s));
+      });
+    if (ipc_on_ && ipc_ag_fn_ && out.is_contiguous() && in.is_contiguous() && out.scalar_type() == in.scalar_type())
+      return run(c10d::OpType::_ALLGATHER_BASE, {out, in}, {out}, [&](hipStream_t s) { ipc_all_gather(out, in, s); });
     return run(c10d::OpType::_ALLGATHER_BASE, {out, in}, {out}, [&](hipStream_t s) {
       NCCLCHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm(), s));
     });
@@ -510,6 +578,17 @@ class SmddpBackend : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> _reduce_scatter_base(at::Tensor& out, at::Tensor& in,
                                                       const c10d::ReduceScatterOptions& opts) override {
     TORCH_CHECK(in.numel() == out.numel() * size_, "smddp _reduce_scatter_base: size mismatch");
+    if (solo())
+      return run(c10d::OpType::_REDUCE_SCATTER_BASE, {out, in}, {out}, [&](hipStream_t s) {
+        if (out.data_ptr() != in.data_ptr())
+          HIPCHECK(hipMemcpyAsync(out.data_ptr(), in.data_ptr(), in.numel() * in.element_size(),
+                                  hipMemcpyDeviceToDevice, s));
+      });
+    if (ipc_rs_eligible(out, in, opts.reduceOp)) {
+      const bool avg = opts.reduceOp == c10d::ReduceOp::AVG;
+      return run(c10d::OpType::_REDUCE_SCATTER_BASE, {out, in}, {out},
+                 [&](hipStream_t s) { ipc_reduce_scatter(out, in, avg, s); });
+    }
     return run(c10d::OpType::_REDUCE_SCATTER_BASE, {out, in}, {out}, [&](hipStream_t s) {
       NCCLCHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()),
                                   to_nccl(opts.reduceOp), comm(), s));
@@ -645,6 +724,8 @@ class SmddpBackend : public c10d::Backend {
   Ipc1Fn ipc1_fn_ = nullptr;
   bool ipc_only_ = false;
   bool ipc_trace_ = std::getenv("MI355X_DP_SMDDP_IPC_TRACE") != nullptr;
+  IpcRsFn ipc_rs_fn_ = nullptr;
+  IpcAgFn ipc_ag_fn_ = nullptr;
   size_t ipc_cap_ = 4u << 20;
   size_t ipc_oneshot_bytes_ = 256u << 10;  // MI355X_DP_SMDDP_IPC_ONESHOT_KB
   std::vector<void*> ipc_base_;

@@ -19,6 +19,12 @@
 //  * finish(): launch buckets whose parameters never got a gradient (unused parameters:
 //    their zeroed slice is still reduced, matching DDP's find_unused_parameters=False
 //    semantics where every rank participates) and wait for all outstanding work.
+//  * balanced-shard mode (SMDDP's "each GPU reduces one shard of the fused buffer", SURVEY.md
+//    §2.4 / §5.8): a bucket is REDUCE-SCATTERED in place instead of all-reduced -- rank r ends
+//    up with the summed gradient of the r-th 1/world of every bucket, the optimizer updates only
+//    that shard, and gather_params() all-gathers the updated parameter shards in place (one
+//    collective per bucket).  The flat layout pads every bucket to a multiple of world x 64
+//    elements so the shards are equal and aligned.
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Types.hpp>
@@ -108,9 +114,9 @@ class Reducer {
  public:
   Reducer(at::Tensor flat_grad, std::vector<int64_t> offsets, std::vector<int64_t> numels,
           std::vector<std::vector<int64_t>> buckets, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t align,
-          bool force_comm, c10::optional<at::Tensor> comm_buf)
+          bool force_comm, c10::optional<at::Tensor> comm_buf, bool shard)
       : grad_(std::move(flat_grad)), offsets_(std::move(offsets)), numels_(std::move(numels)),
-        buckets_(std::move(buckets)), pg_(std::move(pg)), force_comm_(force_comm) {
+        buckets_(std::move(buckets)), pg_(std::move(pg)), force_comm_(force_comm), shard_(shard) {
     TORCH_CHECK(offsets_.size() == numels_.size(), "offsets / numels mismatch");
     if (comm_buf.has_value() && comm_buf->defined()) {
       // reduced-precision gradient exchange: each bucket is cast into this buffer on the producing
@@ -135,6 +141,13 @@ class Reducer {
       ranges_.emplace_back(lo, hi);
     }
     for (int64_t i = 0; i < np; ++i) TORCH_CHECK(bucket_of_[i] >= 0, "parameter ", i, " not in any bucket");
+    if (shard_) {
+      world_ = pg_ ? pg_->getSize() : 1;
+      rank_ = pg_ ? pg_->getRank() : 0;
+      for (const auto& r : ranges_)
+        TORCH_CHECK((r.second - r.first) % world_ == 0, "shard mode: bucket [", r.first, ", ", r.second,
+                    ") is not a multiple of world size ", world_, " (pad the flat layout per bucket)");
+    }
     reset();
   }
 
@@ -176,11 +189,50 @@ class Reducer {
     if (comm_.defined())
       for (int64_t b = 0; b < (int64_t)ranges_.size(); ++b)
         if (sent_[b]) {
-          const auto& r = ranges_[b];
-          grad_.narrow(0, r.first, r.second - r.first).copy_(comm_.narrow(0, r.first, r.second - r.first));
+          const auto sh = shard_range(b);
+          grad_.narrow(0, sh.first, sh.second - sh.first).copy_(comm_.narrow(0, sh.first, sh.second - sh.first));
         }
     trace_.emplace_back(-1, 0, since_reset_us());
   }
+
+  // [lo, hi) of this rank's shard of bucket b (the whole bucket when not sharding)
+  std::pair<int64_t, int64_t> shard_range(int64_t b) const {
+    const auto& r = ranges_[b];
+    if (!shard_) return r;
+    const int64_t c = (r.second - r.first) / world_;
+    return {r.first + rank_ * c, r.first + (rank_ + 1) * c};
+  }
+
+  // shard mode, after the optimizer updated this rank's shards of `params` (same layout as the
+  // gradient buffer): all-gather every bucket in place, in bucket order, on the backend's stream
+  // (ordered after the optimizer kernel through the producing-stream event); wait_gather() makes
+  // the caller's stream wait for them -- no host synchronisation
+  void gather_params(at::Tensor params) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(shard_, "gather_params: reducer not in shard mode");
+    TORCH_CHECK(params.numel() == grad_.numel() && params.device() == grad_.device(), "gather_params: bad buffer");
+    if (!pg_ || !(pg_->getSize() > 1 || force_comm_)) return;
+    for (int64_t b = 0; b < (int64_t)ranges_.size(); ++b) {
+      const auto& r = ranges_[b];
+      const auto sh = shard_range(b);
+      at::Tensor whole = params.narrow(0, r.first, r.second - r.first);
+      at::Tensor mine = params.narrow(0, sh.first, sh.second - sh.first);
+      gather_works_.push_back(pg_->_allgather_base(whole, mine, c10d::AllgatherOptions()));
+      ++comm_calls_;
+      comm_bytes_ += (r.second - r.first) * params.element_size();
+    }
+  }
+
+  void wait_gather() {
+    std::vector<c10::intrusive_ptr<c10d::Work>> works;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      works.swap(gather_works_);
+    }
+    for (auto& w : works) w->wait();
+  }
+
+  bool sharded() const { return shard_; }
 
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
   int64_t launched() const { return next_; }
@@ -213,10 +265,19 @@ class Reducer {
           slice = c;
           sent_[next_] = true;
         }
-        std::vector<at::Tensor> ts{slice};
-        c10d::AllreduceOptions opts;
-        opts.reduceOp = c10d::ReduceOp::SUM;
-        works_.push_back(pg_->allreduce(ts, opts));
+        if (shard_) {
+          // in place: this rank's shard of the slice receives the sum of every rank's shard
+          const int64_t c = slice.numel() / world_;
+          at::Tensor out = slice.narrow(0, rank_ * c, c);
+          c10d::ReduceScatterOptions opts;
+          opts.reduceOp = c10d::ReduceOp::SUM;
+          works_.push_back(pg_->_reduce_scatter_base(out, slice, opts));
+        } else {
+          std::vector<at::Tensor> ts{slice};
+          c10d::AllreduceOptions opts;
+          opts.reduceOp = c10d::ReduceOp::SUM;
+          works_.push_back(pg_->allreduce(ts, opts));
+        }
         ++comm_calls_;
         comm_bytes_ += (r.second - r.first) * slice.element_size();
       }
@@ -232,8 +293,9 @@ class Reducer {
   std::vector<int64_t> bucket_of_, pending_;
   std::vector<bool> ready_, param_ready_, sent_;
   at::Tensor comm_;
-  std::vector<c10::intrusive_ptr<c10d::Work>> works_;
-  bool force_comm_ = false;
+  std::vector<c10::intrusive_ptr<c10d::Work>> works_, gather_works_;
+  bool force_comm_ = false, shard_ = false;
+  int64_t world_ = 1, rank_ = 0;
   std::vector<std::tuple<int64_t, int64_t, double>> trace_;
   std::chrono::steady_clock::time_point t0_ = std::chrono::steady_clock::now();
   int64_t next_ = 0, comm_calls_ = 0, comm_bytes_ = 0;
@@ -252,12 +314,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("min_bytes") = 0);
   py::class_<mi_ddp::Reducer>(m, "Reducer")
       .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>, std::vector<std::vector<int64_t>>,
-                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t, bool, c10::optional<at::Tensor>>(),
+                    c10::intrusive_ptr<c10d::ProcessGroup>, int64_t, bool, c10::optional<at::Tensor>, bool>(),
            py::arg("flat_grad"), py::arg("offsets"), py::arg("numels"), py::arg("buckets"), py::arg("process_group"),
-           py::arg("align") = 64, py::arg("force_comm") = false, py::arg("comm_buf") = py::none())
+           py::arg("align") = 64, py::arg("force_comm") = false, py::arg("comm_buf") = py::none(),
+           py::arg("shard") = false)
       .def("reset", &mi_ddp::Reducer::reset)
       .def("mark_ready", &mi_ddp::Reducer::mark_ready, py::call_guard<py::gil_scoped_release>())
       .def("finish", &mi_ddp::Reducer::finish, py::call_guard<py::gil_scoped_release>())
+      .def("shard_range", &mi_ddp::Reducer::shard_range)
+      .def("gather_params", &mi_ddp::Reducer::gather_params, py::call_guard<py::gil_scoped_release>())
+      .def("wait_gather", &mi_ddp::Reducer::wait_gather, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("sharded", &mi_ddp::Reducer::sharded)
       .def_property_readonly("num_buckets", &mi_ddp::Reducer::num_buckets)
       .def_property_readonly("launched", &mi_ddp::Reducer::launched)
       .def_property_readonly("comm_calls", &mi_ddp::Reducer::comm_calls)

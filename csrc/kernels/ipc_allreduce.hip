@@ -353,3 +353,115 @@ MI_API int mi_ipc_oneshot(const void* const* data, uint32_t* const* flags, int r
     default: return (int)hipErrorInvalidValue;
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Reduce-scatter and all-gather over the same slots / flags: balanced shards over the xGMI mesh
+// (SMDDP's "every GPU owns one shard of the fused gradient buffer").  Each
+// rank pulls only ITS 1/world of every peer's data, straight over the link to that peer, so the 7
+// links of an MI355X each carry one shard at the same time -- no ring, no multi-hop forwarding.
+//   reduce-scatter: a rank's slot holds its input re-packed as `world` pieces of `c` elements
+//       (piece q is destined for rank q); rank r sums piece r over all slots (fp32 accumulation,
+//       rank order) into out[0, c);
+//   all-gather: a rank's slot holds its own piece; rank r copies every rank q's slot into
+//       out[q * stride, q * stride + c).
+// Slot reuse follows the one-shot argument above (a slot is rewritten two calls later, after
+// every peer has raised the intermediate call's input flag).
+namespace {
+
+__device__ __forceinline__ float ld_f(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float ld_f(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ void st_f(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_f(bf16_t* p, float v) { *p = f2bf(v); }
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void ipc_rs_kernel(IpcRaw p, int rank, int world, T* __restrict__ out, int64_t c,
+                                                     float scale, uint32_t epoch, int* err, uint32_t spin_limit) {
+  if (!ipc_handshake(p, rank, world, epoch, err, spin_limit)) return;
+  const int64_t base = (int64_t)rank * c;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  if constexpr (VEC) {
+    for (int64_t i = 4 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < c; i += 4 * step) {
+      f32x4 s = __builtin_nontemporal_load((const f32x4*)((const float*)p.data[0] + base + i));
+#pragma unroll 1
+      for (int q = 1; q < world; ++q) s += __builtin_nontemporal_load((const f32x4*)((const float*)p.data[q] + base + i));
+      *(f32x4*)((float*)out + i) = s * scale;
+    }
+  } else {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c; i += step) {
+      float s = 0.f;
+#pragma unroll 1
+      for (int q = 0; q < world; ++q) s += ld_f((const T*)p.data[q] + base + i);
+      st_f(out + i, s * scale);
+    }
+  }
+}
+
+template <typename W>
+__global__ __launch_bounds__(256) void ipc_ag_kernel(IpcRaw p, int rank, int world, W* __restrict__ out, int64_t c,
+                                                     int64_t stride, uint32_t epoch, int* err, uint32_t spin_limit) {
+  if (!ipc_handshake(p, rank, world, epoch, err, spin_limit)) return;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int q = 0; q < world; ++q) {
+    const W* src = (const W*)p.data[q];
+    W* dst = out + (int64_t)q * stride;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c; i += step)
+      dst[i] = __builtin_nontemporal_load(src + i);
+  }
+}
+
+int ipc_grid(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(MI_IPC_MAX_GRID, (work + 255) / 256)); }
+
+}  // namespace
+
+// c: elements of the output piece; dtype 0 f32, 4 bf16; scale 1/world for AVG.  Every rank's slot
+// must hold world * c elements (piece q at q * c) before the call.
+MI_API int mi_ipc_reduce_scatter(const void* const* data, uint32_t* const* flags, int rank, int world, void* out,
+                                 int64_t c, int dtype, float scale, uint32_t epoch, int* err, uint32_t spin_limit,
+                                 hipStream_t st) {
+  if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || c < 0 || (dtype != 0 && dtype != 4))
+    return (int)hipErrorInvalidValue;
+  IpcRaw p{};
+  bool vec = dtype == 0 && c % 4 == 0 && ((uintptr_t)out & 15) == 0;
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = data[q];
+    p.flags[q] = flags[q];
+    vec = vec && ((uintptr_t)data[q] & 15) == 0;
+  }
+  if (vec)
+    hipLaunchKernelGGL((ipc_rs_kernel<float, true>), dim3(ipc_grid(c / 4)), dim3(256), 0, st, p, rank, world,
+                       (float*)out, c, scale, epoch, err, spin_limit);
+  else if (dtype == 0)
+    hipLaunchKernelGGL((ipc_rs_kernel<float, false>), dim3(ipc_grid(c)), dim3(256), 0, st, p, rank, world,
+                       (float*)out, c, scale, epoch, err, spin_limit);
+  else
+    hipLaunchKernelGGL((ipc_rs_kernel<bf16_t, false>), dim3(ipc_grid(c)), dim3(256), 0, st, p, rank, world,
+                       (bf16_t*)out, c, scale, epoch, err, spin_limit);
+  return (int)hipGetLastError();
+}
+
+// nbytes: bytes of every rank's piece (its slot payload); stride_bytes: distance between
+// consecutive ranks' pieces in `out`.  Any dtype (a byte copy).
+MI_API int mi_ipc_all_gather(const void* const* data, uint32_t* const* flags, int rank, int world, void* out,
+                             int64_t nbytes, int64_t stride_bytes, uint32_t epoch, int* err, uint32_t spin_limit,
+                             hipStream_t st) {
+  if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || nbytes < 0 || stride_bytes < nbytes)
+    return (int)hipErrorInvalidValue;
+  IpcRaw p{};
+  bool al16 = ((uintptr_t)out & 15) == 0 && nbytes % 16 == 0 && stride_bytes % 16 == 0;
+  bool al4 = ((uintptr_t)out & 3) == 0 && nbytes % 4 == 0 && stride_bytes % 4 == 0;
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = data[q];
+    p.flags[q] = flags[q];
+    al16 = al16 && ((uintptr_t)data[q] & 15) == 0;
+  }
+  if (al16)
+    hipLaunchKernelGGL(ipc_ag_kernel<u32x4>, dim3(ipc_grid(nbytes / 16)), dim3(256), 0, st, p, rank, world,
+                       (u32x4*)out, nbytes / 16, stride_bytes / 16, epoch, err, spin_limit);
+  else if (al4)
+    hipLaunchKernelGGL(ipc_ag_kernel<uint32_t>, dim3(ipc_grid(nbytes / 4)), dim3(256), 0, st, p, rank, world,
+                       (uint32_t*)out, nbytes / 4, stride_bytes / 4, epoch, err, spin_limit);
+  else
+    hipLaunchKernelGGL(ipc_ag_kernel<uint8_t>, dim3(ipc_grid(nbytes)), dim3(256), 0, st, p, rank, world,
+                       (uint8_t*)out, nbytes, stride_bytes, epoch, err, spin_limit);
+  return (int)hipGetLastError();
+}

@@ -22,6 +22,15 @@ Design (MI355X-first):
     ``finish_gradient_sync`` scales explicitly for foreign optimizers.
   * ``state_dict`` keys carry the ``module.`` prefix exactly like torch DDP so
     checkpoints match the reference's rank-0 ``torch.save`` layout.
+  * ``shard_optimizer=True`` is SMDDP's balanced-shard scheme (SURVEY.md §2.4 "SMDDP fused
+    balanced shards", §5.8): every bucket is reduce-scattered instead of all-reduced, so rank r
+    holds the summed gradient of the r-th 1/world of each bucket; ``FlatSGD`` updates only those
+    shards (its momentum buffer holds only them: 1/world of the optimizer state per GPU), and the
+    updated parameter shards are all-gathered in place, one collective per bucket, behind the
+    optimizer on the comm stream.  The next forward waits for them (a stream wait, no host sync)
+    and refreshes the bf16 compute copy.  Same bytes on the wire as the all-reduce (RS + AG), 1/world
+    of the optimizer work and state.  Gradients outside the own shards are undefined after the
+    sync, so only ``FlatSGD`` can drive this mode.
 """
 from __future__ import annotations
 
@@ -55,6 +64,8 @@ CALIBRATE = os.environ.get("MI355X_DP_CALIBRATE", "0") == "1"
 # run conv weight gradients on a side HIP stream, overlapping the data-gradient chain
 # (mi355x_dp.ops.functional.WgradStream); CUDA engines only
 WGRAD_STREAM = os.environ.get("MI355X_DP_WGRAD_STREAM", "1") == "1"
+# balanced-shard mode: reduce-scatter gradients, shard-local optimizer, all-gather parameters
+SHARD_OPTIMIZER = os.environ.get("MI355X_DP_SHARD_OPTIMIZER", "0") == "1"
 
 
 def plan_buckets(sizes_bytes: List[int], cap_bytes: int, first_cap_bytes: int, last_cap_bytes: int = None,
@@ -163,7 +174,8 @@ class DataParallel(nn.Module):
                  bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
                  check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM,
-                 wgrad_stream: bool = WGRAD_STREAM, calibrate: bool = CALIBRATE):
+                 wgrad_stream: bool = WGRAD_STREAM, calibrate: bool = CALIBRATE,
+                 shard_optimizer: bool = SHARD_OPTIMIZER):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -181,12 +193,11 @@ class DataParallel(nn.Module):
         params = list(reversed(params))  # approximate backward order
         from mi355x_dp.models.layers import Conv2d as _NativeConv
         kernel_ids = {id(m.weight) for m in module.modules() if isinstance(m, _NativeConv)}
-        self.flat = FlatParams(params, bf16_copy=bf16_copy, kernel_layout_ids=kernel_ids)
         self.buffers = FlatBuffers(list(module.buffers()))
 
         from . import _reducer_native
         native = _reducer_native.load()
-        sizes = [p.numel() * 4 for p in self.flat.params]
+        sizes = [p.numel() * 4 for p in params]
         self.calibration = None
         if bucket_cap_mb is None and calibrate and self.distributed and self.world_size > 1:
             dev = params[0].device if params else torch.device("cpu")
@@ -205,6 +216,12 @@ class DataParallel(nn.Module):
             self.buckets = [list(b) for b in native.plan_buckets(sizes, cap, first_b, last_b, min_b)]
         else:
             self.buckets = plan_buckets(sizes, cap, first_b, last_b, min_b)
+        # balanced shards: every bucket padded to world x 64 elements (equal, aligned shards)
+        self.sharded = bool(shard_optimizer)
+        self.bucket_align = 64 * (self.world_size if self.sharded else 1)
+        self.flat = FlatParams(params, bf16_copy=bf16_copy, kernel_layout_ids=kernel_ids,
+                               group_ends=[b[-1] for b in self.buckets] if self.sharded else (),
+                               group_align=self.bucket_align)
         self.bucket_of = {}
         for b, idxs in enumerate(self.buckets):
             for i in idxs:
@@ -213,8 +230,18 @@ class DataParallel(nn.Module):
         for idxs in self.buckets:
             lo = self.flat.offsets[idxs[0]]
             hi = self.flat.offsets[idxs[-1]] + self.flat.params[idxs[-1]].numel()
-            hi = min(self.flat.numel, (hi + 63) // 64 * 64)
+            hi = min(self.flat.numel, (hi + self.bucket_align - 1) // self.bucket_align * self.bucket_align)
             self.bucket_ranges.append((lo, hi))
+        # this rank's [lo, hi) of every bucket (the whole bucket unless sharded)
+        self.shard_ranges = []
+        for lo, hi in self.bucket_ranges:
+            if self.sharded:
+                c = (hi - lo) // self.world_size
+                self.shard_ranges.append((lo + self.rank * c, lo + (self.rank + 1) * c))
+            else:
+                self.shard_ranges.append((lo, hi))
+        self._gather_works = []
+        self._gather_pending = False
         self._pending = [0] * len(self.buckets)
         self._ready = [False] * len(self.buckets)
         self._works = []
@@ -235,8 +262,8 @@ class DataParallel(nn.Module):
             if self.comm_on:
                 pg = process_group if process_group is not None else dist.distributed_c10d._get_default_group()
             self.reducer = native.Reducer(self.flat.grad, [int(o) for o in self.flat.offsets],
-                                          [p.numel() for p in self.flat.params], self.buckets, pg, 64,
-                                          bool(force_comm), self._comm_buf)
+                                          [p.numel() for p in self.flat.params], self.buckets, pg, self.bucket_align,
+                                          bool(force_comm), self._comm_buf, self.sharded)
         self.wgrad_stream = None
         if wgrad_stream and self.flat.grad.is_cuda:
             from mi355x_dp.ops.functional import WgradStream
@@ -325,7 +352,12 @@ class DataParallel(nn.Module):
             self._comm_buf[lo:hi].copy_(buf)
             buf = self._comm_buf[lo:hi]
             self._sent.add(b)
-        w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+        if self.sharded:
+            c = (hi - lo) // self.world_size
+            w = dist.reduce_scatter_tensor(buf[self.rank * c:(self.rank + 1) * c], buf, op=dist.ReduceOp.SUM,
+                                           group=self.process_group, async_op=True)
+        else:
+            w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
         self._works.append(w)
         self._py_comm_calls += 1
 
@@ -346,17 +378,21 @@ class DataParallel(nn.Module):
             with torch.cuda.stream(side):
                 stage = g[lo:hi].clone()
                 seen = checksum(stage)
-                w = None
-                if self.comm_on:
-                    w = dist.all_reduce(stage, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+                w = self._reduce_stage(stage) if self.comm_on else None
         else:
             stage = g[lo:hi].clone()
             seen = checksum(stage)
-            w = dist.all_reduce(stage, op=dist.ReduceOp.SUM, group=self.process_group,
-                                async_op=True) if self.comm_on else None
+            w = self._reduce_stage(stage) if self.comm_on else None
         if w is not None:
             self._py_comm_calls += 1
         self._works.append((b, lo, hi, stage, seen, w))
+
+    def _reduce_stage(self, stage):
+        if self.sharded:
+            c = stage.numel() // self.world_size
+            return dist.reduce_scatter_tensor(stage[self.rank * c:(self.rank + 1) * c], stage, op=dist.ReduceOp.SUM,
+                                              group=self.process_group, async_op=True)
+        return dist.all_reduce(stage, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
 
     def _finish_checked(self):
         from mi355x_dp.ops import checksum
@@ -385,9 +421,41 @@ class DataParallel(nn.Module):
         if self.wgrad_stream is not None:
             self.wgrad_stream.join()
 
+    # ------------------------------------------------- balanced-shard mode
+    def gather_params(self):
+        """Shard mode, after the optimizer updated this rank's shards of ``flat.data``: all-gather
+        every bucket's parameter shards in place (async, comm stream).  ``wait_param_sync`` -- called
+        by the next forward, ``state_dict`` and ``sync_params`` -- joins them."""
+        if not self.sharded:
+            return
+        self._gather_pending = True
+        if not self.comm_on:
+            return
+        if self.reducer is not None:
+            self.reducer.gather_params(self.flat.data)
+            return
+        for (lo, hi), (slo, shi) in zip(self.bucket_ranges, self.shard_ranges):
+            self._gather_works.append(dist.all_gather_into_tensor(self.flat.data[lo:hi], self.flat.data[slo:shi],
+                                                                  group=self.process_group, async_op=True))
+            self._py_comm_calls += 1
+
+    def wait_param_sync(self):
+        """Make the current stream wait for the parameter all-gathers, then refresh the bf16
+        compute copy (and the transposed data-gradient operands) from the gathered fp32 masters."""
+        if not self._gather_pending:
+            return
+        if self.reducer is not None:
+            self.reducer.wait_gather()
+        for w in self._gather_works:
+            w.wait()
+        self._gather_works = []
+        self._gather_pending = False
+        self.flat.refresh_bf16()
+
     def forward(self, *args, **kwargs):
         self._join_side()  # a backward whose sync was skipped (no_sync / accumulation) left side work
         self._reset()
+        self.wait_param_sync()
         self._wait_buffer_sync()
         out = self.module(*args, **kwargs)
         if self.broadcast_buffers and self.buffers.buffers and self.module.training:
@@ -409,6 +477,9 @@ class DataParallel(nn.Module):
         """Launch any bucket not yet launched (unused params), then wait for all."""
         self._join_side()
         self._wait_buffer_sync()
+        if average and self.sharded:
+            raise RuntimeError("shard_optimizer=True: gradients outside this rank's shards are not reduced; "
+                               "drive the engine with FlatSGD")
         if self.reducer is not None:
             self.reducer.finish()
             if average and self.world_size > 1:
@@ -424,7 +495,7 @@ class DataParallel(nn.Module):
                 w.wait()
             self._works = []
             for b in sorted(self._sent):
-                lo, hi = self.bucket_ranges[b]
+                lo, hi = self.shard_ranges[b]
                 self.flat.grad[lo:hi].copy_(self._comm_buf[lo:hi])
             self._sent = set()
         if average and self.world_size > 1:
@@ -441,6 +512,7 @@ class DataParallel(nn.Module):
 
     def state_dict(self, *args, **kwargs):
         self._wait_buffer_sync()
+        self.wait_param_sync()
         return super().state_dict(*args, **kwargs)
 
 
@@ -453,7 +525,13 @@ class FlatSGD:
         self.engine = engine
         self.lr, self.momentum, self.dampening = lr, momentum, dampening
         self.weight_decay, self.nesterov = weight_decay, nesterov
-        self.momentum_buf = torch.zeros_like(engine.flat.data) if momentum else None
+        # shard mode: momentum only for this rank's shards, packed (1/world of the optimizer state)
+        self.segments = []  # (flat lo, flat hi, momentum offset)
+        off = 0
+        for lo, hi in engine.shard_ranges if engine.sharded else [(0, engine.flat.numel)]:
+            self.segments.append((lo, hi, off))
+            off += hi - lo
+        self.momentum_buf = torch.zeros(off, dtype=torch.float32, device=engine.flat.data.device) if momentum else None
         self.steps = 0
         self.param_groups = [dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov,
                                   dampening=dampening)]
@@ -466,16 +544,30 @@ class FlatSGD:
         self.engine.finish_gradient_sync(average=False)
         g = self.param_groups[0]
         f = self.engine.flat
-        sgd_flat_(f.data, f.grad, self.momentum_buf, f.bf16, g["lr"], g["momentum"], g["dampening"],
-                  g["weight_decay"], g["nesterov"], first_step=(self.steps == 0), grad_scale=self.engine.grad_scale)
-        f.refresh_transposed()  # dgrad operands of every conv, one launch
+        for lo, hi, mo in self.segments:
+            mom = self.momentum_buf[mo:mo + hi - lo] if self.momentum_buf is not None else None
+            sgd_flat_(f.data[lo:hi], f.grad[lo:hi], mom, f.bf16[lo:hi] if f.bf16 is not None else None, g["lr"],
+                      g["momentum"], g["dampening"], g["weight_decay"], g["nesterov"], first_step=(self.steps == 0),
+                      grad_scale=self.engine.grad_scale)
+        if self.engine.sharded and self.engine.comm_on:
+            self.engine.gather_params()  # bf16 copy + transposed operands refreshed after the gather
+        else:
+            f.refresh_transposed()  # dgrad operands of every conv, one launch
         self.steps += 1
 
     def state_dict(self):
-        return {"steps": self.steps, "param_groups": self.param_groups,
-                "momentum_buf": self.momentum_buf.detach().cpu() if self.momentum_buf is not None else None}
+        """In shard mode ``momentum_buf`` is this rank's packed shards (a per-rank optimizer
+        checkpoint, tagged with ``shard``)."""
+        sd = {"steps": self.steps, "param_groups": self.param_groups,
+              "momentum_buf": self.momentum_buf.detach().cpu() if self.momentum_buf is not None else None}
+        if self.engine.sharded:
+            sd["shard"] = {"rank": self.engine.rank, "world": self.engine.world_size}
+        return sd
 
     def load_state_dict(self, sd):
+        if self.engine.sharded and sd.get("shard") != {"rank": self.engine.rank, "world": self.engine.world_size}:
+            raise ValueError(f"optimizer shard {sd.get('shard')} does not match this rank "
+                             f"({self.engine.rank} of {self.engine.world_size})")
         self.steps = sd["steps"]
         self.param_groups = sd["param_groups"]
         if sd.get("momentum_buf") is not None and self.momentum_buf is not None:

@@ -42,10 +42,14 @@ def _kernel_view(flat: torch.Tensor, off: int, shape, kernel_layout: bool = True
 class FlatParams:
     """Owns the flat fp32 params, fp32 grads and bf16 copy for a list of parameters."""
 
-    def __init__(self, params: Sequence[torch.nn.Parameter], bf16_copy: bool = True, kernel_layout_ids=None):
+    def __init__(self, params: Sequence[torch.nn.Parameter], bf16_copy: bool = True, kernel_layout_ids=None,
+                 group_ends=(), group_align: int = ALIGN):
         """``kernel_layout_ids``: ids of 4-D params consumed by the native conv kernels; they are
         stored [K][R][S][C].  Every other parameter keeps PyTorch's default contiguous layout (a
-        stock nn.Conv2d would otherwise start producing channels_last outputs).  ``None`` = all."""
+        stock nn.Conv2d would otherwise start producing channels_last outputs).  ``None`` = all.
+        ``group_ends``: indices of parameters that close a gradient bucket; the offset after each
+        is rounded up to ``group_align`` elements (balanced-shard mode: every bucket a multiple of
+        world x 64 elements, so its reduce-scatter shards are equal and aligned)."""
         params = [p for p in params if p.requires_grad]
         if not params:
             raise ValueError("no trainable parameters")
@@ -55,9 +59,12 @@ class FlatParams:
         self.kernel_layout = [kernel_layout_ids is None or id(p) in kernel_layout_ids for p in self.params]
         self.offsets = []
         off = 0
-        for p in self.params:
+        ends = set(group_ends)
+        for i, p in enumerate(self.params):
             self.offsets.append(off)
             off += _align(p.numel())
+            if i in ends:
+                off = (off + group_align - 1) // group_align * group_align
         self.numel = off
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)

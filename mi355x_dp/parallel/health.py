@@ -49,6 +49,8 @@ class ReplicaChecker:
 
     def checksum(self) -> float:
         from mi355x_dp.ops import checksum
+        if hasattr(self.engine, "wait_param_sync"):
+            self.engine.wait_param_sync()  # balanced-shard mode: the parameter all-gathers land first
         v = checksum(self.engine.flat.data)
         return float(v) if not isinstance(v, torch.Tensor) else float(v.item())
 

@@ -128,6 +128,24 @@ def test_force_comm_world1_bench(backend, wgrad_stream):
     assert launch_ms == sorted(launch_ms)
 
 
+@pytest.mark.parametrize("backend", ["smddp", "nccl"])
+def test_force_comm_world1_shard_optimizer(backend):
+    """Balanced-shard mode through a real process group at N=1: every bucket goes through
+    reduce-scatter (RCCL in place) and the updated parameters through all-gather; ResNet-50's
+    loss falls the same way as in the all-reduce engine."""
+    common = ["--model", "resnet50", "--batch", "32", "--image-size", "64", "--steps", "4", "--warmup", "1",
+              "--force-comm", "--backend", backend]
+    port = 29610 + 2 * (backend == "nccl")
+    ref = _bench(common, {"MASTER_PORT": str(port)})
+    out = _bench(common + ["--shard-optimizer"], {"MASTER_PORT": str(port + 1)})
+    assert out["config"]["shard_optimizer"] is True and ref["config"]["shard_optimizer"] is False
+    assert out["config"]["buckets"] == ref["config"]["buckets"]
+    trace = out["bucket_launch_ms"]
+    assert [t[0] for t in trace[:-1]] == list(range(out["config"]["buckets"]))
+    # world 1: reduce-scatter and all-gather are identities, so the trajectory is the all-reduce one
+    assert abs(out["loss_last"] - ref["loss_last"]) < 1e-3 * max(1.0, abs(ref["loss_last"])), (out, ref)
+
+
 def test_smddp_error_reporting_and_stream():
     """A failure recorded by the backend's watchdog path makes in-flight and later Works report
     is_success() False and wait() raise; collectives run on the backend's own comm stream."""

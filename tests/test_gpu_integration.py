@@ -240,6 +240,72 @@ def test_smddp_ipc_only_two_ranks(tmp_path):
     assert r.stdout.count("IPC_ONLY_OK") == 2
 
 
+def test_smddp_ipc_balanced_shards_two_ranks(tmp_path):
+    """Balanced shards over the xGMI mesh (IPC-only smddp, 2 ranks sharing cuda:0): reduce-scatter
+    (fp32 SUM / AVG, bf16, in place and out of place, sizes far beyond the 1 MB slot: chunked) and
+    all-gather (fp32, bf16, odd byte counts) against exact references; then ResNet-18 trained with
+    DataParallel(shard_optimizer=True) -- reduce-scatter buckets, shard-local SGD, all-gather params
+    -- ends bit-identical across ranks and equal to the all-reduce engine's parameters."""
+    script = tmp_path / "ipc_shard.py"
+    script.write_text(
+        "import os, sys, torch, torch.distributed as dist\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.append({os.path.join(ROOT, 'compat')!r})\n"
+        "import smdistributed.dataparallel.torch.torch_smddp\n"
+        "dist.init_process_group(backend='smddp')\n"
+        "r, w = dist.get_rank(), dist.get_world_size()\n"
+        "for S in (1, 1000, 700_001):\n"
+        "    base = torch.arange(w * S, device='cuda', dtype=torch.float32)\n"
+        "    for op in (dist.ReduceOp.SUM, dist.ReduceOp.AVG):\n"
+        "        x = base * (r + 1)\n"
+        "        out = torch.empty(S, device='cuda')\n"
+        "        dist.reduce_scatter_tensor(out, x, op=op)\n"
+        "        ref = base[r * S:(r + 1) * S] * 3 / (2 if op == dist.ReduceOp.AVG else 1)\n"
+        "        assert torch.equal(out, ref), (S, op, (out - ref).abs().max().item())\n"
+        "    x = base * (r + 1)\n"
+        "    dist.reduce_scatter_tensor(x[r * S:(r + 1) * S], x)  # in place (the engine's form)\n"
+        "    assert torch.equal(x[r * S:(r + 1) * S], base[r * S:(r + 1) * S] * 3)\n"
+        "    h = torch.full((w * S,), 1.5 + r, device='cuda', dtype=torch.bfloat16)\n"
+        "    ho = torch.empty(S, device='cuda', dtype=torch.bfloat16); dist.reduce_scatter_tensor(ho, h)\n"
+        "    assert float(ho.float().min()) == 4.0 and float(ho.float().max()) == 4.0\n"
+        "    g = torch.zeros(w * S, device='cuda'); g[r * S:(r + 1) * S] = base[r * S:(r + 1) * S] + 0.5\n"
+        "    dist.all_gather_into_tensor(g, g[r * S:(r + 1) * S])\n"
+        "    assert torch.equal(g, base + 0.5)\n"
+        "    gb = torch.empty(w * S, device='cuda', dtype=torch.bfloat16)\n"
+        "    dist.all_gather_into_tensor(gb, torch.full((S,), float(r + 1), device='cuda', dtype=torch.bfloat16))\n"
+        "    assert torch.equal(gb.float(), torch.arange(w, device='cuda').float().repeat_interleave(S) + 1)\n"
+        "u = torch.empty(w * 3, device='cuda', dtype=torch.uint8)\n"
+        "dist.all_gather_into_tensor(u, torch.full((3,), 7 + r, device='cuda', dtype=torch.uint8))\n"
+        "assert u.tolist() == [7] * 3 + [8] * 3, u.tolist()\n"
+        "from mi355x_dp.models import resnet18\n"
+        "from mi355x_dp.ops import cross_entropy\n"
+        "from mi355x_dp.parallel import DataParallel, FlatSGD\n"
+        "from mi355x_dp.parallel.health import ReplicaChecker\n"
+        "res = {}\n"
+        "for shard in (False, True):\n"
+        "    torch.manual_seed(0)\n"
+        "    eng = DataParallel(resnet18(num_classes=10).cuda(), bucket_cap_mb=8, min_bucket_mb=0, shard_optimizer=shard)\n"
+        "    opt = FlatSGD(eng, lr=0.05, momentum=0.9, weight_decay=1e-4)\n"
+        "    g = torch.Generator(device='cuda').manual_seed(r)\n"
+        "    for _ in range(3):\n"
+        "        x = torch.randn(16, 3, 32, 32, device='cuda', generator=g); y = torch.randint(0, 10, (16,), device='cuda', generator=g)\n"
+        "        eng.zero_grad(); cross_entropy(eng(x), y).backward(); opt.step()\n"
+        "    assert ReplicaChecker(eng)(force=True)\n"
+        "    if shard: assert opt.momentum_buf.numel() * w == eng.flat.numel\n"
+        "    res[shard] = {k: v.clone() for k, v in eng.state_dict().items()}\n"
+        "for k, v in res[False].items():\n"
+        "    d = (res[True][k].float() - v.float()).abs().max().item()\n"
+        "    assert d <= 1e-6, (k, d)\n"
+        "torch.cuda.synchronize()\n"
+        "print('IPC_SHARD_OK', r, flush=True)\n"
+        "dist.destroy_process_group()\n")
+    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC_ONLY": "1", "MI355X_DP_SMDDP_DEVICE": "0",
+           "MI355X_DP_SMDDP_IPC_MB": "1", "MI355X_DP_SMDDP_TERMINATE_TRACE": "1"}
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2", str(script)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("IPC_SHARD_OK") == 2
+
+
 @pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "mi355x_dp", "_native", "libmi355x_kernels_debug.so")),
                     reason="debug kernel library not built (python -m mi355x_dp.build kernels --debug)")
 def test_debug_kernels_training_step_clean(tmp_path):

@@ -491,3 +491,84 @@ def test_calibrated_bucket_plan_agrees_across_ranks():
     for r, (c, _) in res.items():
         assert not isinstance(c, Exception), f"rank {r}: {c!r}"
     assert res[0] == res[1]
+
+
+def _worker_shard(rank, world, port, q, py, shard, comm):
+    try:
+        if py:
+            os.environ["MI355X_DP_PY_REDUCER"] = "1"
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0, grad_comm=comm,
+                         shard_optimizer=shard)
+        opt = FlatSGD(m, lr=0.1, momentum=0.9, weight_decay=1e-3)
+        x, y = _data()
+        per = 16 // world
+        part = slice(rank * per, (rank + 1) * per)
+        for _ in range(3):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x[part]), y[part]).backward()
+            opt.step()
+        sd = m.state_dict()  # joins the parameter all-gathers
+        osd = opt.state_dict()
+        ranges = [(lo, hi) for lo, hi in m.bucket_ranges]
+        q.put((rank, {k: v.clone().numpy() for k, v in sd.items()}, m.native_reducer, m.comm_calls,
+               osd["momentum_buf"].numel(), m.flat.numel, ranges, osd.get("shard")))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, None, None, None, None, None))
+        raise
+
+
+def _run_shard(world, py, shard, comm="fp32"):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_shard, args=(r, world, port, q, py, shard, comm)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in ps:
+        r, *rest = q.get(timeout=180)
+        res[r] = rest
+    for p in ps:
+        p.join(60)
+    for r, v in res.items():
+        assert not isinstance(v[0], Exception), f"rank {r}: {v[0]!r}"
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_balanced_shard_optimizer_matches_allreduce(world):
+    """shard_optimizer=True (SMDDP balanced shards: reduce-scatter, shard-local SGD, all-gather):
+    every rank ends with the same parameters as the all-reduce engine, replicas bit-identical, each
+    rank's momentum is 1/world of the (padded) flat buffer, every bucket splits into equal shards,
+    and the native and Python reducers agree bit for bit."""
+    ref = _run_shard(world, py=False, shard=False)
+    nat = _run_shard(world, py=False, shard=True)
+    pyr = _run_shard(world, py=True, shard=True)
+    for res in (nat, pyr):
+        for r in range(1, world):
+            for k in res[0][0]:
+                assert (res[r][0][k] == res[0][0][k]).all(), f"rank {r} diverged at {k}"
+        for k, v in ref[0][0].items():
+            assert abs(res[0][0][k] - v).max() < 1e-5, k
+    assert nat[0][1] is True and pyr[0][1] is False
+    for k in nat[0][0]:
+        assert (nat[0][0][k] == pyr[0][0][k]).all(), k
+    numel, ranges = nat[0][4], nat[0][5]
+    assert all((hi - lo) % (64 * world) == 0 for lo, hi in ranges) and len(ranges) > 1
+    assert nat[0][3] * world == numel  # packed momentum: this rank's shards only
+    assert [nat[r][6] for r in range(world)] == [{"rank": r, "world": world} for r in range(world)]
+    # one reduce-scatter + one all-gather per bucket per step
+    assert nat[0][2] == pyr[0][2] == 3 * 2 * len(ranges)
+
+
+def test_balanced_shard_with_bf16_gradients():
+    """shard_optimizer + grad_comm='bf16': bf16 reduce-scatter, fp32 shard update, fp32 all-gather;
+    replicas bit-identical and within bf16 rounding of the fp32 all-reduce trajectory."""
+    ref = _run_shard(2, py=False, shard=False)
+    res = _run_shard(2, py=False, shard=True, comm="bf16")
+    for k in res[0][0]:
+        assert (res[1][0][k] == res[0][0][k]).all(), k
+        assert abs(res[0][0][k] - ref[0][0][k]).max() < 2e-3, k
