@@ -73,6 +73,12 @@ def main():
         # them -- gloo's host-synchronised copies then crawl (profiles/multirank_rehearsal.md).
         # Must be set before the first HIP call (device_count() does not initialise HIP here).
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
+    else:
+        # one rank per GPU: enough hardware queues that the compute, weight-gradient and comm
+        # streams never share one (mi355x_dp/utils/hwqueues.py: 10.6k -> 12.6k img/s with a
+        # process group on one MI355X)
+        from mi355x_dp.utils import hwqueues
+        hwqueues.ensure()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -95,7 +101,7 @@ def main():
             sys.path.append(os.path.join(ROOT, "compat"))
             import smdistributed.dataparallel.torch.torch_smddp  # noqa: F401  (registers 'smddp')
         pg_options = None
-        if args.backend == "nccl":
+        if args.backend == "nccl" and os.environ.get("MI355X_DP_NCCL_HIPRIO", "1") == "1":
             # RCCL kernels on a high-priority stream (as the native smddp backend does): with the
             # compute and weight-gradient streams filling the CUs, the bucket all-reduces are
             # dispatched first instead of queueing behind backward kernels

@@ -205,3 +205,31 @@ def test_launcher_numa_binding(tmp_path):
     plan = _binding(tmp_path / "missing", 4)
     assert all(how == "slices" for how, _ in plan.values())
     assert plan[0][1][0] == allowed[0]
+
+
+def test_hw_queue_sizing(monkeypatch):
+    """utils.hwqueues.ensure: raises GPU_MAX_HW_QUEUES to 8 before HIP starts when each GPU hosts at
+    most one rank, never lowers an explicit larger value, leaves ranks that share GPUs alone, and
+    does nothing without a GPU or with MI355X_DP_HW_QUEUES=0."""
+    import torch
+    from mi355x_dp.utils import hwqueues
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.delenv("MI355X_DP_HW_QUEUES", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert hwqueues.ensure() == 8 and os.environ["GPU_MAX_HW_QUEUES"] == "8"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
+    assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "16"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "16")  # two ranks per GPU
+    assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    monkeypatch.setenv("MI355X_DP_HW_QUEUES", "0")
+    assert hwqueues.ensure() is None
+    monkeypatch.delenv("MI355X_DP_HW_QUEUES")
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    assert hwqueues.ensure() is None
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
