@@ -164,8 +164,17 @@ class Reducer {
     t0_ = std::chrono::steady_clock::now();
   }
 
+  // DDP no_sync(): while disabled, gradients only accumulate locally -- no bucket is launched
+  // and finish() returns at once; the next synchronised backward reduces the accumulated sums
+  void set_enabled(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    enabled_ = on;
+  }
+  bool enabled() const { return enabled_; }
+
   void mark_ready(int64_t i) {
     std::lock_guard<std::mutex> g(mu_);
+    if (!enabled_) return;
     TORCH_CHECK(i >= 0 && i < (int64_t)param_ready_.size(), "parameter index out of range");
     if (param_ready_[i]) return;
     param_ready_[i] = true;
@@ -180,6 +189,7 @@ class Reducer {
     std::vector<c10::intrusive_ptr<c10d::Work>> works;
     {
       std::lock_guard<std::mutex> g(mu_);
+      if (!enabled_) return;
       std::fill(ready_.begin(), ready_.end(), true);
       launch_ready_locked();
       works.swap(works_);
@@ -294,7 +304,7 @@ class Reducer {
   std::vector<bool> ready_, param_ready_, sent_;
   at::Tensor comm_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_, gather_works_;
-  bool force_comm_ = false, shard_ = false;
+  bool force_comm_ = false, shard_ = false, enabled_ = true;
   int64_t world_ = 1, rank_ = 0;
   std::vector<std::tuple<int64_t, int64_t, double>> trace_;
   std::chrono::steady_clock::time_point t0_ = std::chrono::steady_clock::now();
@@ -325,6 +335,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("gather_params", &mi_ddp::Reducer::gather_params, py::call_guard<py::gil_scoped_release>())
       .def("wait_gather", &mi_ddp::Reducer::wait_gather, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("sharded", &mi_ddp::Reducer::sharded)
+      .def_property("enabled", &mi_ddp::Reducer::enabled, &mi_ddp::Reducer::set_enabled)
       .def_property_readonly("num_buckets", &mi_ddp::Reducer::num_buckets)
       .def_property_readonly("launched", &mi_ddp::Reducer::launched)
       .def_property_readonly("comm_calls", &mi_ddp::Reducer::comm_calls)

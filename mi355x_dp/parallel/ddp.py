@@ -34,6 +34,7 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 import os
 from typing import List, Optional
@@ -175,8 +176,26 @@ class DataParallel(nn.Module):
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
                  check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM,
                  wgrad_stream: bool = WGRAD_STREAM, calibrate: bool = CALIBRATE,
-                 shard_optimizer: bool = SHARD_OPTIMIZER):
+                 shard_optimizer: bool = SHARD_OPTIMIZER, device_ids=None, output_device=None, dim: int = 0,
+                 find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
+                 static_graph: bool = False):
+        """The trailing keyword arguments are torch DDP's (and SMDDP v1's), accepted so the
+        engine is a drop-in ``DistributedDataParallel``: ``device_ids`` / ``output_device`` must
+        name the module's own device (one process per GPU), ``dim`` must be 0 (batch-dim data
+        parallelism); ``find_unused_parameters`` is implied (a bucket whose parameters got no
+        gradient is still reduced at the end of backward), gradients are always bucket views, and
+        ``static_graph`` needs no special path (the bucket order is fixed)."""
         super().__init__()
+        if dim != 0:
+            raise ValueError("DataParallel: only batch-dimension (dim=0) data parallelism")
+        mod_dev = next((p.device for p in module.parameters()), None)
+        for d in list(device_ids or []) + ([output_device] if output_device is not None else []):
+            d = torch.device("cuda", d) if isinstance(d, int) else torch.device(d)
+            if mod_dev is not None and d.type == "cuda" and mod_dev.type == "cuda" and \
+                    d.index not in (None, mod_dev.index):
+                raise ValueError(f"DataParallel: device {d} is not the module's device {mod_dev} "
+                                 "(one process per GPU)")
+        self.require_backward_grad_sync = True
         self.module = module
         self.process_group = process_group
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -325,7 +344,27 @@ class DataParallel(nn.Module):
         self._sent = set()
         self._next = 0
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """torch DDP's gradient-accumulation context: backward passes inside it only accumulate
+        into the flat gradient buffer (no collective); the first backward after it reduces the
+        accumulated sum.  Not available in balanced-shard mode (non-own shards are not kept)."""
+        if self.sharded:
+            raise RuntimeError("no_sync() is not supported with shard_optimizer=True")
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        if self.reducer is not None:
+            self.reducer.enabled = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+            if self.reducer is not None:
+                self.reducer.enabled = old
+
     def _mark_ready(self, i):
+        if not self.require_backward_grad_sync:
+            return
         if self._param_ready[i]:
             return
         self._param_ready[i] = True
@@ -477,6 +516,8 @@ class DataParallel(nn.Module):
         """Launch any bucket not yet launched (unused params), then wait for all."""
         self._join_side()
         self._wait_buffer_sync()
+        if not self.require_backward_grad_sync:
+            return  # inside no_sync(): local accumulation only
         if average and self.sharded:
             raise RuntimeError("shard_optimizer=True: gradients outside this rank's shards are not reduced; "
                                "drive the engine with FlatSGD")

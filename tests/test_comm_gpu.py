@@ -263,3 +263,45 @@ def test_shortcut_aux_stream_bitwise():
     assert all(atomic(n) for n in diff), diff
     g2 = res[(True, True)][1]
     assert float((g2 - g0).norm() / g0.norm()) < 1e-5
+
+
+@pytest.mark.parametrize("model", ["resnet50", "vit_b_16"])
+def test_native_gradients_accumulate(model):
+    """Gradient accumulation (DDP no_sync): every native backward kernel ADDS into the flat fp32
+    gradient -- two backward passes without zero_grad give grad(batch 1) + grad(batch 2) for every
+    parameter (conv wgrad split-K, BN affine, stem, fc / Linear with fused bias, LayerNorm,
+    attention projections), with the weight-gradient side stream on."""
+    sys.path.insert(0, ROOT)
+    from mi355x_dp.models import get_model
+    from mi355x_dp.ops import cross_entropy
+    from mi355x_dp.parallel import DataParallel
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    size = 64 if model == "resnet50" else 224
+    e = DataParallel(get_model(model, num_classes=10).to(dev))
+    g = torch.Generator(device=dev).manual_seed(0)
+    xs = [torch.randn(4, 3, size, size, device=dev, generator=g) for _ in range(2)]
+    ys = [torch.randint(0, 10, (4,), device=dev, generator=g) for _ in range(2)]
+    single = []
+    for x, y in zip(xs, ys):
+        e.zero_grad()
+        cross_entropy(e(x), y).backward()
+        e.finish_gradient_sync()
+        torch.cuda.synchronize()
+        single.append(e.flat.grad.clone())
+    e.zero_grad()
+    with e.no_sync():
+        cross_entropy(e(xs[0]), ys[0]).backward()
+    cross_entropy(e(xs[1]), ys[1]).backward()
+    e.finish_gradient_sync()
+    torch.cuda.synchronize()
+    acc = e.flat.grad
+    names = {id(p): n for n, p in e.module.named_parameters()}
+    bad = []
+    for p, o in zip(e.flat.params, e.flat.offsets):
+        ref = single[0][o:o + p.numel()] + single[1][o:o + p.numel()]
+        got = acc[o:o + p.numel()]
+        err = float((got - ref).norm() / ref.norm().clamp_min(1e-30))
+        if err > 1e-5:
+            bad.append((names[id(p)], err))
+    assert not bad, bad[:10]

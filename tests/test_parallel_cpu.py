@@ -572,3 +572,68 @@ def test_balanced_shard_with_bf16_gradients():
     for k in res[0][0]:
         assert (res[1][0][k] == res[0][0][k]).all(), k
         assert abs(res[0][0][k] - ref[0][0][k]).max() < 2e-3, k
+
+
+def _worker_no_sync(rank, world, port, q, py):
+    try:
+        if py:
+            os.environ["MI355X_DP_PY_REDUCER"] = "1"
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0,
+                         device_ids=None, find_unused_parameters=True, static_graph=True)
+        opt = FlatSGD(m, lr=0.1, momentum=0.9)
+        x, y = _data()
+        part = slice(rank * 8, (rank + 1) * 8)
+        calls = []
+        for _ in range(2):
+            opt.zero_grad()
+            c0 = m.comm_calls
+            with m.no_sync():  # first micro-batch: local accumulation only
+                torch.nn.functional.cross_entropy(m(x[part][:4]), y[part][:4]).backward()
+            calls.append(m.comm_calls - c0)
+            torch.nn.functional.cross_entropy(m(x[part][4:]), y[part][4:]).backward()
+            opt.step()
+        q.put((rank, m.flat.data.clone().numpy(), calls, m.native_reducer))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, None))
+        raise
+
+
+@pytest.mark.parametrize("py", [False, True])
+def test_no_sync_gradient_accumulation(py):
+    """DataParallel.no_sync() (torch DDP's accumulation API, with DDP's constructor kwargs): the
+    micro-batch inside it issues no collective, the next backward reduces the accumulated sum, and
+    the result equals one process accumulating all four micro-batch gradients."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_no_sync, args=(r, 2, port, q, py)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (d, c, nat) for r, d, c, nat in [q.get(timeout=120) for _ in ps]}
+    for p in ps:
+        p.join(60)
+    for r, (d, _, _) in res.items():
+        assert not isinstance(d, Exception), f"rank {r}: {d!r}"
+    assert res[0][1] == [0, 0] and res[0][2] is (not py)
+    assert (res[0][0] == res[1][0]).all()
+    m = _model()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
+    x, y = _data()
+    for _ in range(2):
+        opt.zero_grad()
+        for r in range(2):  # DDP: sum of micro-batch losses per rank, averaged over ranks
+            for sl in (slice(r * 8, r * 8 + 4), slice(r * 8 + 4, r * 8 + 8)):
+                (0.5 * torch.nn.functional.cross_entropy(m(x[sl]), y[sl])).backward()
+        opt.step()
+    from mi355x_dp.parallel import FlatParams
+    ref = FlatParams(list(reversed(list(m.parameters()))), bf16_copy=False, kernel_layout_ids=set()).data
+    assert torch.allclose(torch.from_numpy(res[0][0]), ref, atol=1e-5, rtol=1e-4)
+
+
+def test_ddp_kwargs_validation():
+    from mi355x_dp.parallel import DataParallel
+    with pytest.raises(ValueError):
+        DataParallel(_model(), dim=1)
