@@ -7,7 +7,10 @@
 * ``save_checkpoint`` / ``load_checkpoint`` -- resumable training state the reference
   lacks: model + optimizer (flat momentum buffer) + step/epoch + RNG states, written
   atomically by rank 0 to a separate file (never changes model.pth), restored on every
-  rank (map_location to the local device) with ``weights_only=True``.
+  rank (map_location to the local device) with ``weights_only=True``.  An optimizer whose state is
+  sharded over ranks (``FlatSGD`` under ``DataParallel(shard_optimizer=True)``: each rank holds the
+  momentum of its own shards only) is written by EVERY rank to ``<path>.optim-rank<r>-of-<w>``;
+  the main file records the world size and loading checks it.
 """
 from __future__ import annotations
 
@@ -36,14 +39,29 @@ def save_model(model: torch.nn.Module, model_dir: str, filename: str = "model.pt
 
 def _atomic_save(obj, path):
     d = os.path.dirname(os.path.abspath(path))
-    fd, tmp = tempfile.mkstemp(dir=d, prefix=".tmp_ckpt_")
+    # no leading dot: torch's zip writer derives the archive name from the file name and rejects
+    # an empty stem ("invalid file name")
+    fd, tmp = tempfile.mkstemp(dir=d, prefix="tmp_ckpt_", suffix=".partial")
     os.close(fd)
     torch.save(obj, tmp)
     os.replace(tmp, path)
 
 
+def _world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def optim_shard_path(path: str, rank: int, world: int) -> str:
+    return f"{path}.optim-rank{rank}-of-{world}"
+
+
 def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, step: int = 0, epoch: int = 0,
                     extra: Optional[Dict[str, Any]] = None) -> Optional[str]:
+    osd = optimizer.state_dict() if optimizer is not None else None
+    sharded = isinstance(osd, dict) and "shard" in osd
+    if sharded:
+        os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+        _atomic_save(osd, optim_shard_path(path, _rank(), _world()))
     if _rank() != 0:
         if dist.is_available() and dist.is_initialized():
             dist.barrier()
@@ -57,7 +75,7 @@ def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, step: int
     if torch.cuda.is_available():
         state["rng_cuda"] = torch.cuda.get_rng_state()
     if optimizer is not None:
-        state["optimizer"] = optimizer.state_dict()
+        state["optimizer"] = {"sharded_over": _world()} if sharded else osd
     if extra:
         state["extra"] = extra
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
@@ -71,7 +89,14 @@ def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None, map_locat
     state = torch.load(path, map_location=map_location or "cpu", weights_only=True)
     model.load_state_dict(state["model"])
     if optimizer is not None and "optimizer" in state:
-        optimizer.load_state_dict(state["optimizer"])
+        osd = state["optimizer"]
+        if isinstance(osd, dict) and "sharded_over" in osd:
+            if osd["sharded_over"] != _world():
+                raise ValueError(f"checkpoint optimizer is sharded over {osd['sharded_over']} ranks, "
+                                 f"this job has {_world()}")
+            osd = torch.load(optim_shard_path(path, _rank(), _world()), map_location=map_location or "cpu",
+                             weights_only=True)
+        optimizer.load_state_dict(osd)
     if "rng_cpu" in state:
         torch.set_rng_state(state["rng_cpu"])
     if "rng_cuda" in state and torch.cuda.is_available():

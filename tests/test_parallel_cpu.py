@@ -637,3 +637,60 @@ def test_ddp_kwargs_validation():
     from mi355x_dp.parallel import DataParallel
     with pytest.raises(ValueError):
         DataParallel(_model(), dim=1)
+
+
+def _worker_shard_resume(rank, world, port, q, ckpt):
+    try:
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        from mi355x_dp.utils import load_checkpoint, save_checkpoint
+        x, y = _data()
+        part = slice(rank * 8, (rank + 1) * 8)
+
+        def engine():
+            m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0,
+                             shard_optimizer=True)
+            return m, FlatSGD(m, lr=0.1, momentum=0.9, weight_decay=1e-3)
+
+        def step(m, opt):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x[part]), y[part]).backward()
+            opt.step()
+        m, opt = engine()
+        for _ in range(2):
+            step(m, opt)
+        save_checkpoint(ckpt, m, opt, step=2)
+        for _ in range(2):
+            step(m, opt)
+        a = {k: v.clone() for k, v in m.state_dict().items()}
+        m2, opt2 = engine()
+        for p in m2.module.parameters():  # resume must not depend on the fresh init
+            p.data.add_(1.0)
+        info = load_checkpoint(ckpt, m2, opt2)
+        for _ in range(2):
+            step(m2, opt2)
+        b = m2.state_dict()
+        diff = max(float((a[k] - b[k]).abs().max()) for k in a)
+        q.put((rank, diff, info["step"], os.path.exists(f"{ckpt}.optim-rank{rank}-of-{world}")))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, None))
+        raise
+
+
+def test_balanced_shard_checkpoint_resume(tmp_path):
+    """Resumable checkpoint of a balanced-shard job: every rank writes its optimizer shard next to
+    the rank-0 checkpoint; resuming on fresh engines continues the exact trajectory."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ckpt = str(tmp_path / "ckpt.pt")
+    ps = [ctx.Process(target=_worker_shard_resume, args=(r, 2, port, q, ckpt)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (d, s, e) for r, d, s, e in [q.get(timeout=120) for _ in ps]}
+    for p in ps:
+        p.join(60)
+    for r, (d, s, e) in res.items():
+        assert not isinstance(d, Exception), f"rank {r}: {d!r}"
+        assert d == 0.0 and s == 2 and e, (r, d, s, e)

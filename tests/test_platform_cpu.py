@@ -233,3 +233,30 @@ def test_hw_queue_sizing(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
     assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    """utils.save_model writes the reference's model.pth (plain state_dict) and save_checkpoint /
+    load_checkpoint round-trip model + FlatSGD momentum + step, loaded with weights_only=True."""
+    import torch
+    from mi355x_dp.models import Net
+    from mi355x_dp.parallel import DataParallel, FlatSGD
+    from mi355x_dp.utils import load_checkpoint, save_checkpoint, save_model
+    torch.manual_seed(0)
+    m = DataParallel(Net())
+    opt = FlatSGD(m, lr=0.1, momentum=0.9)
+    x, y = torch.randn(4, 3, 32, 32), torch.randint(0, 10, (4,))
+    for _ in range(2):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    p = save_model(m, str(tmp_path / "model"))
+    sd = torch.load(p, weights_only=True)
+    assert next(iter(sd)).startswith("module.") and all(not k.startswith("tmp") for k in os.listdir(tmp_path / "model"))
+    c = save_checkpoint(str(tmp_path / "ck.pt"), m, opt, step=7, epoch=1)
+    torch.manual_seed(1)
+    m2 = DataParallel(Net())
+    opt2 = FlatSGD(m2, lr=0.1, momentum=0.9)
+    info = load_checkpoint(c, m2, opt2)
+    assert info["step"] == 7 and info["epoch"] == 1 and opt2.steps == 2
+    assert torch.equal(m2.flat.data, m.flat.data) and torch.equal(opt2.momentum_buf, opt.momentum_buf)
