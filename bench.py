@@ -158,6 +158,11 @@ def main():
             return graphed()
         return core()
 
+    # MI355X_DP_MAIN_PRIORITY=-1: the training step's compute stream at high priority (its
+    # workgroups dispatched ahead of the weight-gradient side stream's)
+    main_prio = int(os.environ.get("MI355X_DP_MAIN_PRIORITY", "0"))
+    if main_prio:
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=main_prio))
     t_w0 = time.time()
     for i in range(args.warmup):
         loss = step(i)

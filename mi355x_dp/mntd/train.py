@@ -66,9 +66,12 @@ def _dist():
 
 def generate(task, kind, troj_type="M", shadow_prop=0.02, target_prop=0.5, shadow_num=24, target_num=8,
              n_epoch=None, gpu=False, save_root="./shadow_model_ckpt", data_root="./raw_data/", verbose=False,
-             limit_train=None):
+             limit_train=None, batched=False):
     """kind: 'benign' (shadow_benign_i + target_benign_i), 'jumbo' (shadow_jumbo_i),
-    'trojaned' (target_troj{M,B}_i).  Returns the JSON log dict (written by rank 0)."""
+    'trojaned' (target_troj{M,B}_i).  Returns the JSON log dict (written by rank 0).
+    ``batched=True``: this rank's models train together, one vmapped step for all of them
+    (``mntd.batched``) -- same initial weights, same per-model data order, same Adam arithmetic as
+    the one-at-a-time loop."""
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     np.random.seed(0)
@@ -102,18 +105,31 @@ def generate(task, kind, troj_type="M", shadow_prop=0.02, target_prop=0.5, shado
     # attack settings drawn serially (same RNG stream as the single-process reference run)
     settings = [troj_setting(t) if t else None for (_, _, _, t) in jobs]
     results = {}
+    mine = []
     for j, ((name, idx, ep, t), atk) in enumerate(zip(jobs, settings)):
         if j % world != rank:
             continue
         torch.manual_seed(1000 + j)  # per-model seeds: identical models whichever rank trains them
         np.random.seed(1000 + j)
         model = Model(gpu=gpu)
+        # per-model shuffle generator: the data order does not depend on which rank trains the
+        # model or whether it trains alone or batched with others
+        shuf = torch.Generator().manual_seed(2000 + j)
         if atk is None:
-            loader = torch.utils.data.DataLoader(torch.utils.data.Subset(trainset, idx), batch_size=bs, shuffle=True)
+            loader = torch.utils.data.DataLoader(torch.utils.data.Subset(trainset, idx), batch_size=bs, shuffle=True,
+                                                 generator=shuf)
         else:
             loader = torch.utils.data.DataLoader(BackdoorDataset(trainset, atk, troj_gen, choice=idx,
-                                                                 need_pad=need_pad), batch_size=bs, shuffle=True)
-        train_model(model, loader, ep, is_binary, verbose=verbose)
+                                                                 need_pad=need_pad), batch_size=bs, shuffle=True,
+                                                 generator=shuf)
+        mine.append((name, model, loader, ep, atk))
+    if batched and mine:
+        from .batched import train_models_batched
+        train_models_batched([m for _, m, _, _, _ in mine], [l for _, _, l, _, _ in mine], [e for *_, e, _ in mine],
+                             is_binary, verbose=verbose)
+    for name, model, loader, ep, atk in mine:
+        if not batched:
+            train_model(model, loader, ep, is_binary, verbose=verbose)
         path = os.path.join(save_dir, name + ".model")
         torch.save(model.state_dict(), path)
         acc = eval_model(model, testloader, is_binary)
@@ -149,11 +165,12 @@ def main(argv=None):
     ap.add_argument("--epochs", type=int, default=None)
     ap.add_argument("--gpu", action="store_true")
     ap.add_argument("--distributed", action="store_true", help="task-parallel over WORLD_SIZE ranks (gloo/smddp)")
+    ap.add_argument("--batched", action="store_true", help="train this rank's models together (one vmapped step)")
     a = ap.parse_args(argv)
     if a.distributed:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    print(json.dumps(generate(a.task, a.kind, a.troj_type, n_epoch=a.epochs, gpu=a.gpu)))
+    print(json.dumps(generate(a.task, a.kind, a.troj_type, n_epoch=a.epochs, gpu=a.gpu, batched=a.batched)))
 
 
 if __name__ == "__main__":

@@ -149,3 +149,47 @@ def test_batched_meta_eval_matches_sequential():
             M.BATCHED_EVAL = True
         assert np.allclose(p1, p2, rtol=1e-4, atol=1e-5), (p1, p2)
         assert (l1 == l2).all() and np.allclose(loss1, loss2, rtol=1e-4, atol=1e-6)
+
+
+def test_batched_shadow_training_matches_serial(tmp_path):
+    """mntd.batched: the generation drivers with batched=True (all of a rank's shadow models in one
+    vmapped step, stacked Adam) give the serial loop's models -- same init, same per-model data
+    order -- to fp32 rounding of the batched convolutions; also the trainer alone on models whose
+    datasets (and so last-batch sizes) and epoch counts differ."""
+    from mi355x_dp.mntd.batched import train_models_batched
+    from mi355x_dp.mntd.models import MNISTCNN
+    from mi355x_dp.mntd.train import generate
+    root = str(tmp_path)
+    for b in (False, True):
+        generate("mnist", "jumbo", shadow_num=3, n_epoch=1, save_root=os.path.join(root, f"b{int(b)}"),
+                 data_root=os.path.join(root, "data"), limit_train=300, batched=b)
+    for i in range(3):
+        a = torch.load(os.path.join(root, "b0", "mnist", "models", f"shadow_jumbo_{i}.model"), weights_only=True)
+        b = torch.load(os.path.join(root, "b1", "mnist", "models", f"shadow_jumbo_{i}.model"), weights_only=True)
+        for k in a:
+            assert torch.allclose(a[k], b[k], atol=1e-4), (i, k, (a[k] - b[k]).abs().max())
+    torch.manual_seed(0)
+    data = [(torch.randn(40 + 10 * i, 1, 28, 28), torch.randint(0, 10, (40 + 10 * i,))) for i in range(3)]
+
+    def loaders():
+        return [torch.utils.data.DataLoader(torch.utils.data.TensorDataset(*d), batch_size=16, shuffle=True,
+                                            generator=torch.Generator().manual_seed(5 + i)) for i, d in enumerate(data)]
+    models, ref = [], []
+    for i in range(3):
+        torch.manual_seed(100 + i)
+        models.append(MNISTCNN())
+        torch.manual_seed(100 + i)
+        ref.append(MNISTCNN())
+    epochs = [2, 1, 2]
+    train_models_batched(models, loaders(), epochs, False)
+    for i, (m, l) in enumerate(zip(ref, loaders())):
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        for _ in range(epochs[i]):
+            for x, y in l:
+                loss = m.loss(m(x), y)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+    for a, b in zip(models, ref):
+        for pa, pb in zip(a.parameters(), b.parameters()):
+            assert torch.allclose(pa, pb, atol=5e-5), (pa - pb).abs().max()
