@@ -283,12 +283,13 @@ class DataParallel(nn.Module):
             self.reducer = native.Reducer(self.flat.grad, [int(o) for o in self.flat.offsets],
                                           [p.numel() for p in self.flat.params], self.buckets, pg, self.bucket_align,
                                           bool(force_comm), self._comm_buf, self.sharded)
+        self._comm_hook = None
         self.wgrad_stream = None
         if wgrad_stream and self.flat.grad.is_cuda:
             from mi355x_dp.ops.functional import WgradStream
             self.wgrad_stream = WgradStream(self.flat.grad.device)
         for i, p in enumerate(self.flat.params):
-            cb = functools.partial(self.reducer.mark_ready, i) if self.reducer is not None \
+            cb = functools.partial(self._ready_native, i) if self.reducer is not None \
                 else self._make_ready_cb(i)
             p._mi_on_grad_ready = cb
             p._mi_side = self.wgrad_stream
@@ -314,7 +315,9 @@ class DataParallel(nn.Module):
 
     @property
     def comm_calls(self) -> int:
-        return self.reducer.comm_calls if self.reducer is not None else self._py_comm_calls
+        if self.reducer is not None and self._comm_hook is None:
+            return self.reducer.comm_calls
+        return self._py_comm_calls
 
     @property
     def native_reducer(self) -> bool:
@@ -332,10 +335,33 @@ class DataParallel(nn.Module):
             cb()
         return hook
 
+    def _ready_native(self, i):
+        if self._comm_hook is None:
+            self.reducer.mark_ready(i)
+        else:
+            self._mark_ready(i)
+
+    def register_comm_hook(self, state, hook):
+        """torch DDP's communication hook: ``hook(state, bucket) -> Future[Tensor]`` replaces the
+        bucket all-reduce.  ``bucket`` offers DDP's GradBucket interface (``index``, ``buffer`` --
+        the bucket's slice of the flat gradient, ``gradients``, ``parameters``, ``is_last``,
+        ``set_buffer``); the future's tensor becomes the bucket's gradient.  As in torch DDP the hook
+        owns the averaging (torch's ``allreduce_hook`` / ``fp16_compress_hook`` /
+        ``bf16_compress_hook`` divide by the world size), so ``FlatSGD`` no longer scales by
+        1/world.  Buckets keep the engine's plan and launch order; the hooked path runs in Python."""
+        if self._comm_hook is not None:
+            raise RuntimeError("register_comm_hook can only be called once")
+        if self.sharded or self.check_stream_order or self.grad_comm != "fp32":
+            raise RuntimeError("register_comm_hook: not combinable with shard_optimizer, check_stream_order "
+                               "or grad_comm='bf16' (a hook can compress itself)")
+        self._comm_hook = (state, hook)
+        self._reset()
+
     def _reset(self):
         if self.reducer is not None:
             self.reducer.reset()
-            return
+            if self._comm_hook is None:
+                return
         for b, idxs in enumerate(self.buckets):
             self._pending[b] = len(idxs)
             self._ready[b] = False
@@ -385,6 +411,11 @@ class DataParallel(nn.Module):
             self._launch_checked(b, lo, hi)
             return
         if not self.comm_on:
+            return
+        if self._comm_hook is not None:
+            state, hook = self._comm_hook
+            self._works.append((lo, hi, hook(state, _GradBucket(self, b))))
+            self._py_comm_calls += 1
             return
         buf = self.flat.grad[lo:hi]
         if self._comm_buf is not None:
@@ -521,6 +552,18 @@ class DataParallel(nn.Module):
         if average and self.sharded:
             raise RuntimeError("shard_optimizer=True: gradients outside this rank's shards are not reduced; "
                                "drive the engine with FlatSGD")
+        if self._comm_hook is not None:
+            for b in range(len(self.buckets)):
+                self._ready[b] = True
+            self._launch_ready()
+            for lo, hi, fut in self._works:
+                t = fut.wait()
+                t = t[0] if isinstance(t, (list, tuple)) else t
+                dst = self.flat.grad[lo:hi]
+                if t.data_ptr() != dst.data_ptr():
+                    dst.copy_(t.reshape(-1))
+            self._works = []
+            return  # the hook averaged
         if self.reducer is not None:
             self.reducer.finish()
             if average and self.world_size > 1:
@@ -544,7 +587,7 @@ class DataParallel(nn.Module):
 
     @property
     def grad_scale(self) -> float:
-        return 1.0 / self.world_size
+        return 1.0 if self._comm_hook is not None and self.comm_on else 1.0 / self.world_size
 
     def zero_grad(self, set_to_none: bool = False):
         self._join_side()
@@ -555,6 +598,33 @@ class DataParallel(nn.Module):
         self._wait_buffer_sync()
         self.wait_param_sync()
         return super().state_dict(*args, **kwargs)
+
+
+class _GradBucket:
+    """torch.distributed.GradBucket's interface over one bucket of the flat gradient buffer."""
+
+    def __init__(self, engine: DataParallel, b: int):
+        self._e, self._b = engine, b
+        lo, hi = engine.bucket_ranges[b]
+        self._buf = engine.flat.grad[lo:hi]
+
+    def index(self) -> int:
+        return self._b
+
+    def buffer(self) -> torch.Tensor:
+        return self._buf
+
+    def set_buffer(self, t: torch.Tensor):
+        self._buf.copy_(t.reshape(-1))
+
+    def is_last(self) -> bool:
+        return self._b == len(self._e.buckets) - 1
+
+    def parameters(self):
+        return [self._e.flat.params[i] for i in self._e.buckets[self._b]]
+
+    def gradients(self):
+        return [p.grad for p in self.parameters()]
 
 
 class FlatSGD:

@@ -694,3 +694,64 @@ def test_balanced_shard_checkpoint_resume(tmp_path):
     for r, (d, s, e) in res.items():
         assert not isinstance(d, Exception), f"rank {r}: {d!r}"
         assert d == 0.0 and s == 2 and e, (r, d, s, e)
+
+
+def _worker_comm_hook(rank, world, port, q, which):
+    try:
+        _init(rank, world, port)
+        from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+        from mi355x_dp.parallel import DataParallel, FlatSGD
+        m = DataParallel(_model(), bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0)
+        if which == "allreduce":
+            m.register_comm_hook(None, default_hooks.allreduce_hook)
+        elif which == "fp16":
+            m.register_comm_hook(None, default_hooks.fp16_compress_hook)
+        seen = []
+        if which == "custom":
+            def hook(state, bucket):  # records the bucket interface, then a plain averaged all-reduce
+                seen.append((bucket.index(), bucket.is_last(), len(bucket.parameters()),
+                             sum(g.numel() for g in bucket.gradients()) <= bucket.buffer().numel()))
+                t = bucket.buffer().div_(world)
+                return dist.all_reduce(t, async_op=True).get_future().then(lambda f: f.value()[0])
+            m.register_comm_hook("state", hook)
+        opt = FlatSGD(m, lr=0.1, momentum=0.9)
+        x, y = _data()
+        part = slice(rank * 8, (rank + 1) * 8)
+        for _ in range(3):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x[part]), y[part]).backward()
+            opt.step()
+        q.put((rank, m.flat.data.clone().numpy(), seen, len(m.buckets)))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e, None, None))
+        raise
+
+
+def test_ddp_comm_hooks():
+    """register_comm_hook with torch's own DDP hooks (allreduce_hook, fp16_compress_hook) and a
+    custom hook: same trajectory as the engine's fused all-reduce (fp16: within fp16 rounding),
+    replicas identical, GradBucket interface (index / is_last / parameters / gradients / buffer)."""
+    out = {}
+    for which in ("none", "allreduce", "fp16", "custom"):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _port()
+        ps = [ctx.Process(target=_worker_comm_hook, args=(r, 2, port, q, which)) for r in range(2)]
+        for p in ps:
+            p.start()
+        res = {r: (d, seen, nb) for r, d, seen, nb in [q.get(timeout=120) for _ in ps]}
+        for p in ps:
+            p.join(60)
+        for r, (d, _, _) in res.items():
+            assert not isinstance(d, Exception), f"{which} rank {r}: {d!r}"
+        assert (res[0][0] == res[1][0]).all(), which
+        out[which] = res[0]
+    base = out["none"][0]
+    assert abs(out["allreduce"][0] - base).max() < 1e-6
+    assert abs(out["custom"][0] - base).max() < 1e-6
+    assert 0 < abs(out["fp16"][0] - base).max() < 1e-2
+    seen, nb = out["custom"][1], out["custom"][2]
+    assert [s[0] for s in seen] == list(range(nb)) * 3
+    assert [s[1] for s in seen[:nb]] == [False] * (nb - 1) + [True]
+    assert all(s[2] > 0 and s[3] for s in seen)

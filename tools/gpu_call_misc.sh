@@ -1,0 +1,4 @@
+bash tools/gpu_steps.sh \
+  mntd_train 300 "python tools/bench_mntd_train.py --device cuda --models 24 --epochs 3" \
+  r18_graph_force 200 "python bench.py --model resnet18 --image-size 32 --batch 32 --graph --force-comm --steps 200 --warmup 5" \
+  r18_graph 200 "python bench.py --model resnet18 --image-size 32 --batch 32 --graph --steps 200 --warmup 5"
