@@ -27,7 +27,8 @@ def main():
     from mi355x_dp.mntd.train import train_model
     dev = torch.device(a.device)
     torch.manual_seed(0)
-    data = [(torch.rand(a.n, 1, 28, 28, device=dev), torch.randint(0, 10, (a.n,), device=dev)) for _ in range(a.models)]
+    # host-resident data, as the reference's loaders (the models move each batch to their device)
+    data = [(torch.rand(a.n, 1, 28, 28), torch.randint(0, 10, (a.n,))) for _ in range(a.models)]
 
     def loaders():
         return [torch.utils.data.DataLoader(torch.utils.data.TensorDataset(*d), batch_size=100, shuffle=True,
