@@ -377,3 +377,16 @@ def test_reference_notebook2_verbatim(tmp_path):
     assert accs[-1] > 0.3  # learned something (synthetic data; Bayes accuracy ~0.78)
     secs = int(re.search(r"Training seconds: (\d+)", out).group(1))
     assert secs < 438, f"job slower than the reference's 8xA100 438 s: {secs}"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_smddp_ipc_mesh_collectives_multi_rank(world):
+    """IPC mesh reduce-scatter / all-gather / chunked all-reduce at world 2 and 4 (ranks sharing
+    cuda:0, one hardware queue each), every rank against exact references (tools/ipc_mesh_check.py)."""
+    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC_ONLY": "1", "MI355X_DP_SMDDP_DEVICE": "0",
+           "MI355X_DP_SMDDP_IPC_MB": "1", "GPU_MAX_HW_QUEUES": "1"}
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", str(world),
+                        os.path.join(ROOT, "tools", "ipc_mesh_check.py")], cwd=ROOT, capture_output=True, text=True,
+                       timeout=150, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("MESH_OK") == world

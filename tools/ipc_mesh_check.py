@@ -1,0 +1,45 @@
+"""IPC mesh collectives at world size W (IPC-only smddp; ranks may share one GPU): reduce-scatter
+(fp32 SUM / AVG, bf16, in place, chunked past the slot), all-gather (fp32, bf16, odd bytes) and the
+chunked two-shot all-reduce against exact references.  Prints MESH_OK <rank> <world>."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.append(os.path.join(ROOT, "compat"))
+import smdistributed.dataparallel.torch.torch_smddp  # noqa: E402,F401
+
+dist.init_process_group(backend="smddp")
+r, w = dist.get_rank(), dist.get_world_size()
+tot = sum(q + 1 for q in range(w))
+for S in (1, 1000, 300_001):
+    base = torch.arange(w * S, device="cuda", dtype=torch.float32)
+    for op in (dist.ReduceOp.SUM, dist.ReduceOp.AVG):
+        out = torch.empty(S, device="cuda")
+        dist.reduce_scatter_tensor(out, base * (r + 1), op=op)
+        ref = base[r * S:(r + 1) * S] * tot / (w if op == dist.ReduceOp.AVG else 1)
+        assert torch.allclose(out, ref, rtol=1e-6), (S, op, (out - ref).abs().max().item())
+    x = base * (r + 1)
+    dist.reduce_scatter_tensor(x[r * S:(r + 1) * S], x)
+    assert torch.allclose(x[r * S:(r + 1) * S], base[r * S:(r + 1) * S] * tot, rtol=1e-6)
+    h = torch.full((w * S,), 0.5 + r, device="cuda", dtype=torch.bfloat16)
+    ho = torch.empty(S, device="cuda", dtype=torch.bfloat16)
+    dist.reduce_scatter_tensor(ho, h)
+    want = sum(0.5 + q for q in range(w))
+    assert float(ho.float().min()) == want and float(ho.float().max()) == want
+    g = torch.zeros(w * S, device="cuda")
+    g[r * S:(r + 1) * S] = base[r * S:(r + 1) * S] + 0.5
+    dist.all_gather_into_tensor(g, g[r * S:(r + 1) * S])
+    assert torch.equal(g, base + 0.5)
+    t = torch.arange(S, device="cuda", dtype=torch.float32) * (r + 1)
+    dist.all_reduce(t)
+    assert torch.allclose(t, torch.arange(S, device="cuda", dtype=torch.float32) * tot, rtol=1e-6)
+u = torch.empty(w * 3, device="cuda", dtype=torch.uint8)
+dist.all_gather_into_tensor(u, torch.full((3,), 7 + r, device="cuda", dtype=torch.uint8))
+assert u.tolist() == sum(([7 + q] * 3 for q in range(w)), []), u.tolist()
+torch.cuda.synchronize()
+print("MESH_OK", r, w, flush=True)
+dist.destroy_process_group()
