@@ -195,6 +195,16 @@ def main():
             print(f"[bench] {e}", file=sys.stderr)
             replicas_ok = False
 
+    comm_probe = None
+    if world > 1 and os.environ.get("MI355X_DP_BENCH_COMM_PROBE", "1") == "1":
+        # after the timed region: the fabric's measured collective times, recorded with the result
+        # (feeds the bucket planner's alpha-beta model; all-reduce vs the balanced-shard RS + AG)
+        from mi355x_dp.parallel.ddp import probe_collectives
+        try:
+            comm_probe = probe_collectives(device=dev)
+        except Exception as e:  # never lose the measurement over the probe
+            comm_probe = f"failed: {type(e).__name__}: {e}"
+
     for i in range(args.profile_steps):
         step(10_000 + i)
     torch.cuda.synchronize()
@@ -238,6 +248,7 @@ def main():
             "warmup_s": round(t_w1 - t_w0, 2),
             "replicas_identical": replicas_ok,
             "comm_calibration": engine.calibration,
+            "comm_probe": comm_probe,
             "bucket_launch_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
         }
         print(json.dumps(out), flush=True)

@@ -135,6 +135,56 @@ def calibrate_allreduce(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32
     return alpha * 1e6, 1.0 / slope / 1e9
 
 
+def probe_collectives(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32.0, 128.0), iters=5, warmup=2):
+    """Measured collective times on the live group (fp32): all-reduce per size, and
+    reduce-scatter + all-gather (the balanced-shard pair) at each size >= 4 MB; ms per call and
+    ring bus bandwidth 2 (W-1)/W * S / t.  MAX over ranks.  Used by bench.py after its timed region
+    so every multi-GPU run records the fabric it ran on."""
+    import time
+    dev = device if device is not None else torch.device("cpu")
+    cuda = dev.type == "cuda"
+    world = dist.get_world_size(process_group)
+    rank = dist.get_rank(process_group)
+    buf = torch.zeros(int(max(sizes_mb) * 2**20) // 4, dtype=torch.float32, device=dev)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        if cuda:
+            torch.cuda.synchronize(dev)
+        dist.barrier(group=process_group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        if cuda:
+            torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / iters
+
+    rows = []
+    for mb in sizes_mb:
+        n = (int(mb * 2**20) // 4) // (world * 64) * (world * 64)
+        t = buf[:n]
+        ar = timed(lambda: dist.all_reduce(t, group=process_group))
+        rsag = None
+        if mb >= 4:
+            c = n // world
+            mine = t[rank * c:(rank + 1) * c]
+            rsag = timed(lambda: (dist.reduce_scatter_tensor(mine, t, group=process_group),
+                                  dist.all_gather_into_tensor(t, mine, group=process_group)))
+        rows.append([mb, ar, rsag if rsag is not None else -1.0])
+    v = torch.tensor(rows, dtype=torch.float64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=process_group)
+    out = []
+    for mb, ar, rsag in v.tolist():
+        nbytes = mb * 2**20
+        row = {"mb": mb, "allreduce_ms": round(ar * 1e3, 4),
+               "allreduce_busbw_GBps": round(2 * (world - 1) / world * nbytes / ar / 1e9, 1)}
+        if rsag > 0:
+            row["rs_plus_ag_ms"] = round(rsag * 1e3, 4)
+        out.append(row)
+    return out
+
+
 def calibrated_cap(alpha_us, bw_gbps, overhead=0.1, min_bytes=4 << 20, max_bytes=64 << 20):
     """bucket size whose all-reduce spends `overhead` of its time in the fixed latency alpha"""
     s = alpha_us * 1e-6 * (1.0 - overhead) / overhead * bw_gbps * 1e9

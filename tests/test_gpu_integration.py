@@ -350,6 +350,10 @@ def test_bench_two_ranks_torchrun_gloo():
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 64 and out["value"] > 0
     assert out["replicas_identical"] is True
+    probe = out["comm_probe"]  # post-timing fabric probe (gloo here: list of rows, or the failure text)
+    assert probe is not None
+    if isinstance(probe, list):
+        assert all(row["allreduce_ms"] > 0 for row in probe)
 
 
 @pytest.mark.skipif(REF_NB is None, reason="reference notebooks not staged (run build())")

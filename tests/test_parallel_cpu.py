@@ -755,3 +755,33 @@ def test_ddp_comm_hooks():
     assert [s[0] for s in seen] == list(range(nb)) * 3
     assert [s[1] for s in seen[:nb]] == [False] * (nb - 1) + [True]
     assert all(s[2] > 0 and s[3] for s in seen)
+
+
+def _worker_probe(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from mi355x_dp.parallel.ddp import probe_collectives
+        q.put((rank, probe_collectives(sizes_mb=(0.25, 4.0), iters=2, warmup=1)))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, e))
+        raise
+
+
+def test_probe_collectives_agrees_across_ranks():
+    """bench.py's post-timing fabric probe: all-reduce and RS+AG times, MAX over ranks (identical
+    on every rank), positive bus bandwidths."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_probe, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r, v in res.items():
+        assert not isinstance(v, Exception), f"rank {r}: {v!r}"
+    assert res[0] == res[1] and len(res[0]) == 2
+    assert res[0][0]["allreduce_busbw_GBps"] > 0 and "rs_plus_ag_ms" not in res[0][0]
+    assert res[0][1]["rs_plus_ag_ms"] > 0
