@@ -35,10 +35,16 @@ def train_models_batched(models: Sequence[torch.nn.Module], loaders: Sequence, e
     epochs = [epoch_num] * K if isinstance(epoch_num, int) else list(epoch_num)
     for m in models:
         m.train()
+    if any(isinstance(mod, torch.nn.RNNBase) for mod in models[0].modules()):
+        raise NotImplementedError("train_models_batched: recurrent models (no vmap batching rule for fused RNNs); "
+                                  "train them one at a time")
     base = copy.deepcopy(models[0])
     params, buffers = stack_module_state(list(models))
-    params = {k: v.detach().clone() for k, v in params.items()}
-    buffers = {k: v.detach().clone() for k, v in buffers.items()}
+    trainable = {k for k, p in models[0].named_parameters() if p.requires_grad}
+    # frozen parameters (the rtNLP model's embedding) ride with the buffers: never differentiated
+    buffers = {**{k: v.detach().clone() for k, v in buffers.items()},
+               **{k: v.detach().clone() for k, v in params.items() if k not in trainable}}
+    params = {k: v.detach().clone() for k, v in params.items() if k in trainable}
     exp_avg = {k: torch.zeros_like(v) for k, v in params.items()}
     exp_avg_sq = {k: torch.zeros_like(v) for k, v in params.items()}
     dev = next(iter(params.values())).device
@@ -101,7 +107,9 @@ def train_models_batched(models: Sequence[torch.nn.Module], loaders: Sequence, e
     with torch.no_grad():
         for i, m in enumerate(models):
             for k, p in m.named_parameters():
-                p.copy_(params[k][i])
+                if k in params:
+                    p.copy_(params[k][i])
             for k, b in m.named_buffers():
-                b.copy_(buffers[k][i])
+                if k in buffers:
+                    b.copy_(buffers[k][i])
     return list(models)

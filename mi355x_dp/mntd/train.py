@@ -123,6 +123,9 @@ def generate(task, kind, troj_type="M", shadow_prop=0.02, target_prop=0.5, shado
                                                                  need_pad=need_pad), batch_size=bs, shuffle=True,
                                                  generator=shuf)
         mine.append((name, model, loader, ep, atk))
+    if batched and mine and any(isinstance(mod, torch.nn.RNNBase) for mod in mine[0][1].modules()):
+        print("batched training: recurrent model (%s), training one model at a time" % type(mine[0][1]).__name__)
+        batched = False
     if batched and mine:
         from .batched import train_models_batched
         train_models_batched([m for _, m, _, _, _ in mine], [l for _, _, l, _, _ in mine], [e for *_, e, _ in mine],
