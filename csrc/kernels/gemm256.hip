@@ -27,6 +27,9 @@
 //    ds_read_b128 fragment reads spread over the banks;
 //  * XCD-aware, M-grouped tile order (GROUP_M 8) for L2 reuse of the B panel.
 #include "common.h"
+#ifndef MI_MASK_PROBE
+#define MI_MASK_PROBE 0  // timing probe (tools/gpu_call_maskprobe.sh)
+#endif
 #include <cstdio>
 #include <cstdlib>
 #ifndef MI_CONV_NTSTORE
@@ -398,8 +401,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         }
         if (ok[u] && a.epi >= 4) {
           if (a.epi == 5) cv[u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[u]) : make_uint4(0, 0, 0, 0);
+#if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
+          if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
+          if (a.bn_relu) yq[u] = xq[u];
+#else
           if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
           if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
+#endif
         } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
           yq[u] = acc_ok ? *(const uint4*)(a.aux + offs[u]) : make_uint4(0, 0, 0, 0);
         }
