@@ -136,8 +136,9 @@ def calibrate_allreduce(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32
 
 
 def probe_collectives(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32.0, 128.0), iters=5, warmup=2):
-    """Measured collective times on the live group (fp32): all-reduce per size, and
-    reduce-scatter + all-gather (the balanced-shard pair) at each size >= 4 MB; ms per call and
+    """Measured collective times on the live group (fp32): all-reduce per size, and at each size
+    >= 4 MB reduce-scatter + all-gather (the balanced-shard pair) and a bf16 all-reduce of the same
+    element count (grad_comm='bf16'); ms per call and
     ring bus bandwidth 2 (W-1)/W * S / t.  MAX over ranks.  Used by bench.py after its timed region
     so every multi-GPU run records the fabric it ran on."""
     import time
@@ -146,6 +147,7 @@ def probe_collectives(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32.0
     world = dist.get_world_size(process_group)
     rank = dist.get_rank(process_group)
     buf = torch.zeros(int(max(sizes_mb) * 2**20) // 4, dtype=torch.float32, device=dev)
+    buf16 = torch.zeros(buf.numel(), dtype=torch.bfloat16, device=dev)
 
     def timed(fn):
         for _ in range(warmup):
@@ -165,22 +167,26 @@ def probe_collectives(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32.0
         n = (int(mb * 2**20) // 4) // (world * 64) * (world * 64)
         t = buf[:n]
         ar = timed(lambda: dist.all_reduce(t, group=process_group))
-        rsag = None
+        rsag = ar16 = None
         if mb >= 4:
             c = n // world
             mine = t[rank * c:(rank + 1) * c]
             rsag = timed(lambda: (dist.reduce_scatter_tensor(mine, t, group=process_group),
                                   dist.all_gather_into_tensor(t, mine, group=process_group)))
-        rows.append([mb, ar, rsag if rsag is not None else -1.0])
+            t16 = buf16[:n]
+            ar16 = timed(lambda: dist.all_reduce(t16, group=process_group))  # grad_comm='bf16'
+        rows.append([mb, ar, rsag if rsag is not None else -1.0, ar16 if ar16 is not None else -1.0])
     v = torch.tensor(rows, dtype=torch.float64, device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=process_group)
     out = []
-    for mb, ar, rsag in v.tolist():
+    for mb, ar, rsag, ar16 in v.tolist():
         nbytes = mb * 2**20
         row = {"mb": mb, "allreduce_ms": round(ar * 1e3, 4),
                "allreduce_busbw_GBps": round(2 * (world - 1) / world * nbytes / ar / 1e9, 1)}
         if rsag > 0:
             row["rs_plus_ag_ms"] = round(rsag * 1e3, 4)
+        if ar16 > 0:
+            row["allreduce_bf16_same_elems_ms"] = round(ar16 * 1e3, 4)
         out.append(row)
     return out
 
