@@ -72,6 +72,9 @@ def main():
         # per process, 3+ processes oversubscribe the GPU's queue slots and the scheduler time-slices
         # them -- gloo's host-synchronised copies then crawl (profiles/multirank_rehearsal.md).
         # Must be set before the first HIP call (device_count() does not initialise HIP here).
+        from mi355x_dp.utils import hwqueues
+        if os.environ.get(hwqueues.AUTO_MARK) == "1":  # inherited from a one-rank-per-GPU parent
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
     else:
         # one rank per GPU: enough hardware queues that the compute, weight-gradient and comm

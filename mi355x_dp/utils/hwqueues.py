@@ -48,4 +48,8 @@ def ensure(n: int | None = None) -> int | None:
     if cur and cur.isdigit() and int(cur) >= want:
         return None
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+    os.environ[AUTO_MARK] = "1"  # child processes can tell our setting from a user's
     return min(want, 32)
+
+
+AUTO_MARK = "MI355X_DP_HW_QUEUES_AUTO"

@@ -216,9 +216,11 @@ def test_hw_queue_sizing(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     monkeypatch.delenv("MI355X_DP_HW_QUEUES", raising=False)
+    monkeypatch.setenv(hwqueues.AUTO_MARK, "0")  # restored after the test (ensure() sets it)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
     assert hwqueues.ensure() == 8 and os.environ["GPU_MAX_HW_QUEUES"] == "8"
+    assert os.environ[hwqueues.AUTO_MARK] == "1"
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
     assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "16"
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
