@@ -182,7 +182,7 @@ def probe_collectives(process_group=None, device=None, sizes_mb=(0.25, 4.0, 32.0
     for mb, ar, rsag, ar16 in v.tolist():
         nbytes = mb * 2**20
         row = {"mb": mb, "allreduce_ms": round(ar * 1e3, 4),
-               "allreduce_busbw_GBps": round(2 * (world - 1) / world * nbytes / ar / 1e9, 1)}
+               "allreduce_busbw_GBps": round(2 * (world - 1) / world * nbytes / ar / 1e9, 3)}
         if rsag > 0:
             row["rs_plus_ag_ms"] = round(rsag * 1e3, 4)
         if ar16 > 0:
