@@ -3,7 +3,16 @@
 whole job) on synthetic ImageNet-shaped data, 1..8 MI355X (BASELINE.json metric).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+        N>1 without a launcher: bench.py spawns the N ranks itself through the native
+        launcher (csrc/launch/launcher.cpp, the mpirun/smddprun replacement, reference
+        nb2:284 `mpirun -np 8 ... smddprun`) and relays rank 0's JSON line and the job's
+        exit code.  The parent makes no HIP call.
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+        (or any launcher that sets WORLD_SIZE / RANK / LOCAL_RANK): one rank per process.
+
+Every rank checks that the process group it joined really has --gpus ranks (exit 3 otherwise,
+never a world-1 number under an N-GPU label) and the JSON line reports ``ranks_seen`` and the
+collective backend (RCCL version for ``nccl``).
 
 Every timed step is a full training step through the framework's own engine:
 GPU input pipeline (uint8 -> random flip + normalize -> bf16 NHWC), forward
@@ -11,12 +20,17 @@ GPU input pipeline (uint8 -> random flip + normalize -> bf16 NHWC), forward
 cross-entropy, backward (dgrad/wgrad MFMA kernels, BN backward), bucketed
 gradient all-reduce over RCCL overlapped with backward, fused flat SGD
 (momentum 0.9, weight decay 1e-4).  Weak scaling: fixed per-GPU batch.
+
+``--device cpu`` runs the same distributed code path (bucket planner, C++ reducer, gloo
+collectives, comm probe, replica check) on CPU ranks -- a rehearsal of the world-8 path for
+tests on machines without a GPU; its numbers are not GPU measurements.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -25,9 +39,10 @@ sys.path.insert(0, ROOT)
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
+EXIT_WORLD_MISMATCH = 3
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -37,7 +52,10 @@ def parse():
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--num-classes", type=int, default=1000)
     p.add_argument("--lr", type=float, default=0.01)  # reference hyperparameter (nb2:110)
-    p.add_argument("--backend", default=os.environ.get("MI355X_DP_BACKEND", "nccl"))
+    p.add_argument("--backend", default=os.environ.get("MI355X_DP_BACKEND"),
+                   help="collective backend (default: nccl = RCCL on cuda, gloo on cpu)")
+    p.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                   help="cpu: rehearse the distributed path on CPU ranks (tests; not a GPU number)")
     p.add_argument("--bucket-mb", type=float, default=None)
     p.add_argument("--force-comm", action="store_true",
                    help="create the process group and issue every bucket collective even at N=1 "
@@ -54,47 +72,141 @@ def parse():
     p.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (rocprof)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as one captured HIP graph (launch-bound small-batch configs)")
-    return p.parse_args()
+    p.add_argument("--launcher", default=os.environ.get("MI355X_DP_BENCH_LAUNCHER", "native"),
+                   choices=("native", "torchrun"), help="how --gpus N > 1 spawns its ranks without WORLD_SIZE")
+    a = p.parse_args(argv)
+    if a.backend is None:
+        a.backend = "nccl" if a.device == "cuda" else "gloo"
+    return a
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------------ self-spawn (parent process)
+def spawn_ranks(args, argv) -> int:
+    """Run this script as ``args.gpus`` ranks on this node and relay the result.
+
+    The parent never initialises HIP (``torch.cuda.device_count`` does not on this stack; no other
+    torch.cuda call is made).  Child stdout lines that parse as the result JSON are printed on this
+    process's stdout (exactly one, from rank 0); every other line goes to stderr.  Returns the job
+    exit code: the first failing rank's (the native launcher aborts the others), 0 otherwise."""
+    n = args.gpus
+    if args.device == "cuda":
+        try:
+            import torch
+            ngpu = torch.cuda.device_count()
+        except Exception:
+            ngpu = 0
+        if ngpu == 0:
+            print("[bench] --gpus N > 1 needs GPUs (or --device cpu for a CPU rehearsal)", file=sys.stderr)
+            return 2
+        if n > ngpu and args.backend == "nccl":
+            print(f"[bench] --gpus {n} > {ngpu} visible GPUs: RCCL needs one device per rank "
+                  f"(use --backend gloo to rehearse {n} ranks sharing the GPUs)", file=sys.stderr)
+            return 2
+    from mi355x_dp.launch import NATIVE_LAUNCHER, compat_pythonpath, free_port
+    port = int(os.environ.get("MASTER_PORT") or free_port())
+    script = [sys.executable, os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env["PYTHONUNBUFFERED"] = "1"  # rank output relayed line by line
+    env["PYTHONPATH"] = compat_pythonpath(env.get("PYTHONPATH"))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["MI355X_DP_BENCH_SPAWNED"] = args.launcher
+    if args.launcher == "native" and os.path.exists(NATIVE_LAUNCHER):
+        cmd = [NATIVE_LAUNCHER, "--nproc", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+               "--"] + script
+    else:
+        env["MI355X_DP_BENCH_SPAWNED"] = "torchrun"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr=127.0.0.1", f"--master-port={port}"] + script[1:]
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    results = 0
+    for line in proc.stdout:
+        if _is_result(line):
+            results += 1
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and results != 1:
+        print(f"[bench] ranks exited 0 but {results} result lines were printed", file=sys.stderr)
+        return 1
+    return rc
+
+
+def _is_result(line: str) -> bool:
+    s = line.strip()
+    if not (s.startswith("{") and '"metric"' in s):
+        return False
+    try:
+        return "value" in json.loads(s)
+    except ValueError:
+        return False
+
+
+def _backend_info(dist, backend: str):
+    """(backend name as the process group reports it, collective library version)"""
+    name = str(dist.get_backend())
+    lib = None
+    if name == "nccl":
+        try:
+            import torch
+            v = torch.cuda.nccl.version()
+            lib = "RCCL " + (".".join(str(x) for x in v) if isinstance(v, tuple) else str(v))
+        except Exception:
+            lib = "RCCL"
+    elif name == "gloo":
+        lib = "gloo"
+    else:
+        lib = name
+    return name, lib
+
+
+# --------------------------------------------------------------------------------- rank process
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, argv))
     if os.environ.get("MI355X_DP_BENCH_STACKS"):  # hang diagnosis: every rank dumps its Python stacks
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["MI355X_DP_BENCH_STACKS"]), repeat=True, file=sys.stderr)
     if args.graph and args.warmup < 2:
         args.warmup = 2  # the graph is captured during warmup, never inside the timed region
-    import torch
-    import torch.distributed as dist
-
-    if int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(1, torch.cuda.device_count()):
-        # ranks share GPUs (multi-rank rehearsal on a small box): with the default 4 hardware queues
-        # per process, 3+ processes oversubscribe the GPU's queue slots and the scheduler time-slices
-        # them -- gloo's host-synchronised copies then crawl (profiles/multirank_rehearsal.md).
-        # Must be set before the first HIP call (device_count() does not initialise HIP here).
-        from mi355x_dp.utils import hwqueues
-        if os.environ.get(hwqueues.AUTO_MARK) == "1":  # inherited from a one-rank-per-GPU parent
-            os.environ.pop("GPU_MAX_HW_QUEUES", None)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
-    else:
-        # one rank per GPU: enough hardware queues that the compute, weight-gradient and comm
-        # streams never share one (mi355x_dp/utils/hwqueues.py: 10.6k -> 12.6k img/s with a
-        # process group on one MI355X)
-        from mi355x_dp.utils import hwqueues
-        hwqueues.ensure()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if rank == 0:
-            print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    # one rank per GPU; more ranks than GPUs share them (gloo rehearsal of the multi-rank path on a
-    # 1-GPU box -- RCCL itself refuses two ranks on one device)
-    gpu = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
+        # never report a number for a world the caller did not ask for
+        print(f"[bench] rank {rank}: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks; "
+              "refusing to run", file=sys.stderr)
+        sys.exit(EXIT_WORLD_MISMATCH)
+    cuda = args.device == "cuda"
+
+    import torch
+    import torch.distributed as dist
+
+    if cuda:
+        # hardware queues per process, sized before the first HIP call (utils/hwqueues.py): one
+        # rank per GPU gets enough queues that the compute, weight-gradient and comm streams never
+        # share one; ranks sharing a GPU (multi-rank rehearsal) get one each
+        from mi355x_dp.utils import hwqueues
+        hwqueues.ensure()
+        # one rank per GPU; more ranks than GPUs share them (gloo rehearsal of the multi-rank path on
+        # a 1-GPU box -- RCCL itself refuses two ranks on one device)
+        gpu = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
+    else:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, int(os.environ.get("MI355X_DP_BENCH_CPU_THREADS", "1"))))
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
     use_pg = world > 1 or args.force_comm
+    ranks_seen, backend_name, comm_lib = 1, "none", None
     if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
@@ -112,6 +224,11 @@ def main():
             pg_options.is_high_priority_stream = True
         dist.init_process_group(backend=args.backend, device_id=dev if args.backend == "nccl" else None,
                                 pg_options=pg_options)
+        ranks_seen = dist.get_world_size()
+        backend_name, comm_lib = _backend_info(dist, args.backend)
+        if ranks_seen != args.gpus and not (args.force_comm and args.gpus == 1 and ranks_seen == 1):
+            print(f"[bench] rank {rank}: process group has {ranks_seen} ranks, --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(EXIT_WORLD_MISMATCH)
 
     from mi355x_dp.models import get_model
     from mi355x_dp.ops import augment, cross_entropy
@@ -139,7 +256,8 @@ def main():
     labels = torch.randint(0, args.num_classes, (B,), dtype=torch.int64, device=dev, generator=g)
 
     pad = 4 if S <= 64 else 0  # CIFAR-style random crop for small images (reference transforms)
-    x_static = torch.empty((B, 8, S, S), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+    x_static = (torch.empty((B, 8, S, S), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+                if cuda else None)
 
     def core():
         engine.zero_grad()
@@ -152,7 +270,10 @@ def main():
     graphed = None
 
     def step(i):
-        nonlocal graphed
+        nonlocal graphed, x_static
+        if not cuda:  # CPU rehearsal: the op library's ATen fallback returns a fresh fp32 NCHW batch
+            x_static = augment(images, 3, IMAGENET_MEAN, IMAGENET_STD, pad=pad, flip=True, seed=i)
+            return core()
         augment(images, 8, IMAGENET_MEAN, IMAGENET_STD, pad=pad, flip=True, seed=i, out=x_static)  # 3 ch + 5 zero
         if args.graph and i >= 1:  # capture after one eager step (optimizer first-step semantics)
             if graphed is None:
@@ -164,22 +285,22 @@ def main():
     # MI355X_DP_MAIN_PRIORITY=-1: the training step's compute stream at high priority (its
     # workgroups dispatched ahead of the weight-gradient side stream's)
     main_prio = int(os.environ.get("MI355X_DP_MAIN_PRIORITY", "0"))
-    if main_prio:
+    if main_prio and cuda:
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=main_prio))
     t_w0 = time.time()
     for i in range(args.warmup):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     first_loss = float(loss.detach()) if args.warmup else float("nan")
     t_w1 = time.time()
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(args.warmup + i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -203,14 +324,15 @@ def main():
         # after the timed region: the fabric's measured collective times, recorded with the result
         # (feeds the bucket planner's alpha-beta model; all-reduce vs the balanced-shard RS + AG)
         from mi355x_dp.parallel.ddp import probe_collectives
+        sizes = tuple(float(s) for s in os.environ.get("MI355X_DP_BENCH_PROBE_MB", "0.25,4,32,128").split(","))
         try:
-            comm_probe = probe_collectives(device=dev)
+            comm_probe = probe_collectives(device=dev, sizes_mb=sizes)
         except Exception as e:  # never lose the measurement over the probe
             comm_probe = f"failed: {type(e).__name__}: {e}"
 
     for i in range(args.profile_steps):
         step(10_000 + i)
-    torch.cuda.synchronize()
+    sync()
 
     total_images = world * B * args.steps
     value = total_images / elapsed
@@ -221,15 +343,16 @@ def main():
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic (random uint8 ImageNet-shaped images, random labels; GPU flip+normalize pipeline; "
-                    "random-init weights)",
+                    "random-init weights)" + ("" if cuda else "; CPU REHEARSAL, not a GPU measurement"),
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
@@ -237,14 +360,18 @@ def main():
                 "image_size": S,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
-                "optimizer": "SGD(momentum=0.9, wd=1e-4), fp32 master weights, bf16 compute",
-                "backend": args.backend if use_pg else "none",
+                "optimizer": "SGD(momentum=0.9, wd=1e-4), fp32 master weights, " + ("bf16 compute" if cuda else "fp32 compute"),
+                "backend": backend_name,
+                "comm_library": comm_lib,
+                "launcher": os.environ.get("MI355X_DP_BENCH_SPAWNED", "external" if world > 1 else "none"),
+                "device": args.device,
                 "comm_forced_at_world1": bool(args.force_comm and world == 1),
                 "buckets": len(engine.buckets),
                 "grad_comm": args.grad_comm,
                 "shard_optimizer": bool(args.shard_optimizer),
                 "wgrad_stream": bool(args.wgrad_stream),
                 "hip_graph": bool(args.graph),
+                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             },
             "loss_first_warmup": round(first_loss, 4),
             "loss_last": round(last_loss, 4),

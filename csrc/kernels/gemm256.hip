@@ -680,7 +680,6 @@ struct TailWs {
 };
 constexpr int TAIL_WS_STREAMS = 4;
 static TailWs g_tail_ws[16][TAIL_WS_STREAMS];
-static int g_tail_evict[16];
 static std::mutex g_tail_mu;
 static int g_num_cus = 0;
 static int g_tail_split_env = -1;
@@ -717,11 +716,9 @@ static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
     if (!wp)
       for (auto& e : g_tail_ws[dev & 15])
         if (!e.used) { e.used = true; e.st = st; wp = &e; break; }
-    if (!wp) {
-      wp = &g_tail_ws[dev & 15][g_tail_evict[dev & 15]++ % TAIL_WS_STREAMS];
-      hipDeviceSynchronize();  // its previous owner may still have partials in flight
-      wp->st = st;
-    }
+    // table full: no tail split for this stream (a valid schedule that needs no workspace; never a
+    // host-blocking takeover of another stream's slot, which would abort a graph capture)
+    if (!wp) split = 1;
   }
   a.full_blocks = split > 1 ? full : tiles;
   a.tail_split = split;

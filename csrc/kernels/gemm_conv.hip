@@ -1062,19 +1062,23 @@ hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
 // Split-K slab workspace of the TN kernels (fp32, grown on demand and reused in stream order).  One
 // per device for every stream, plus one for the device's registered weight-gradient side stream
 // (mi_register_wgrad_stream): side-stream weight gradients run concurrently with compute-stream
-// TN work and must not share slabs with it.  Contract: the first call that needs a given size
+// TN work and must not share slabs with it; likewise the residual blocks' auxiliary (shortcut)
+// stream (mi_register_aux_stream), whose shortcut weight gradient can run concurrently with
+// compute-stream TN work when the weight-gradient stream is off.  Contract: the first call that needs a given size
 // allocates (hipMalloc) -- it must not run inside a HIP graph capture; GraphedStep's eager warm-up
 // step makes every allocation first (capture streams use the shared slot, like the warm-up).
 // MI355X_DP_TN_SLABS=0 selects the fp32-atomic split-K path instead.
 struct SplitkWs { float* p = nullptr; size_t n = 0; };
-static SplitkWs g_splitk_ws[16][2];
+static SplitkWs g_splitk_ws[16][3];  // [device][0: any other stream, 1: wgrad stream, 2: aux stream]
 static hipStream_t g_wgrad_stream[16];
+static hipStream_t g_aux_stream[16];
 static std::mutex g_splitk_mu;
 static float* splitk_workspace(size_t floats, hipStream_t st) {
   int dev = 0;
   hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_splitk_mu);
-  SplitkWs& w = g_splitk_ws[dev & 15][st != nullptr && st == g_wgrad_stream[dev & 15] ? 1 : 0];
+  const int slot = st == nullptr ? 0 : st == g_wgrad_stream[dev & 15] ? 1 : st == g_aux_stream[dev & 15] ? 2 : 0;
+  SplitkWs& w = g_splitk_ws[dev & 15][slot];
   if (w.n < floats) {
     const size_t n = std::max(floats, (size_t)16 << 20);  // >= 64 MB: every RN50 / RN152 wgrad fits
     float* p = nullptr;
@@ -1166,6 +1170,15 @@ MI_API int mi_register_wgrad_stream(hipStream_t st) {
   hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_splitk_mu);
   g_wgrad_stream[dev & 15] = st;
+  return 0;
+}
+
+// The current device's auxiliary (projection-shortcut) stream: its own split-K slab workspace.
+MI_API int mi_register_aux_stream(hipStream_t st) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_splitk_mu);
+  g_aux_stream[dev & 15] = st;
   return 0;
 }
 

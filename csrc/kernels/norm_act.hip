@@ -871,7 +871,8 @@ inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const f
 // stream) gets its own slot of a table allocated up front by mi_bn_init_counters() (called when
 // the library is loaded -- never lazily, which would break a HIP graph capture).  A stream beyond
 // the table, or a device that was never initialised, takes the two-launch split + finalize path,
-// which needs no counters (same results, deterministic either way).
+// which needs no counters (deterministic either way; the two paths may round differently in the last
+// bit, so every rank of a job must use the same streams -- which the engine guarantees).
 constexpr int FIN_STREAM_SLOTS = 16, FIN_GROUPS = 128;  // 128 x 64 = 8192 channels
 struct FinCounters {
   int* cnt = nullptr;  // [FIN_STREAM_SLOTS][FIN_GROUPS]
@@ -879,7 +880,6 @@ struct FinCounters {
   bool used[FIN_STREAM_SLOTS] = {};
 };
 static FinCounters g_fin_cnt[16];
-static int g_fin_evict[16];
 static std::mutex g_fin_mu;
 
 static int* fin_counters(int groups, hipStream_t st) {
@@ -897,13 +897,8 @@ static int* fin_counters(int groups, hipStream_t st) {
       w.owner[i] = st;
       return w.cnt + i * FIN_GROUPS;
     }
-  // table full (streams come and go): take over a slot round-robin once its owner's finalizes
-  // have drained, so the one-launch path -- and its reduction order -- never depends on how many
-  // streams the process used before (never inside a capture: the warm-up claimed the slot)
-  const int i = g_fin_evict[dev & 15]++ % FIN_STREAM_SLOTS;
-  hipDeviceSynchronize();
-  w.owner[i] = st;
-  return w.cnt + i * FIN_GROUPS;
+  // table full: the counter-free two-launch path (no host synchronisation, safe inside a capture)
+  return nullptr;
 }
 
 // finalize a [nblk][2][C] partial slab: one launch (finalize, or split + finalize for tall slabs)

@@ -69,6 +69,12 @@ def _aux_stream(dev):
     s = _AUX_STREAMS.get(dev.index)
     if s is None:
         s = _AUX_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+        # its own split-K slab workspace: with the weight-gradient stream off, the shortcut's weight
+        # gradient on this stream runs concurrently with the compute stream's split-K TN kernels
+        from . import _lib
+        import ctypes
+        with torch.cuda.device(dev):
+            _lib.call("mi_register_aux_stream", ctypes.c_void_p(s.cuda_stream))
     return s
 
 

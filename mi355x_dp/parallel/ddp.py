@@ -344,6 +344,9 @@ class DataParallel(nn.Module):
         if wgrad_stream and self.flat.grad.is_cuda:
             from mi355x_dp.ops.functional import WgradStream
             self.wgrad_stream = WgradStream(self.flat.grad.device)
+            from mi355x_dp.utils import hwqueues
+            self.hw_queue_warning = hwqueues.check(
+                self.comm_on, True, shared_gpu=hwqueues.ranks_per_node() > torch.cuda.device_count())
         for i, p in enumerate(self.flat.params):
             cb = functools.partial(self._ready_native, i) if self.reducer is not None \
                 else self._make_ready_cb(i)
@@ -728,13 +731,30 @@ class FlatSGD:
         sd = {"steps": self.steps, "param_groups": self.param_groups,
               "momentum_buf": self.momentum_buf.detach().cpu() if self.momentum_buf is not None else None}
         if self.engine.sharded:
-            sd["shard"] = {"rank": self.engine.rank, "world": self.engine.world_size}
+            sd["shard"] = self._shard_meta()
         return sd
 
+    def _shard_meta(self):
+        """Which slice of the packed momentum belongs to which flat range: the bucket plan (flat
+        [lo, hi) of every bucket and of this rank's shard of it) depends on the planner settings
+        and, with calibrate=True, on timing -- a resume must see the same plan."""
+        e = self.engine
+        return {"rank": e.rank, "world": e.world_size, "numel": int(e.flat.numel),
+                "bucket_ranges": [[int(lo), int(hi)] for lo, hi in e.bucket_ranges],
+                "shard_ranges": [[int(lo), int(hi)] for lo, hi in e.shard_ranges]}
+
     def load_state_dict(self, sd):
-        if self.engine.sharded and sd.get("shard") != {"rank": self.engine.rank, "world": self.engine.world_size}:
-            raise ValueError(f"optimizer shard {sd.get('shard')} does not match this rank "
-                             f"({self.engine.rank} of {self.engine.world_size})")
+        if self.engine.sharded:
+            want, got = self._shard_meta(), sd.get("shard") or {}
+            if {k: got.get(k) for k in ("rank", "world")} != {"rank": want["rank"], "world": want["world"]}:
+                raise ValueError(f"optimizer shard (rank {got.get('rank')} of {got.get('world')}) does not match "
+                                 f"this rank ({want['rank']} of {want['world']})")
+            for k in ("numel", "bucket_ranges", "shard_ranges"):
+                if got.get(k) != want[k]:
+                    raise ValueError(f"optimizer shard checkpoint was written with a different bucket plan ({k} "
+                                     "differs): its packed momentum would pair with the wrong parameters; resume "
+                                     "with the same bucket_cap_mb / first / last / min bucket settings and without "
+                                     "calibrate=True")
         self.steps = sd["steps"]
         self.param_groups = sd["param_groups"]
         if sd.get("momentum_buf") is not None and self.momentum_buf is not None:

@@ -9,17 +9,32 @@ kernels queued behind it on the same hardware queue.  Measured on one MI355X, Re
 with a process group (``bench.py --force-comm``): 10.6k img/s at 4 queues, 12.64k at 6 or 8,
 12.7k without a process group (``profiles/hw_queues.md``).  That is every N > 1 run.
 
-``ensure(n)`` raises the limit to ``n`` before the HIP runtime starts, but only when each GPU
-hosts at most one rank: ranks sharing a GPU keep few queues (4 processes x 4 queues already
-over-subscribed the scheduler, profiles/multirank_rehearsal.md).  ``MI355X_DP_HW_QUEUES=0``
+``ensure(n)`` raises the limit to ``n`` before the HIP runtime starts when each GPU hosts at most
+one rank.  Ranks sharing a GPU (multi-rank rehearsals on a small box) get ``SHARED`` queues each
+instead: 4 processes x 4 queues already over-subscribed the scheduler
+(profiles/multirank_rehearsal.md), so an 8 inherited from a one-rank-per-GPU parent (marked by
+``AUTO_MARK``) is dropped.  A value the user set is never touched; ``MI355X_DP_HW_QUEUES=0``
 leaves the variable alone.  Must run before the first HIP call of the process; counting
 devices does not initialise HIP on this stack.
+
+``check(...)`` is called when an engine is built: a process group plus the weight-gradient stream
+on fewer than ``MIN_OK`` queues prints one warning (the 17 % cliff is otherwise silent, e.g. when a
+user script touched ``torch.cuda`` before importing the framework).
 """
 from __future__ import annotations
 
 import os
+import sys
 
 DEFAULT = 8
+SHARED = 1
+MIN_OK = 6
+HIP_DEFAULT = 4
+AUTO_MARK = "MI355X_DP_HW_QUEUES_AUTO"
+
+# GPU_MAX_HW_QUEUES as it stood when ensure() found HIP already running (None: ensure() ran first)
+_late_value = None
+_warned = False
 
 
 def ranks_per_node() -> int:
@@ -32,19 +47,32 @@ def ranks_per_node() -> int:
 
 def ensure(n: int | None = None) -> int | None:
     """Returns the value set, or None when the variable was left alone."""
+    global _late_value
     want = int(os.environ.get("MI355X_DP_HW_QUEUES", str(DEFAULT if n is None else n)))
     if want <= 0:
         return None
     try:
         import torch
         if torch.cuda.is_initialized():
+            if _late_value is None:
+                _late_value = os.environ.get("GPU_MAX_HW_QUEUES", "")
             return None
         devices = torch.cuda.device_count()
     except Exception:
         return None
-    if devices == 0 or ranks_per_node() > devices:
+    if devices == 0:
         return None
     cur = os.environ.get("GPU_MAX_HW_QUEUES")
+    if ranks_per_node() > devices:
+        if os.environ.get(AUTO_MARK) == "1":  # inherited from a one-rank-per-GPU parent, not the user's
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
+            os.environ.pop(AUTO_MARK, None)
+            cur = None
+        if cur:
+            return None
+        os.environ["GPU_MAX_HW_QUEUES"] = str(SHARED)
+        os.environ[AUTO_MARK] = "1"
+        return SHARED
     if cur and cur.isdigit() and int(cur) >= want:
         return None
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
@@ -52,4 +80,26 @@ def ensure(n: int | None = None) -> int | None:
     return min(want, 32)
 
 
-AUTO_MARK = "MI355X_DP_HW_QUEUES_AUTO"
+def effective() -> int:
+    """Hardware queues this process's HIP runtime is using (best knowledge: the value in the
+    environment when HIP started, if ensure() saw HIP already running; else the current one)."""
+    v = _late_value if _late_value is not None else os.environ.get("GPU_MAX_HW_QUEUES", "")
+    return int(v) if v and v.isdigit() else HIP_DEFAULT
+
+
+def check(process_group: bool, side_stream: bool, shared_gpu: bool = False, stream=sys.stderr) -> bool:
+    """Warn (once per process) when a process group and the weight-gradient stream run on fewer
+    than MIN_OK hardware queues.  Returns True when the warning condition holds."""
+    global _warned
+    if not (process_group and side_stream) or shared_gpu:
+        return False
+    q = effective()
+    if q >= MIN_OK:
+        return False
+    if not _warned:
+        _warned = True
+        print(f"[mi355x_dp] warning: {q} hardware queues per process (GPU_MAX_HW_QUEUES) for a process group "
+              f"plus the weight-gradient stream; expect ~17% slower steps (profiles/hw_queues.md).  Import "
+              f"mi355x_dp.parallel before the first torch.cuda call, or export GPU_MAX_HW_QUEUES={DEFAULT}.",
+              file=stream, flush=True)
+    return True

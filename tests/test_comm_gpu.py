@@ -221,9 +221,11 @@ def test_wgrad_stream_vit_layers():
 
 def test_shortcut_aux_stream_bitwise():
     """The projection shortcut on its own stream (ops/resblock.py DS_STREAM), forward and backward,
-    with the weight-gradient stream on: gradients, running statistics and the next forward's loss
-    are bit-identical to the single-stream schedule (apart from the atomically summed stem / fc
-    gradients), and the stream-order checker sees no late bucket write."""
+    with the weight-gradient stream on AND off: gradients, running statistics and the next forward's
+    loss are bit-identical to the single-stream schedule (apart from the atomically summed stem / fc
+    gradients), and the stream-order checker sees no late bucket write.  With the weight-gradient
+    stream off the shortcut's split-K weight gradient runs on the aux stream concurrently with the
+    compute stream's -- it must use its own slab workspace (mi_register_aux_stream)."""
     sys.path.insert(0, ROOT)
     from mi355x_dp.models import resnet50
     from mi355x_dp.ops import cross_entropy, resblock
@@ -235,12 +237,14 @@ def test_shortcut_aux_stream_bitwise():
     res = {}
     old = resblock.DS_STREAM
     try:
-        for aux, check in ((False, False), (True, False), (True, True)):
+        for aux, check, wgs in ((False, False, True), (True, False, True), (True, True, True),
+                                (False, False, False), (True, False, False)):
             resblock.DS_STREAM = aux
             torch.manual_seed(0)
             m = resnet50().to(dev)
             names = {id(p): n for n, p in m.named_parameters()}
-            e = DataParallel(m, bucket_cap_mb=8, first_bucket_mb=1, min_bucket_mb=0, check_stream_order=check)
+            e = DataParallel(m, bucket_cap_mb=8, first_bucket_mb=1, min_bucket_mb=0, check_stream_order=check,
+                             wgrad_stream=wgs)
             for _ in range(2):
                 e.zero_grad()
                 loss = cross_entropy(e(x), y)
@@ -250,18 +254,20 @@ def test_shortcut_aux_stream_bitwise():
             assert e.order_violations == []
             if aux:
                 assert resblock._AUX_STREAMS
-            res[(aux, check)] = (float(loss), e.flat.grad.clone(),
-                                 torch.cat([b.float().flatten() for b in m.buffers()]))
+            res[(aux, check, wgs)] = (float(loss), e.flat.grad.clone(),
+                                      torch.cat([b.float().flatten() for b in m.buffers()]))
     finally:
         resblock.DS_STREAM = old
     spans = [(names[id(p)], int(o), int(o) + p.numel()) for p, o in zip(e.flat.params, e.flat.offsets)]
     atomic = lambda n: n == "conv1.weight" or n.startswith("fc.")  # noqa: E731
-    l0, g0, b0 = res[(False, False)]
-    l1, g1, b1 = res[(True, False)]
-    assert l0 == l1 and torch.equal(b0, b1)
-    diff = [n for n, lo, hi in spans if not torch.equal(g0[lo:hi], g1[lo:hi])]
-    assert all(atomic(n) for n in diff), diff
-    g2 = res[(True, True)][1]
+    for wgs in (True, False):
+        l0, g0, b0 = res[(False, False, wgs)]
+        l1, g1, b1 = res[(True, False, wgs)]
+        assert l0 == l1 and torch.equal(b0, b1)
+        diff = [n for n, lo, hi in spans if not torch.equal(g0[lo:hi], g1[lo:hi])]
+        assert all(atomic(n) for n in diff), (wgs, diff)
+    g0 = res[(False, False, True)][1]
+    g2 = res[(True, True, True)][1]
     assert float((g2 - g0).norm() / g0.norm()) < 1e-5
 
 

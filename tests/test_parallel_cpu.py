@@ -559,7 +559,9 @@ def test_balanced_shard_optimizer_matches_allreduce(world):
     numel, ranges = nat[0][4], nat[0][5]
     assert all((hi - lo) % (64 * world) == 0 for lo, hi in ranges) and len(ranges) > 1
     assert nat[0][3] * world == numel  # packed momentum: this rank's shards only
-    assert [nat[r][6] for r in range(world)] == [{"rank": r, "world": world} for r in range(world)]
+    assert [{k: nat[r][6][k] for k in ("rank", "world")} for r in range(world)] == \
+        [{"rank": r, "world": world} for r in range(world)]
+    assert all(nat[r][6]["bucket_ranges"] == nat[0][6]["bucket_ranges"] for r in range(world))
     # one reduce-scatter + one all-gather per bucket per step
     assert nat[0][2] == pyr[0][2] == 3 * 2 * len(ranges)
 
@@ -785,3 +787,25 @@ def test_probe_collectives_agrees_across_ranks():
     assert res[0] == res[1] and len(res[0]) == 2
     assert res[0][0]["allreduce_ms"] > 0 and res[0][0]["allreduce_busbw_GBps"] >= 0 and "rs_plus_ag_ms" not in res[0][0]
     assert res[0][1]["rs_plus_ag_ms"] > 0 and res[0][1]["allreduce_bf16_same_elems_ms"] > 0
+
+
+def test_shard_checkpoint_rejects_a_different_bucket_plan():
+    """A balanced-shard optimizer checkpoint records the bucket plan its packed momentum was laid out
+    for; loading it into an engine planned differently (other bucket caps) raises instead of pairing
+    momentum with the wrong parameters -- even when the packed lengths happen to agree."""
+    from mi355x_dp.parallel import DataParallel, FlatSGD
+    e1 = DataParallel(_model(), shard_optimizer=True, bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0)
+    o1 = FlatSGD(e1, lr=0.1, momentum=0.9)
+    x, y = _data()
+    torch.nn.functional.cross_entropy(e1(x), y).backward()
+    o1.step()
+    sd = o1.state_dict()
+    assert sd["shard"]["bucket_ranges"] == [list(r) for r in e1.bucket_ranges]
+    same = DataParallel(_model(), shard_optimizer=True, bucket_cap_mb=0.05, first_bucket_mb=0.01, min_bucket_mb=0)
+    o_same = FlatSGD(same, lr=0.1, momentum=0.9)
+    o_same.load_state_dict(sd)
+    assert torch.equal(o_same.momentum_buf, o1.momentum_buf)
+    other = DataParallel(_model(), shard_optimizer=True, bucket_cap_mb=0.2, first_bucket_mb=0.05, min_bucket_mb=0)
+    assert len(other.buckets) != len(e1.buckets)
+    with pytest.raises(ValueError, match="bucket plan"):
+        FlatSGD(other, lr=0.1, momentum=0.9).load_state_dict(sd)

@@ -224,8 +224,18 @@ def test_hw_queue_sizing(monkeypatch):
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
     assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "16"
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv(hwqueues.AUTO_MARK, "0")  # a user's value
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "16")  # two ranks per GPU
     assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    # ranks sharing GPUs that inherited the automatic 8 of a one-rank-per-GPU parent: dropped to 1
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    monkeypatch.setenv(hwqueues.AUTO_MARK, "1")
+    assert hwqueues.ensure() == hwqueues.SHARED and os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    monkeypatch.setenv(hwqueues.AUTO_MARK, "0")
+    assert hwqueues.ensure() == hwqueues.SHARED and os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv(hwqueues.AUTO_MARK, "0")
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     monkeypatch.setenv("MI355X_DP_HW_QUEUES", "0")
     assert hwqueues.ensure() is None
@@ -235,6 +245,31 @@ def test_hw_queue_sizing(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
     assert hwqueues.ensure() is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
+
+
+def test_hw_queue_warning(monkeypatch):
+    """hwqueues.check: one warning when a process group and the weight-gradient stream run on fewer
+    than 6 hardware queues (including HIP's default of 4 when the variable is unset, and the value
+    that was in force when HIP started before ensure() could raise it); silent otherwise."""
+    import io
+    from mi355x_dp.utils import hwqueues
+    monkeypatch.setattr(hwqueues, "_warned", False)
+    monkeypatch.setattr(hwqueues, "_late_value", None)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    s = io.StringIO()
+    assert not hwqueues.check(True, True, stream=s) and s.getvalue() == ""
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    assert hwqueues.effective() == 4
+    assert not hwqueues.check(False, True, stream=s)  # no process group: no comm stream
+    assert not hwqueues.check(True, False, stream=s)  # single-stream backward
+    assert not hwqueues.check(True, True, shared_gpu=True, stream=s)  # rehearsal ranks keep 1 queue
+    assert hwqueues.check(True, True, stream=s) and "4 hardware queues" in s.getvalue()
+    n = len(s.getvalue())
+    assert hwqueues.check(True, True, stream=s) and len(s.getvalue()) == n  # warned once
+    # HIP started at 4 before ensure(): raising the variable afterwards does not count
+    monkeypatch.setattr(hwqueues, "_late_value", "4")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    assert hwqueues.effective() == 4 and hwqueues.check(True, True, stream=s)
 
 
 def test_checkpoint_roundtrip(tmp_path):
