@@ -336,6 +336,15 @@ def main(argv=None):
 
     total_images = world * B * args.steps
     value = total_images / elapsed
+    if use_pg:
+        dist.destroy_process_group()
+        use_pg = False
+    ipc_probe = None
+    if (rank == 0 and world > 1 and cuda and world <= torch.cuda.device_count()
+            and os.environ.get("MI355X_DP_BENCH_IPC_PROBE", "1") == "1"):
+        # after the timed region, as its own job: the native smddp backend's IPC one-/two-shot
+        # all-reduce against RCCL per size on this fabric, and the per-size path choice it implies
+        ipc_probe = run_ipc_probe(world)
     if rank == 0:
         out = {
             "metric": "images/sec (whole node) ResNet-50 DDP" if args.model == "resnet50"
@@ -379,11 +388,34 @@ def main(argv=None):
             "replicas_identical": replicas_ok,
             "comm_calibration": engine.calibration,
             "comm_probe": comm_probe,
+            "ipc_probe": ipc_probe,
             "bucket_launch_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
         }
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.destroy_process_group()
+
+
+def run_ipc_probe(world: int, timeout_s: int = 180):
+    """The smddp IPC-vs-RCCL path table of this node (tools/ipc_probe.py), as a separate N-rank job
+    started by rank 0 after the benchmark finished: a probe failure cannot cost the measurement."""
+    from mi355x_dp.launch import NATIVE_LAUNCHER, compat_pythonpath, free_port
+    if not os.path.exists(NATIVE_LAUNCHER):
+        return "skipped: native launcher not built"
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_PORT",
+                        "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS")}
+    env["PYTHONPATH"] = compat_pythonpath(env.get("PYTHONPATH"))
+    cmd = [NATIVE_LAUNCHER, "--nproc", str(world), "--master-addr", "127.0.0.1", "--master-port",
+           str(free_port()), "--", sys.executable, os.path.join(ROOT, "tools", "ipc_probe.py")]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return f"failed: timeout after {timeout_s} s"
+    for line in r.stdout.splitlines():
+        if line.startswith('{"ipc_probe"'):
+            return json.loads(line)["ipc_probe"]
+    return f"failed: rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}"
 
 
 if __name__ == "__main__":

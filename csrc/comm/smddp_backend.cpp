@@ -47,11 +47,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <pybind11/chrono.h>
+#include <pybind11/stl.h>
 
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <deque>
+#include <map>
 #include <memory>
 #include <dlfcn.h>
 #include <execinfo.h>
@@ -214,9 +216,12 @@ class SmddpBackend : public c10d::Backend {
     if (comm_) ncclCommDestroy(comm_);
     if (ipc_on_) {
       hipDeviceSynchronize();
-      for (int q = 0; q < size_; ++q)
+      for (int q = 0; q < size_; ++q) {
         if (q != rank_ && ipc_base_[q]) hipIpcCloseMemHandle(ipc_base_[q]);
+        if (q != rank_ && ipc_flags_[q]) hipIpcCloseMemHandle(ipc_flags_[q]);
+      }
       if (ipc_base_[rank_]) hipFree(ipc_base_[rank_]);
+      if (ipc_flags_[rank_]) hipFree(ipc_flags_[rank_]);
       if (ipc_err_) hipHostFree(ipc_err_);
     }
   }
@@ -246,14 +251,15 @@ class SmddpBackend : public c10d::Backend {
   }
 
  private:
-  using IpcFn = int (*)(const float* const*, uint32_t* const*, int, int, float*, int64_t, uint32_t, float, int*,
-                        uint32_t, hipStream_t);
-  using Ipc1Fn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int, int, int, uint32_t, int*,
-                         uint32_t, hipStream_t);
-  using IpcRsFn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int, float, uint32_t, int*,
-                          uint32_t, hipStream_t);
-  using IpcAgFn = int (*)(const void* const*, uint32_t* const*, int, int, void*, int64_t, int64_t, uint32_t, int*,
-                          uint32_t, hipStream_t);
+  // csrc/kernels/ipc_allreduce.hip: every kernel copies its input into this rank's slot itself
+  using IpcFn = int (*)(const float* const*, uint32_t* const*, int, int, const float*, float*, int64_t, uint32_t,
+                        float, int*, uint32_t, hipStream_t);
+  using Ipc1Fn = int (*)(const void* const*, uint32_t* const*, int, int, const void*, void*, int64_t, int, int, int,
+                         uint32_t, int*, uint32_t, hipStream_t);
+  using IpcRsFn = int (*)(const void* const*, uint32_t* const*, int, int, const void*, int64_t, void*, int64_t, int,
+                          float, uint32_t, int*, uint32_t, hipStream_t);
+  using IpcAgFn = int (*)(const void* const*, uint32_t* const*, int, int, const void*, void*, int64_t, int64_t,
+                          uint32_t, int*, uint32_t, hipStream_t);
 
   void setup_ipc() {
     const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
@@ -270,25 +276,44 @@ class SmddpBackend : public c10d::Backend {
     }
     if (const char* c = std::getenv("MI355X_DP_SMDDP_IPC_MB")) ipc_cap_ = (size_t)(atof(c) * (1 << 20));
     ipc_cap_ = (ipc_cap_ + 255) & ~(size_t)255;
+    ipc_threshold_ = ipc_cap_;
     if (const char* c = std::getenv("MI355X_DP_SMDDP_IPC_ONESHOT_KB")) ipc_oneshot_bytes_ = (size_t)(atof(c) * 1024);
-    const size_t bytes = 2 * ipc_cap_ + (size_t)flag_bytes();
+    // data slots: coarse-grained device memory (the bandwidth path); flags: a separate fine-grained
+    // uncached allocation, so flag stores / polls never hit a stale line of another XCD's L2 or of
+    // a peer GPU's cache (MI355X_DP_SMDDP_IPC_FLAGS=coarse keeps them in plain hipMalloc memory)
     void* mine = nullptr;
-    HIPCHECK(hipMalloc(&mine, bytes));
-    HIPCHECK(hipMemset(mine, 0, bytes));
+    HIPCHECK(hipMalloc(&mine, 2 * ipc_cap_));
+    HIPCHECK(hipMemset(mine, 0, 2 * ipc_cap_));
+    const size_t fbytes = (size_t)flag_bytes();
+    void* fl = nullptr;
+    const char* fmode = std::getenv("MI355X_DP_SMDDP_IPC_FLAGS");
+    flags_kind_ = "coarse";
+    if (!(fmode && std::string(fmode) == "coarse")) {
+      if (hipExtMallocWithFlags(&fl, fbytes, hipDeviceMallocUncached) == hipSuccess) flags_kind_ = "uncached";
+      else if (hipExtMallocWithFlags(&fl, fbytes, hipDeviceMallocFinegrained) == hipSuccess) flags_kind_ = "finegrained";
+      else fl = nullptr;
+      (void)hipGetLastError();
+    }
+    if (!fl) HIPCHECK(hipMalloc(&fl, fbytes));
+    HIPCHECK(hipMemset(fl, 0, fbytes));
     HIPCHECK(hipDeviceSynchronize());
-    hipIpcMemHandle_t hnd;
-    HIPCHECK(hipIpcGetMemHandle(&hnd, mine));
+    hipIpcMemHandle_t hnd[2];
+    HIPCHECK(hipIpcGetMemHandle(&hnd[0], mine));
+    HIPCHECK(hipIpcGetMemHandle(&hnd[1], fl));
     store_->set("smddp/ipc/" + std::to_string(rank_),
-                std::vector<uint8_t>((uint8_t*)&hnd, (uint8_t*)&hnd + sizeof(hnd)));
+                std::vector<uint8_t>((uint8_t*)hnd, (uint8_t*)hnd + sizeof(hnd)));
     ipc_base_.assign(size_, nullptr);
+    ipc_flags_.assign(size_, nullptr);
     ipc_base_[rank_] = mine;
+    ipc_flags_[rank_] = fl;
     for (int q = 0; q < size_; ++q) {
       if (q == rank_) continue;
       auto v = store_->get("smddp/ipc/" + std::to_string(q));
-      TORCH_CHECK(v.size() == sizeof(hipIpcMemHandle_t), "smddp: bad IPC handle from rank ", q);
-      hipIpcMemHandle_t ph;
-      memcpy(&ph, v.data(), sizeof(ph));
-      HIPCHECK(hipIpcOpenMemHandle(&ipc_base_[q], ph, hipIpcMemLazyEnablePeerAccess));
+      TORCH_CHECK(v.size() == sizeof(hnd), "smddp: bad IPC handles from rank ", q);
+      hipIpcMemHandle_t ph[2];
+      memcpy(ph, v.data(), sizeof(ph));
+      HIPCHECK(hipIpcOpenMemHandle(&ipc_base_[q], ph[0], hipIpcMemLazyEnablePeerAccess));
+      HIPCHECK(hipIpcOpenMemHandle(&ipc_flags_[q], ph[1], hipIpcMemLazyEnablePeerAccess));
     }
     // peers' flag waits are bounded spins (never a hang): long enough to absorb the host-side skew
     // between ranks (start-up, Python), MI355X_DP_SMDDP_IPC_SPIN overrides the count (x s_sleep 8)
@@ -307,7 +332,8 @@ class SmddpBackend : public c10d::Backend {
   bool ipc_eligible(const std::vector<at::Tensor>& ts, const c10d::AllreduceOptions& opts) const {
     if (!ipc_on_ || ts.size() != 1) return false;
     const auto& t = ts[0];
-    return t.scalar_type() == at::kFloat && t.is_contiguous() && (ipc_only_ || (size_t)t.numel() * 4 <= ipc_cap_) &&
+    return t.scalar_type() == at::kFloat && t.is_contiguous() &&
+           (ipc_only_ || (size_t)t.numel() * 4 <= ipc_threshold_) &&
            (opts.reduceOp == c10d::ReduceOp::SUM || opts.reduceOp == c10d::ReduceOp::AVG);
   }
 
@@ -316,7 +342,7 @@ class SmddpBackend : public c10d::Backend {
     const size_t slot = (epoch & 1) * ipc_cap_;
     for (int q = 0; q < size_; ++q) {
       data[q] = (const char*)ipc_base_[q] + slot;
-      flags[q] = (uint32_t*)((char*)ipc_base_[q] + 2 * ipc_cap_);
+      flags[q] = (uint32_t*)ipc_flags_[q];
     }
   }
 
@@ -332,13 +358,12 @@ class SmddpBackend : public c10d::Backend {
       uint32_t* flags[8];
       ipc_slots(epoch, data, flags);
       float* src = (float*)t.data_ptr() + off;
-      if (cnt > 0) HIPCHECK(hipMemcpyAsync((void*)data[rank_], src, cnt * 4, hipMemcpyDeviceToDevice, s));
       IpcFn fn = (size_t)cnt * 4 <= ipc_oneshot_bytes_ ? ipc_fn_ : ipc2_fn_;
       if (ipc_trace_)
         fprintf(stderr, "[smddp ipc] rank %d epoch %u allreduce%s f32 n=%lld\n", rank_, epoch,
                 fn == ipc_fn_ ? "1" : "2", (long long)cnt);
-      const int rc = fn((const float* const*)data, flags, rank_, size_, src, cnt, epoch, avg ? 1.f / size_ : 1.f,
-                        ipc_err_dev_, ipc_spin_limit_, s);
+      const int rc = fn((const float* const*)data, flags, rank_, size_, src, src, std::max<int64_t>(cnt, 0), epoch,
+                        avg ? 1.f / size_ : 1.f, ipc_err_dev_, ipc_spin_limit_, s);
       TORCH_CHECK(rc == 0, "smddp: IPC all-reduce launch failed with hipError ", rc);
       if (n == 0) break;
     }
@@ -358,9 +383,7 @@ class SmddpBackend : public c10d::Backend {
       if (ipc_trace_)
         fprintf(stderr, "[smddp ipc] rank %d epoch %u generic op=%d dtype=%d root=%d bytes=%lld\n", rank_, epoch, op,
                 dtype, root, (long long)cnt);
-      if (cnt > 0 && (op != 3 || rank_ == root))
-        HIPCHECK(hipMemcpyAsync((void*)data[rank_], p, cnt, hipMemcpyDeviceToDevice, s));
-      const int rc = ipc1_fn_(data, flags, rank_, size_, p, std::max<int64_t>(cnt, 0), dtype, op, root, epoch,
+      const int rc = ipc1_fn_(data, flags, rank_, size_, p, p, std::max<int64_t>(cnt, 0), dtype, op, root, epoch,
                               ipc_err_dev_, ipc_spin_limit_, s);
       TORCH_CHECK(rc == 0, "smddp: IPC collective launch failed with hipError ", rc);
       if (nbytes == 0) break;
@@ -381,14 +404,12 @@ class SmddpBackend : public c10d::Backend {
       const void* data[8];
       uint32_t* flags[8];
       ipc_slots(epoch, data, flags);
-      if (cnt > 0)
-        HIPCHECK(hipMemcpy2DAsync((void*)data[rank_], cnt * esz, (const char*)in.data_ptr() + off * esz, S * esz,
-                                  cnt * esz, size_, hipMemcpyDeviceToDevice, s));
       if (ipc_trace_)
         fprintf(stderr, "[smddp ipc] rank %d epoch %u reduce_scatter dtype=%d n=%lld\n", rank_, epoch, dt,
                 (long long)cnt);
-      const int rc = ipc_rs_fn_(data, flags, rank_, size_, (char*)out.data_ptr() + off * esz, std::max<int64_t>(cnt, 0),
-                                dt, avg ? 1.f / size_ : 1.f, epoch, ipc_err_dev_, ipc_spin_limit_, s);
+      const int rc = ipc_rs_fn_(data, flags, rank_, size_, (const char*)in.data_ptr() + off * esz, S,
+                                (char*)out.data_ptr() + off * esz, std::max<int64_t>(cnt, 0), dt,
+                                avg ? 1.f / size_ : 1.f, epoch, ipc_err_dev_, ipc_spin_limit_, s);
       TORCH_CHECK(rc == 0, "smddp: IPC reduce-scatter launch failed with hipError ", rc);
       if (S == 0) break;
     }
@@ -404,12 +425,10 @@ class SmddpBackend : public c10d::Backend {
       const void* data[8];
       uint32_t* flags[8];
       ipc_slots(epoch, data, flags);
-      if (cnt > 0)
-        HIPCHECK(hipMemcpyAsync((void*)data[rank_], (const char*)in.data_ptr() + off, cnt, hipMemcpyDeviceToDevice, s));
       if (ipc_trace_)
         fprintf(stderr, "[smddp ipc] rank %d epoch %u all_gather bytes=%lld\n", rank_, epoch, (long long)cnt);
-      const int rc = ipc_ag_fn_(data, flags, rank_, size_, (char*)out.data_ptr() + off, std::max<int64_t>(cnt, 0), nb,
-                                epoch, ipc_err_dev_, ipc_spin_limit_, s);
+      const int rc = ipc_ag_fn_(data, flags, rank_, size_, (const char*)in.data_ptr() + off, (char*)out.data_ptr() + off,
+                                std::max<int64_t>(cnt, 0), nb, epoch, ipc_err_dev_, ipc_spin_limit_, s);
       TORCH_CHECK(rc == 0, "smddp: IPC all-gather launch failed with hipError ", rc);
       if (nb == 0) break;
     }
@@ -684,6 +703,17 @@ class SmddpBackend : public c10d::Backend {
   // MI355X_DP_SMDDP_ABORT_ON_ERROR=0), so isSuccess()/wait() behaviour can be checked
   void inject_error(int code, const std::string& what) { fail(code, what); }
   bool healthy() const { return err_->code.load() == 0; }
+  std::map<std::string, int64_t> ipc_info() const {
+    return {{"on", ipc_on_ ? 1 : 0}, {"only", ipc_only_ ? 1 : 0}, {"cap_bytes", (int64_t)ipc_cap_},
+            {"oneshot_bytes", (int64_t)ipc_oneshot_bytes_}, {"threshold_bytes", (int64_t)ipc_threshold_},
+            {"flags_uncached", std::string(flags_kind_) == "uncached" ? 1 : 0},
+            {"flags_finegrained", std::string(flags_kind_) == "finegrained" ? 1 : 0}};
+  }
+  // every rank must set the same values (the path of a collective must agree across ranks)
+  void set_ipc_paths(int64_t threshold_bytes, int64_t oneshot_bytes) {
+    if (threshold_bytes >= 0) ipc_threshold_ = (size_t)threshold_bytes;
+    if (oneshot_bytes >= 0) ipc_oneshot_bytes_ = (size_t)oneshot_bytes;
+  }
   int64_t comm_stream_handle() const { return (int64_t)(intptr_t)comm_stream_.stream(); }
 
  private:
@@ -728,7 +758,13 @@ class SmddpBackend : public c10d::Backend {
   IpcAgFn ipc_ag_fn_ = nullptr;
   size_t ipc_cap_ = 4u << 20;
   size_t ipc_oneshot_bytes_ = 256u << 10;  // MI355X_DP_SMDDP_IPC_ONESHOT_KB
+  // fp32 SUM/AVG all-reduces up to this many bytes take the IPC path (slot-sized chunks above the
+  // slot), larger ones RCCL; default: the slot size; set at run time from a measured probe table
+  // (set_ipc_threshold, mi355x_dp.parallel.comm_paths)
+  size_t ipc_threshold_ = 0;
   std::vector<void*> ipc_base_;
+  std::vector<void*> ipc_flags_;
+  const char* flags_kind_ = "none";
   int* ipc_err_ = nullptr;      // host-mapped: the watchdog reads it without a device sync
   int* ipc_err_dev_ = nullptr;
   uint32_t ipc_epoch_ = 0;
@@ -786,6 +822,12 @@ bool healthy(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->h
 
 int64_t comm_stream(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->comm_stream_handle(); }
 
+std::map<std::string, int64_t> ipc_info(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->ipc_info(); }
+
+void set_ipc_paths(const c10::intrusive_ptr<c10d::Backend>& b, int64_t threshold_bytes, int64_t oneshot_bytes) {
+  as_smddp(b)->set_ipc_paths(threshold_bytes, oneshot_bytes);
+}
+
 int rccl_version() {
   int v = 0;
   ncclGetVersion(&v);
@@ -802,4 +844,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("inject_error", &smddp::inject_error, pybind11::arg("backend"), pybind11::arg("code"), pybind11::arg("what"));
   m.def("healthy", &smddp::healthy, pybind11::arg("backend"));
   m.def("comm_stream", &smddp::comm_stream, pybind11::arg("backend"));
+  m.def("ipc_info", &smddp::ipc_info, pybind11::arg("backend"));
+  m.def("set_ipc_paths", &smddp::set_ipc_paths, pybind11::arg("backend"), pybind11::arg("threshold_bytes"),
+        pybind11::arg("oneshot_bytes"));
 }

@@ -234,13 +234,21 @@ class DataParallel(nn.Module):
                  wgrad_stream: bool = WGRAD_STREAM, calibrate: bool = CALIBRATE,
                  shard_optimizer: bool = SHARD_OPTIMIZER, device_ids=None, output_device=None, dim: int = 0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 static_graph: bool = False):
+                 static_graph: bool = False, foreign_optimizer: bool = False):
         """The trailing keyword arguments are torch DDP's (and SMDDP v1's), accepted so the
         engine is a drop-in ``DistributedDataParallel``: ``device_ids`` / ``output_device`` must
         name the module's own device (one process per GPU), ``dim`` must be 0 (batch-dim data
         parallelism); ``find_unused_parameters`` is implied (a bucket whose parameters got no
         gradient is still reduced at the end of backward), gradients are always bucket views, and
-        ``static_graph`` needs no special path (the bucket order is fixed)."""
+        ``static_graph`` needs no special path (the bucket order is fixed).
+
+        ``foreign_optimizer=True`` is torch DDP's contract for an optimizer the engine does not own
+        (stock ``optim.SGD`` over ``engine.parameters()``, what the reference scripts use,
+        gpu.py:156-158): gradients are averaged over the ranks when ``backward()`` returns (a final
+        autograd callback joins the bucket collectives and scales by 1/world); a ``zero_grad`` that
+        set the gradients to None re-points them at the flat buffer (zeroed) at the next forward;
+        and parameters changed in place since the last forward refresh the bf16 compute copy and
+        the transposed data-gradient operands first.  Shard mode needs FlatSGD, so it is refused."""
         super().__init__()
         if dim != 0:
             raise ValueError("DataParallel: only batch-dimension (dim=0) data parallelism")
@@ -251,6 +259,10 @@ class DataParallel(nn.Module):
                     d.index not in (None, mod_dev.index):
                 raise ValueError(f"DataParallel: device {d} is not the module's device {mod_dev} "
                                  "(one process per GPU)")
+        if foreign_optimizer and shard_optimizer:
+            raise ValueError("DataParallel: shard_optimizer=True needs FlatSGD (foreign_optimizer=True refused)")
+        self.foreign_optimizer = bool(foreign_optimizer)
+        self._final_cb_pending = False
         self.require_backward_grad_sync = True
         self.module = module
         self.process_group = process_group
@@ -267,7 +279,10 @@ class DataParallel(nn.Module):
         params = [p for p in module.parameters() if p.requires_grad]
         params = list(reversed(params))  # approximate backward order
         from mi355x_dp.models.layers import Conv2d as _NativeConv
-        kernel_ids = {id(m.weight) for m in module.modules() if isinstance(m, _NativeConv)}
+        # conv weights in the native kernels' [K][R][S][C] layout -- only where those kernels run (on
+        # host tensors the stock convolutions then see torch's own layout and round identically)
+        on_gpu = any(p.is_cuda for p in params)
+        kernel_ids = {id(m.weight) for m in module.modules() if isinstance(m, _NativeConv)} if on_gpu else set()
         self.buffers = FlatBuffers(list(module.buffers()))
 
         from . import _reducer_native
@@ -364,6 +379,7 @@ class DataParallel(nn.Module):
         # a state_dict loaded into the wrapped model (checkpoint resume) writes the fp32 masters in
         # place; the bf16 compute copy and the transposed dgrad copies follow it
         module.register_load_state_dict_post_hook(lambda _m, _keys: self.flat.refresh_bf16())
+        self._params_version = self.flat.params_version()
         self._reset()
 
     @property
@@ -581,12 +597,48 @@ class DataParallel(nn.Module):
         self._gather_pending = False
         self.flat.refresh_bf16()
 
+    def _foreign_prepare(self):
+        """foreign_optimizer mode, before a forward: gradients set to None by the user's
+        zero_grad are re-pointed at the (zeroed) flat buffer; parameters the user's optimizer
+        changed refresh the bf16 / transposed compute copies."""
+        v = self.flat.params_version()
+        if v != self._params_version:
+            self.flat.refresh_bf16()  # + transposed dgrad operands
+            self._params_version = v
+        if torch.is_grad_enabled() and self.flat.reattach_grads():
+            self.flat.zero_grad()
+
+    def _final_callback(self):
+        self._final_cb_pending = False
+        self.finish_gradient_sync(average=True)
+
+    def _arm_final_callback(self, out):
+        """torch DDP's end-of-backward contract: the first gradient that reaches this forward's
+        output queues an autograd final callback that joins every bucket collective and averages,
+        so ``p.grad`` holds the all-reduced mean when ``backward()`` returns."""
+        t = out
+        while isinstance(t, (tuple, list)) and t:
+            t = t[0]
+        if not (isinstance(t, torch.Tensor) and t.requires_grad):
+            return
+
+        def hook(g):
+            if not self._final_cb_pending:
+                self._final_cb_pending = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._final_callback)
+            return g
+        t.register_hook(hook)
+
     def forward(self, *args, **kwargs):
         self._join_side()  # a backward whose sync was skipped (no_sync / accumulation) left side work
+        if self.foreign_optimizer:
+            self._foreign_prepare()
         self._reset()
         self.wait_param_sync()
         self._wait_buffer_sync()
         out = self.module(*args, **kwargs)
+        if self.foreign_optimizer and torch.is_grad_enabled():
+            self._arm_final_callback(out)
         if self.broadcast_buffers and self.buffers.buffers and self.module.training:
             # torch DDP broadcasts rank 0's buffers synchronously BEFORE every training forward
             # (SURVEY.md X4), on the critical path.  Same values, off the critical path: broadcast
@@ -646,6 +698,8 @@ class DataParallel(nn.Module):
 
     @property
     def grad_scale(self) -> float:
+        if self.foreign_optimizer:
+            return 1.0  # the end-of-backward callback already averaged
         return 1.0 if self._comm_hook is not None and self.comm_on else 1.0 / self.world_size
 
     def zero_grad(self, set_to_none: bool = False):

@@ -143,11 +143,25 @@ class FlatParams:
             cast_bf16_(self.data, self.bf16)
             self.refresh_transposed()
 
-    def reattach_grads(self):
-        """Re-point .grad at the flat views (after user code set them to None)."""
-        for p, o, kl in zip(self.params, self.offsets, self.kernel_layout):
-            if p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr():
-                p.grad = _kernel_view(self.grad, o, tuple(p.shape), kl)
+    def reattach_grads(self) -> bool:
+        """Re-point .grad at the flat views (after user code set them to None, e.g. a stock
+        optimizer's ``zero_grad(set_to_none=True)``).  Returns True if any was re-pointed."""
+        views = getattr(self, "_grad_views", None)
+        if views is None:
+            views = self._grad_views = [_kernel_view(self.grad, o, tuple(p.shape), kl)
+                                        for p, o, kl in zip(self.params, self.offsets, self.kernel_layout)]
+        changed = False
+        for p, v in zip(self.params, views):
+            g = p.grad
+            if g is None or g.data_ptr() != v.data_ptr():
+                p.grad = v
+                changed = True
+        return changed
+
+    def params_version(self) -> int:
+        """Sum of the parameters' autograd version counters: changes whenever anything (a stock
+        optimizer's step, an in-place update) writes a parameter in place."""
+        return sum(p._version for p in self.params)
 
 
 class FlatBuffers:

@@ -94,6 +94,53 @@ def test_reference_gpu_script_unmodified(tmp_path):
     assert sum(v.numel() for k, v in sd.items() if "running" not in k and "num_batches" not in k) == 11689512
 
 
+def _run_reference_script(tmp_path, tag, engine, batch=32, epochs=1):
+    """the unmodified reference GPU script, directly, with the env a one-rank job would set"""
+    from mi355x_dp.data.cifar import write_synthetic_cifar10
+    data = tmp_path / "data"
+    if not data.exists():
+        write_synthetic_cifar10(str(data), n_train=1024, n_test=256)
+    model_dir = tmp_path / f"model_{tag}"
+    model_dir.mkdir()
+    env = {**os.environ, "SM_HOSTS": '["algo-1"]', "SM_CURRENT_HOST": "algo-1", "SM_MODEL_DIR": str(model_dir),
+           "SM_CHANNEL_TRAIN": str(data), "LOCAL_RANK": "0", "RANK": "0", "WORLD_SIZE": "1",
+           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(29600 + int(engine)),
+           "PYTHONPATH": ROOT + os.pathsep + os.path.join(ROOT, "compat"), "MI355X_DP_ENGINE_DDP": str(int(engine))}
+    code = ("import runpy, sys, torch\n"
+            "orig = torch.nn.parallel.DistributedDataParallel\n"
+            f"sys.argv = [{os.path.join(REF_CODE, 'cifar10-distributed-smddp-gpu.py')!r}, '--backend', 'smddp', "
+            f"'--batch-size', '{batch}', '--epochs', '{epochs}', '--lr', '0.01', '--model-type', 'resnet18', "
+            "'--momentum', '0.9']\n"
+            "import smdistributed.dataparallel.torch.torch_smddp\n"
+            "print('DDP_CLASS', torch.nn.parallel.DistributedDataParallel.__module__)\n"
+            "runpy.run_path(sys.argv[0], run_name='__main__')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=tmp_path, capture_output=True, text=True, timeout=600,
+                       env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    return r.stdout, torch.load(model_dir / "model.pth", map_location="cpu", weights_only=True)
+
+
+@pytest.mark.skipif(REF_CODE is None, reason="reference scripts not staged")
+def test_reference_script_engine_ddp_matches_stock_ddp(tmp_path):
+    """SURVEY §7.1 decision 2(b): with the torch_smddp shim the unmodified script's
+    torch.nn.parallel.DistributedDataParallel(model) is the flat-buffer engine (gradients written
+    by the backward kernels into one buffer, no DDP copy-in/out, bf16 copies refreshed once per
+    step) driven by the script's own stock optim.SGD.  One epoch at the reference's per-rank batch
+    (32) gives the same model.pth -- keys, layout, values -- as torch's stock DDP."""
+    out_e, sd_e = _run_reference_script(tmp_path, "engine", True)
+    out_s, sd_s = _run_reference_script(tmp_path, "stock", False)
+    assert "mi355x_dp.parallel.engine_ddp" in out_e and "Test set: Average loss:" in out_e
+    assert list(sd_e) == list(sd_s) and list(sd_e)[0] == "module.conv1.weight"
+    assert all(v.is_contiguous() for v in sd_e.values())
+    for k in sd_s:
+        a, b = sd_e[k].double(), sd_s[k].double()
+        if k.endswith("num_batches_tracked"):
+            assert torch.equal(a, b), k
+            continue
+        err = float((a - b).norm() / b.norm().clamp_min(1e-12))
+        assert err < 2e-2, (k, err)  # 32 steps through bf16 kernels; different fp32 summation orders
+
+
 def test_two_ranks_one_gpu_gloo(tmp_path):
     """Multi-rank GPU engine path without a second GPU: 2 ranks share cuda:0 over gloo (CUDA
     tensors), exercising DataParallel + native reducer bucket launches + FlatSGD on device;

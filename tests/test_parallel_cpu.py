@@ -142,10 +142,16 @@ def test_flat_params_layout_and_state_dict():
     for k, v in ref.items():
         assert torch.equal(sd["module." + k], v)
         assert sd["module." + k].is_contiguous()
-    # conv weights live in the flat buffer in [K][R][S][C] (channels_last) order
+    # on host tensors the engine keeps torch's layout (stock CPU convolutions round the same); the
+    # native kernels' [K][R][S][C] (channels_last) order is used for GPU engines / kernel_layout_ids
     w = m.layer1[0].conv1.weight
-    assert w.is_contiguous(memory_format=torch.channels_last)
+    assert w.is_contiguous()
     assert w.data_ptr() >= e.flat.data.data_ptr()
+    from mi355x_dp.parallel.flat import FlatParams
+    m2 = resnet18()
+    FlatParams(list(m2.parameters()), bf16_copy=False, kernel_layout_ids={id(m2.layer1[0].conv1.weight)})
+    assert m2.layer1[0].conv1.weight.is_contiguous(memory_format=torch.channels_last)
+    assert m2.layer1[0].conv2.weight.is_contiguous()
     assert w.grad is not None and w.grad.data_ptr() >= e.flat.grad.data_ptr()
 
 
@@ -809,3 +815,99 @@ def test_shard_checkpoint_rejects_a_different_bucket_plan():
     assert len(other.buckets) != len(e1.buckets)
     with pytest.raises(ValueError, match="bucket plan"):
         FlatSGD(other, lr=0.1, momentum=0.9).load_state_dict(sd)
+
+
+def _worker_engine_ddp(rank, world, port, q, use_engine):
+    try:
+        os.environ["MI355X_DP_ENGINE_DDP"] = "force" if use_engine else "0"
+        _init(rank, world, port)
+        from mi355x_dp.models import resnet18
+        from mi355x_dp.parallel import engine_ddp
+        engine_ddp.install()
+        torch.manual_seed(0)
+        model = resnet18(num_classes=10)
+        # the reference's own calls (gpu.py:148, 156-168): stock class name, stock SGD, zero_grad
+        ddp = torch.nn.parallel.DistributedDataParallel(model)
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
+        crit = torch.nn.CrossEntropyLoss()
+        g = torch.Generator().manual_seed(7)
+        x, y = torch.randn(8, 3, 32, 32, generator=g), torch.randint(0, 10, (8,), generator=g)
+        part = slice(rank * 4, (rank + 1) * 4)
+        grads = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = crit(ddp(x[part]), y[part])
+            loss.backward()
+            grads.append(next(ddp.parameters()).grad.detach().clone())  # averaged when backward returns
+            opt.step()
+        ddp.eval()
+        with torch.no_grad():
+            ev = ddp(x[:2])
+        sd = {k: v.detach().clone().numpy() for k, v in ddp.state_dict().items()}
+        q.put((rank, type(ddp).__name__, sd, [g.numpy() for g in grads], ev.numpy()))
+        dist.destroy_process_group()
+        engine_ddp.uninstall()
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, e, None, None, None))
+
+
+def test_engine_ddp_substitution_matches_stock_ddp():
+    """The torch_smddp shim's engine-backed DistributedDataParallel (SURVEY §7.1 decision 2(b)):
+    the reference's unmodified call sequence -- stock class name, stock optim.SGD with
+    zero_grad(set_to_none), backward, step, eval forward, state_dict -- gives the same averaged
+    gradients, parameters, BN buffers and module.-prefixed keys as torch's own DDP, on gloo world 2."""
+    res = {}
+    for use_engine in (True, False):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _port()
+        ps = [ctx.Process(target=_worker_engine_ddp, args=(r, 2, port, q, use_engine)) for r in range(2)]
+        for p in ps:
+            p.start()
+        out = {r: rest for r, *rest in [q.get(timeout=240) for _ in ps]}
+        for p in ps:
+            p.join(60)
+        for r, (name, *_rest) in out.items():
+            assert not isinstance(name, Exception), f"rank {r}: {name!r}"
+        res[use_engine] = out
+    assert res[True][0][0] == "DataParallel" and res[False][0][0] == "DistributedDataParallel"
+    import numpy as np
+    sd_e, sd_s = res[True][0][1], res[False][0][1]
+    assert list(sd_e) == list(sd_s) and all(k.startswith("module.") for k in sd_e)
+    # on host tensors the engine keeps torch's weight layout, so the math is the same op for op
+    rel = lambda a, b: np.linalg.norm((a.astype(np.float64) - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-12)  # noqa
+    for k in sd_s:
+        if sd_s[k].dtype.kind == "f":
+            assert rel(sd_e[k], sd_s[k].astype(np.float64)) < 1e-6, k
+        else:
+            assert np.array_equal(sd_e[k], sd_s[k]), k
+    for ge, gs in zip(res[True][0][2], res[False][0][2]):
+        assert rel(ge, gs.astype(np.float64)) < 1e-6
+    assert rel(res[True][0][3], res[False][0][3].astype(np.float64)) < 1e-6
+    # replicas identical on the engine path
+    for k in sd_e:
+        assert np.array_equal(res[True][0][1][k], res[True][1][1][k]), k
+
+
+def test_comm_path_choice_from_probe_table():
+    """smddp per-size path selection (parallel/comm_paths.py): IPC below the size where RCCL starts
+    to win, one-shot below the size where the two-shot starts to win; unmeasured paths never
+    chosen; a margin keeps near-ties on RCCL."""
+    from mi355x_dp.parallel.comm_paths import choose_paths
+    MB = 2**20
+    rows = [
+        {"bytes": MB // 4, "rccl": 0.060, "ipc_oneshot": 0.020, "ipc_twoshot": 0.030},
+        {"bytes": 1 * MB, "rccl": 0.080, "ipc_oneshot": 0.050, "ipc_twoshot": 0.045},
+        {"bytes": 4 * MB, "rccl": 0.110, "ipc_oneshot": 0.200, "ipc_twoshot": 0.090},
+        {"bytes": 16 * MB, "rccl": 0.250, "ipc_oneshot": 0.800, "ipc_twoshot": 0.260},
+        {"bytes": 32 * MB, "rccl": 0.420, "ipc_oneshot": 1.600, "ipc_twoshot": 0.400},
+    ]
+    assert choose_paths(rows) == (4 * MB, MB // 4)  # 16 MB: RCCL wins, so 32 MB stays RCCL too
+    assert choose_paths(list(reversed(rows))) == (4 * MB, MB // 4)  # order-independent
+    assert choose_paths(rows, margin=0.25) == (MB, MB // 4)  # 4 MB: 0.09 * 1.25 > 0.11
+    # IPC not measured (or failed): RCCL everywhere
+    assert choose_paths([{"bytes": MB, "rccl": 0.1, "ipc_oneshot": -1.0, "ipc_twoshot": None}]) == (0, 0)
+    # RCCL not measured: IPC wins wherever it ran
+    assert choose_paths([{"bytes": MB, "ipc_oneshot": 0.1, "ipc_twoshot": 0.2}]) == (MB, MB)

@@ -40,6 +40,24 @@ for S in (1, 1000, 300_001):
 u = torch.empty(w * 3, device="cuda", dtype=torch.uint8)
 dist.all_gather_into_tensor(u, torch.full((3,), 7 + r, device="cuda", dtype=torch.uint8))
 assert u.tolist() == sum(([7 + q] * 3 for q in range(w)), []), u.tolist()
+# broadcast and MAX (the generic one-shot), then the per-size path probe (IPC one-shot vs two-shot;
+# an IPC-only backend has no RCCL to compare with) and the flag memory kind
+b = torch.full((1001,), float(r), device="cuda")
+dist.broadcast(b, w - 1)
+assert float(b.min()) == w - 1 and float(b.max()) == w - 1
+m = torch.tensor([float(r)], device="cuda", dtype=torch.float64)
+dist.all_reduce(m, op=dist.ReduceOp.MAX)
+assert float(m) == w - 1
+from mi355x_dp.parallel import comm_paths  # noqa: E402
+info = comm_paths.ipc_info()
+assert info["on"] == 1 and info["only"] == 1, info
+rows = comm_paths.probe_paths(sizes_mb=(0.0625, 0.5), iters=2, warmup=1)
+assert all(x["ipc_oneshot"] > 0 and x["ipc_twoshot"] > 0 and x["rccl"] < 0 for x in rows), rows
+thr, one = comm_paths.choose_paths(rows)
+t = torch.arange(4096, device="cuda", dtype=torch.float32) * (r + 1)
+dist.all_reduce(t)  # thresholds restored after the probe: still exact
+assert torch.allclose(t, torch.arange(4096, device="cuda", dtype=torch.float32) * tot, rtol=1e-6)
 torch.cuda.synchronize()
-print("MESH_OK", r, w, flush=True)
+flags = "uncached" if info["flags_uncached"] else "finegrained" if info["flags_finegrained"] else "coarse"
+print("MESH_OK", r, w, "flags", flags, "rows", rows, flush=True)
 dist.destroy_process_group()
