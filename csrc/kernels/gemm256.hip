@@ -751,8 +751,16 @@ static int grid_of(const G256Args& a) {
 
 // Returns hipErrorInvalidValue when the shape is outside this kernel's contract (caller falls
 // back to the 128x128 kernel).
+MI_API int mi_gemm256p_nt(const void* A, const void* B, void* C, const float* bias, void* aux, int epi, int M, int N,
+                          int K, int lda, int ldb, int ldc, hipStream_t st);  // gemm256p.hip
+
 MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bias, void* aux, int epi, int M, int N,
                          int K, int lda, int ldb, int ldc, int out_f32, int accumulate, hipStream_t st) {
+  // bf16 out, no accumulation, plain / GELU epilogue: the persistent kernel (epilogue overlapped
+  // with the next tile's main loop); it declines shapes outside its contract
+  if (!out_f32 && !accumulate && (epi == 0 || epi == 1) &&
+      mi_gemm256p_nt(A, B, C, bias, aux, epi, M, N, K, lda, ldb, ldc, st) == (int)hipSuccess)
+    return (int)hipSuccess;
   if (K % 8 != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || (epi && (out_f32 || !aux)) || M <= 0 || N <= 0)
     return (int)hipErrorInvalidValue;
   G256Args a{};
