@@ -187,9 +187,11 @@ __global__ __launch_bounds__(512, 1) void gemm256p_nt_kernel(G256PArgs a) {
       f32x4& v1 = acc[mq * 4 + i][nq * 2 + 1];
       f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
       if (has_bias) {
-        const int nb = min(pn0 + wn * 64 + nq * 32 + 4 * fq, a.N - 20);  // clamp: chunks past N never stored
-        b0 = *(const f32x4*)(bias_lds + nb);
-        b1 = *(const f32x4*)(bias_lds + nb + 16);
+        // the two fragments' 4-column groups; a group past N is never stored (N % 8 == 0), its read
+        // is only kept inside the staged vector
+        const int nb0 = pn0 + wn * 64 + nq * 32 + 4 * fq, nb1 = nb0 + 16;
+        b0 = *(const f32x4*)(bias_lds + (nb0 < a.N ? nb0 : a.N - 4));
+        b1 = *(const f32x4*)(bias_lds + (nb1 < a.N ? nb1 : a.N - 4));
       }
       const uint32_t p0 = pack2bf(v0[0] + b0[0], v0[1] + b0[1]), p1 = pack2bf(v0[2] + b0[2], v0[3] + b0[3]);
       const uint32_t q0 = pack2bf(v1[0] + b1[0], v1[1] + b1[1]), q1 = pack2bf(v1[2] + b1[2], v1[3] + b1[3]);
