@@ -20,6 +20,8 @@
 //               dK^T += Q^T dS, reduction over q in registers (no atomics).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int HD = 64;     // head dim
@@ -59,14 +61,15 @@ __device__ __forceinline__ void store4bf(bf16_t* p, f32x4 v, float s) {
 // rows [0, TP) of two [T][ld] bf16 matrices (64 columns each) -> LDS [TP][KSTR], zero rows >= T.
 // All of a thread's global loads are issued before any LDS store (fully unrolled, fixed trip
 // count), so the staging costs one memory latency instead of one per 16-byte chunk.
-template <int TP>
+template <int TP, int NW>
 __device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, int ld0, bf16_t* dst1,
                                             const bf16_t* src1, int ld1, int T) {
-  constexpr int PER = (TP * 8 + 255) / 256;
+  constexpr int NT = 64 * NW;
+  constexpr int PER = (TP * 8 + NT - 1) / NT;
   uint4 v0[PER], v1[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, part = c & 7;
+    const int c = threadIdx.x + NT * i, row = c >> 3, part = c & 7;
     v0[i] = make_uint4(0, 0, 0, 0);
     v1[i] = make_uint4(0, 0, 0, 0);
     if (c < TP * 8 && row < T) {
@@ -76,7 +79,7 @@ __device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, in
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, part = c & 7;
+    const int c = threadIdx.x + NT * i, row = c >> 3, part = c & 7;
     if (c < TP * 8) {
       *(uint4*)&dst0[row * KSTR + part * 8] = v0[i];
       *(uint4*)&dst1[row * KSTR + part * 8] = v1[i];
@@ -84,8 +87,12 @@ __device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, in
   }
 }
 
-template <int NK2>  // keys padded to 32 * NK2 >= T
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+// NW waves per (batch, head) workgroup.  Backward: 8 (default) puts 4 waves on each SIMD at 2
+// workgroups per CU (the LDS holds two heads' operands; ~100 VGPRs), so one wave's LDS reads, exp
+// and MFMA-result latencies hide behind the others' MFMAs; MI355X_DP_ATT_WAVES=4 selects one wave
+// per SIMD per workgroup.  Forward: always 4 (~210 VGPRs).
+template <int NK2, int NW>  // keys padded to 32 * NK2 >= T
+__global__ __launch_bounds__(64 * NW, NW / 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int T, int H, float sl2) {
   constexpr int TP = 32 * NK2, NKT = 2 * NK2;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
@@ -93,12 +100,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
-  stage_rows2<TP>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
+  stage_rows2<TP, NW>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   const int nqt = (T + 15) >> 4;
-  for (int qt = wv; qt < nqt; qt += 4) {
+  for (int qt = wv; qt < nqt; qt += NW) {
     const int q = qt * 16 + li;
     const bool qv = q < T;
     bf16x8 qf[2];
@@ -152,8 +159,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   }
 }
 
-template <int NK2>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+template <int NK2, int NW>
+__global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                              const bf16_t* __restrict__ o,
                                                              const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ lse,
@@ -165,12 +172,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
-  stage_rows2<TP>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
+  stage_rows2<TP, NW>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   const int nqt = (T + 15) >> 4;
-  for (int qt = wv; qt < nqt; qt += 4) {
+  for (int qt = wv; qt < nqt; qt += NW) {
     const int q = qt * 16 + li;
     const bool qv = q < T;
     const size_t orow = ((size_t)b * T + q) * D + h * HD;
@@ -224,8 +231,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
   }
 }
 
-template <int NK2>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
+template <int NK2, int NW>
+__global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
                                                               const bf16_t* __restrict__ dout,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ dvec,
@@ -238,8 +245,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const bf16_t* __re
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
-  stage_rows2<TP>(Qs, base, ld, Ds, dout + (size_t)b * T * D + h * HD, D, T);
-  for (int i = threadIdx.x; i < TP; i += 256) {
+  stage_rows2<TP, NW>(Qs, base, ld, Ds, dout + (size_t)b * T * D + h * HD, D, T);
+  for (int i = threadIdx.x; i < TP; i += 64 * NW) {
     Ls[i] = i < T ? lse[(size_t)bh * T + i] * LOG2E : INFINITY;  // padded queries: P = 0
     Dv[i] = i < T ? dvec[(size_t)bh * T + i] : 0.f;
   }
@@ -247,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const bf16_t* __re
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   const int nkt = (T + 15) >> 4;
-  for (int kt = wv; kt < nkt; kt += 4) {
+  for (int kt = wv; kt < nkt; kt += NW) {
     const int key = kt * 16 + li;
     const bool kv = key < T;
     bf16x8 kf[2], vf[2];
@@ -315,13 +322,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const bf16_t* __re
 
 MI_API int mi_attn_max_seq() { return 256; }
 
+static int g_att_waves = 0;
+static int att_waves() {
+  if (!g_att_waves) {
+    const char* e = std::getenv("MI355X_DP_ATT_WAVES");
+    g_att_waves = (e && e[0] == '4') ? 4 : 8;
+  }
+  return g_att_waves;
+}
+
+// backward workgroup size in waves (4 or 8): A/B runs in one process
+MI_API int mi_set_att_waves(int w) {
+  g_att_waves = w == 4 ? 4 : 8;
+  return 0;
+}
+
 // qkv [B*T][3*H*64] bf16 (q | k | v, heads contiguous), o [B*T][H*64] bf16, lse [B*H][T] fp32
 MI_API int mi_attn_fwd(const void* qkv, void* o, float* lse, int B, int T, int H, float scale, hipStream_t st) {
   if (T <= 0 || T > 256 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
   const float sl2 = scale * LOG2E;
+  // forward: 4 waves (its 14 score tiles per q tile need ~210 VGPRs: 2 waves per SIMD)
 #define L(N)                                                                                             \
-  hipLaunchKernelGGL(attn_fwd_kernel<N>, dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, T, \
-                     H, sl2)
+  hipLaunchKernelGGL((attn_fwd_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)o, \
+                     lse, T, H, sl2)
   MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
   return (int)hipGetLastError();
@@ -333,13 +356,21 @@ MI_API int mi_attn_bwd(const void* qkv, const void* o, const void* dout, const f
   if (T <= 0 || T > 256 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
   const float sl2 = scale * LOG2E;
 #define L(N)                                                                                             \
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<N>, dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)o, \
-                     (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
+  if (att_waves() == 8)                                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<N, 8>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv,    \
+                       (const bf16_t*)o, (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale); \
+  else                                                                                                   \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv,    \
+                       (const bf16_t*)o, (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
   MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
 #define L(N)                                                                                             \
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel<N>, dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv,          \
-                     (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
+  if (att_waves() == 8)                                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<N, 8>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv,   \
+                       (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale);                  \
+  else                                                                                                   \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv,   \
+                       (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
   MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
   return (int)hipGetLastError();

@@ -685,18 +685,25 @@ static int g_num_cus = 0;
 static int g_tail_split_env = -1;
 static int g_tail_min_kt = 12;
 
-MI_API void mi_set_tail_split(int on) { g_tail_split_env = on ? 1 : 0; }
+
+static void plan_defaults() {
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+    g_num_cus = 256;
+  const char* e = std::getenv("MI355X_DP_TAIL_SPLIT");
+  g_tail_split_env = (e && e[0] == '0') ? 0 : 1;
+  if (const char* m = std::getenv("MI355X_DP_TAIL_MIN_KT")) g_tail_min_kt = std::max(1, std::atoi(m));
+}
+
+MI_API int mi_set_tail_split(int on) {
+  if (g_num_cus == 0) plan_defaults();
+  g_tail_split_env = on ? 1 : 0;
+  return 0;
+}
 
 static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
-  if (g_num_cus == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
-      g_num_cus = 256;
-    const char* e = std::getenv("MI355X_DP_TAIL_SPLIT");
-    g_tail_split_env = (e && e[0] == '0') ? 0 : 1;
-    if (const char* m = std::getenv("MI355X_DP_TAIL_MIN_KT")) g_tail_min_kt = std::max(1, std::atoi(m));
-  }
+  if (g_num_cus == 0) plan_defaults();
   const int tiles = a.tiles_m * a.tiles_n;
   const int full = (tiles / g_num_cus) * g_num_cus, tail = tiles - full;
   int split = 1;

@@ -61,11 +61,13 @@ signature("mi_colsum_bf16", P, P, I, I, I, P)
 signature("mi_attn_max_seq")
 signature("mi_attn_fwd", P, P, P, I, I, I, F, P)
 signature("mi_attn_bwd", P, P, P, P, P, P, I, I, I, F, P)
+signature("mi_set_att_waves", I)
 
 # gemm256.hip
 signature("mi_gemm256_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, I, P)
 signature("mi_gemm256p_nt", P, P, P, P, P, I, I, I, I, I, I, I, P)
 signature("mi_set_gemm_persist", I)
+signature("mi_set_tail_split", I)
 signature("mi_set_gemm256", I)
 signature("mi_gemm256_tn", P, P, P, I, I, I, I, I, I, P)
 signature("mi_dgrad_stat_rows", I, I, I, I, I, I, I, I, I)

@@ -61,9 +61,15 @@ def test_gemm256p_matches_reference_and_plain_kernel(M, N, K, use_bias):
     ref = A.float() @ B.float().t() + (bias if use_bias else 0)
     assert not torch.isnan(C).any()
     assert rel_err(C, ref) < 1e-2
-    # the same fp32 accumulation order and rounding points as the non-persistent kernel: identical
+    # the same fp32 accumulation order and rounding points as the non-persistent kernel without its
+    # tail split-K (which sums a last partial wave's tiles in K slices): identical
+    from mi355x_dp.ops import _lib
     C2 = torch.empty_like(C)
-    _plain(A, B, C2, bias)
+    _lib.call("mi_set_tail_split", 0)
+    try:
+        _plain(A, B, C2, bias)
+    finally:
+        _lib.call("mi_set_tail_split", 1)
     assert torch.equal(C, C2)
 
 

@@ -50,6 +50,7 @@ def main():
         A = (torch.rand(M, K, device="cuda") * 2 - 1).to(BF)
         B = (torch.rand(N, K, device="cuda") * 2 - 1).to(BF)
         bias = torch.randn(N, device="cuda") if has_bias else None
+        bias16 = bias.to(BF) if has_bias else None
         C = torch.empty(M, N, dtype=BF, device="cuda")
         st = stream_of(A)
 
@@ -57,7 +58,7 @@ def main():
             _lib.call("mi_gemm256_nt", ptr(A), ptr(B), ptr(C), ptr(bias), ptr(None), 0, M, N, K, K, K, N, 0, 0, st)
 
         def blas():
-            torch.nn.functional.linear(A, B, bias)
+            torch.nn.functional.linear(A, B, bias16)
         res = {"old": [], "p": [], "blas": []}
         for _ in range(a.rounds):
             _lib.call("mi_set_gemm_persist", 0)
