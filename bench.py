@@ -408,14 +408,23 @@ def run_ipc_probe(world: int, timeout_s: int = 180):
     env["PYTHONPATH"] = compat_pythonpath(env.get("PYTHONPATH"))
     cmd = [NATIVE_LAUNCHER, "--nproc", str(world), "--master-addr", "127.0.0.1", "--master-port",
            str(free_port()), "--", sys.executable, os.path.join(ROOT, "tools", "ipc_probe.py")]
+    # the launcher forwards SIGTERM to every rank (abort-all) and SIGKILLs them after its grace
+    # period: a hung probe never leaves orphaned GPU processes behind
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+        out, err = proc.communicate(timeout=timeout_s)
     except subprocess.TimeoutExpired:
+        proc.terminate()
+        try:
+            proc.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.communicate()
         return f"failed: timeout after {timeout_s} s"
-    for line in r.stdout.splitlines():
+    for line in out.splitlines():
         if line.startswith('{"ipc_probe"'):
             return json.loads(line)["ipc_probe"]
-    return f"failed: rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}"
+    return f"failed: rc={proc.returncode}: {(err or out)[-300:]}"
 
 
 if __name__ == "__main__":
