@@ -93,9 +93,19 @@ def _wbgrad(weight, bias, dy2, x2):
     return _finish_grad(weight, g), _finish_grad(bias, gb)
 
 
+# Plain data-gradient GEMMs (no fused epilogue: the qkv / proj / fc1 input gradients) through the
+# library GEMM (hipBLASLt): on the ViT-B/16 batch-256 shapes it runs 1.1-1.4x the native 256x256
+# kernel (profiles/vit_r3_gemm_attention.md).  Every GEMM with a fused epilogue stays native.
+# MI355X_DP_BLAS_DGRAD=0 keeps all of them native.
+import os as _os
+BLAS_DGRAD = _os.environ.get("MI355X_DP_BLAS_DGRAD", "1") == "1"
+
+
 def _dgrad(dy2, weight, epi=EPI_NONE, aux=None):
     """dX[M][K] = dY[M][N] · W[N][K] (NT against the transposed bf16 weight, cached by the flat
     engine once per optimizer step)."""
+    if epi == EPI_NONE and BLAS_DGRAD:
+        return torch.matmul(dy2, weight_bf16(weight))
     return _gemm(dy2, linear_weight_t(weight), None, epi, aux)
 
 

@@ -13,8 +13,16 @@ plus markdown-it).
 * ``docs/static/``: copied as-is;
 * concept slides (reference ``static/images/training/training21-24.png``) are drawn as SVG from
   code, written to ``<out>/images/``, and referenced from pages as ``/images/<name>.svg``;
-* shortcode ``{{< run-local cmd="..." >}}`` renders a "run it locally" box (the reference's
-  ``cf-launch`` / ``cf-download`` CloudFormation buttons);
+* ``docs/layouts/partials/*.html``: header / menu / toc / footer pieces, included by
+  ``{{partial "name"}}`` (the reference's ``layouts/partials``);
+* shortcodes (the reference's ``layouts/shortcodes``): ``{{< run-local cmd="..." >}}`` renders a
+  "run it locally" box, and so do ``cf-launch`` / ``cf-download`` (the reference's CloudFormation
+  buttons: there is no AWS account to launch into -- the box names the local command instead);
+  ``{{< tabs >}}{{< tab name="..." >}}...{{< /tab >}}{{< /tabs >}}`` renders a tab set (CSS radio
+  tabs, no JavaScript); ``{{< mermaid >}}...{{< /mermaid >}}`` keeps the diagram source in a
+  ``<pre class="mermaid">`` block (rendered by mermaid.js where a page loads it, readable as text
+  otherwise); ``{{< year >}}`` and ``{{< github repo="..." >}}``;
+* a table of contents per page from its ``##`` / ``###`` headings (the reference's ``toc`` partial);
 * links: ``x.md`` -> ``x.html`` and root-relative ``/...`` made page-relative (``relative_urls``).
 """
 from __future__ import annotations
@@ -164,11 +172,61 @@ def _rel(from_page, target):
     return "../" * depth + target.lstrip("/")
 
 
-def _shortcodes(text):
-    def run_local(m):
-        cmd = html.escape(m.group(1))
-        return f'<div class="run-local"><strong>Run locally</strong><pre><code>{cmd}</code></pre></div>'
-    return re.sub(r'\{\{<\s*run-local\s+cmd="([^"]*)"\s*>\}\}', run_local, text)
+def _run_local_box(cmd):
+    return f'<div class="run-local"><strong>Run locally</strong><pre><code>{html.escape(cmd)}</code></pre></div>'
+
+
+_TABSET = [0]
+
+
+def _shortcodes(text, md=None):
+    """Expand the shortcodes (module docstring) before markdown rendering; tab bodies are rendered
+    as markdown themselves (``md``)."""
+    text = re.sub(r'\{\{<\s*run-local\s+cmd="([^"]*)"\s*>\}\}', lambda m: _run_local_box(m.group(1)), text)
+    # CloudFormation buttons of the reference -> the local command of the same step
+    text = re.sub(r'\{\{<\s*cf-(?:launch|download)\s+([^>]*)>\}\}',
+                  lambda m: _run_local_box(re.search(r'cmd="([^"]*)"', m.group(1)).group(1)
+                                           if 'cmd="' in m.group(1) else "python -m mi355x_dp.launch --help"), text)
+    text = re.sub(r'\{\{<\s*year\s*>\}\}', lambda m: str(__import__("datetime").date.today().year), text)
+    text = re.sub(r'\{\{<\s*github\s+repo="([^"]*)"\s*>\}\}',
+                  lambda m: f'<a class="github" href="https://github.com/{html.escape(m.group(1))}">'
+                            f'{html.escape(m.group(1))}</a>', text)
+
+    def mermaid(m):
+        return f'<pre class="mermaid">{html.escape(m.group(1).strip())}</pre>'
+    text = re.sub(r'\{\{<\s*mermaid\s*>\}\}(.*?)\{\{<\s*/mermaid\s*>\}\}', mermaid, text, flags=re.S)
+
+    def tabs(m):
+        _TABSET[0] += 1
+        sid = f"tabset-{_TABSET[0]}"
+        items = re.findall(r'\{\{<\s*tab\s+name="([^"]*)"\s*>\}\}(.*?)\{\{<\s*/tab\s*>\}\}', m.group(1), flags=re.S)
+        out = [f'<div class="tabs" id="{sid}">']
+        for i, (name, body) in enumerate(items):
+            tid = f"{sid}-{i}"
+            inner = md.render(body.strip()) if md is not None else html.escape(body.strip())
+            out.append(f'<input type="radio" name="{sid}" id="{tid}"{" checked" if i == 0 else ""}>'
+                       f'<label for="{tid}">{html.escape(name.strip())}</label>'
+                       f'<div class="tab-body">{inner}</div>')
+        out.append("</div>")
+        return "".join(out)
+    return re.sub(r'\{\{<\s*tabs[^>]*>\}\}(.*?)\{\{<\s*/tabs\s*>\}\}', tabs, text, flags=re.S)
+
+
+def _toc(body_html):
+    """table of contents from the rendered page's h2 / h3 headings (ids added in place)"""
+    heads = []
+
+    def anchor(m):
+        level, inner = m.group(1), m.group(2)
+        text = re.sub(r"<[^>]+>", "", inner)
+        slug = re.sub(r"[^a-z0-9]+", "-", text.lower()).strip("-") or f"h{len(heads)}"
+        heads.append((int(level), slug, text))
+        return f'<h{level} id="{slug}">{inner}</h{level}>'
+    body_html = re.sub(r"<h([23])>(.*?)</h\1>", anchor, body_html)
+    if not heads:
+        return body_html, ""
+    items = "".join(f'<li class="toc-h{lv}"><a href="#{slug}">{t}</a></li>' for lv, slug, t in heads)
+    return body_html, f"<ul>{items}</ul>"
 
 
 def collect(docs=DOCS):
@@ -213,6 +271,11 @@ def render(out_dir, docs=DOCS):
     cfg = tomli.load(open(os.path.join(docs, "site.toml"), "rb"))
     md = MarkdownIt("commonmark", {"html": True}).enable("table")
     layout = open(os.path.join(docs, "layouts", "page.html"), encoding="utf-8").read()
+    pdir = os.path.join(docs, "layouts", "partials")
+    for name in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
+        if name.endswith(".html"):
+            part = open(os.path.join(pdir, name), encoding="utf-8").read().strip()
+            layout = layout.replace('{{partial "' + name[:-5] + '"}}', part)
     if os.path.exists(out_dir):
         shutil.rmtree(out_dir)
     shutil.copytree(os.path.join(docs, "static"), out_dir)
@@ -222,7 +285,7 @@ def render(out_dir, docs=DOCS):
             f.write(DIAGRAMS[name](title))
     pages = collect(docs)
     for p in pages:
-        body = md.render(_shortcodes(p["text"]))
+        body, toc = _toc(md.render(_shortcodes(p["text"], md)))
         cur = p["out"]
 
         def fix(m, cur=cur):
@@ -239,7 +302,8 @@ def render(out_dir, docs=DOCS):
         page = layout
         for k, v in (("language", cfg.get("language", "en")), ("description", cfg.get("description", "")),
                      ("author", cfg.get("author", "")), ("site_title", cfg["title"]), ("title", p["title"]),
-                     ("root", _rel(cur, "")), ("menu", _menu(pages, cfg, cur)), ("content", body)):
+                     ("root", _rel(cur, "")), ("menu", _menu(pages, cfg, cur)), ("toc", toc),
+                     ("year", str(__import__("datetime").date.today().year)), ("content", body)):
             page = page.replace("{{" + k + "}}", html.escape(v) if k in ("title", "site_title", "description", "author") else v)
         dst = os.path.join(out_dir, cur)
         os.makedirs(os.path.dirname(dst), exist_ok=True)

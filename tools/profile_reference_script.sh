@@ -24,3 +24,7 @@ timeout -k 10 400 python3 $SCRIPT $ARGS > gpurun_out/refprof_${TAG}_plain.log 2>
 end=$(date +%s.%N)
 echo "wall_s $(python -c "print(round($end - $start, 2))") epochs $EPOCHS batch $BATCH engine $ENGINE" | tee gpurun_out/refprof_${TAG}_wall.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/refprof_${TAG} -o run -- python3 $SCRIPT $ARGS > gpurun_out/refprof_${TAG}_rocprof.log 2>&1
+# keep the summary (span, GPU busy, per-kernel table), drop the database (too large to copy back)
+python tools/prof_summary.py $(find gpurun_out/refprof_${TAG} -name '*results.db' | head -1) --steps $((50000 / BATCH * EPOCHS)) \
+  --title "unmodified cifar10-distributed-smddp-gpu.py, batch $BATCH, engine DDP $ENGINE" > gpurun_out/refprof_${TAG}.summary.md
+rm -rf gpurun_out/refprof_${TAG}
