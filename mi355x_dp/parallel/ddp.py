@@ -380,6 +380,9 @@ class DataParallel(nn.Module):
         # place; the bf16 compute copy and the transposed dgrad copies follow it
         module.register_load_state_dict_post_hook(lambda _m, _keys: self.flat.refresh_bf16())
         self._params_version = self.flat.params_version()
+        self._params_dirty = False
+        if self.foreign_optimizer:
+            _watch_optimizer_steps(self)
         self._reset()
 
     @property
@@ -600,11 +603,13 @@ class DataParallel(nn.Module):
     def _foreign_prepare(self):
         """foreign_optimizer mode, before a forward: gradients set to None by the user's
         zero_grad are re-pointed at the (zeroed) flat buffer; parameters the user's optimizer
-        changed refresh the bf16 / transposed compute copies."""
+        changed (any optimizer step -- a global step hook -- or any in-place write, seen in the
+        parameters' version counters) refresh the bf16 / transposed compute copies."""
         v = self.flat.params_version()
-        if v != self._params_version:
+        if v != self._params_version or self._params_dirty:
             self.flat.refresh_bf16()  # + transposed dgrad operands
             self._params_version = v
+            self._params_dirty = False
         if torch.is_grad_enabled() and self.flat.reattach_grads():
             self.flat.zero_grad()
 
@@ -711,6 +716,24 @@ class DataParallel(nn.Module):
         self._wait_buffer_sync()
         self.wait_param_sync()
         return super().state_dict(*args, **kwargs)
+
+
+_FOREIGN_ENGINES = None
+
+
+def _watch_optimizer_steps(engine):
+    """Every optimizer step (any torch.optim optimizer) marks the foreign-optimizer engines' compute
+    copies stale; the next forward refreshes them."""
+    global _FOREIGN_ENGINES
+    import weakref
+    if _FOREIGN_ENGINES is None:
+        _FOREIGN_ENGINES = weakref.WeakSet()
+
+        def after_step(_opt, _args, _kwargs):
+            for e in list(_FOREIGN_ENGINES):
+                e._params_dirty = True
+        torch.optim.optimizer.register_optimizer_step_post_hook(after_step)
+    _FOREIGN_ENGINES.add(engine)
 
 
 class _GradBucket:
