@@ -732,7 +732,8 @@ def _watch_optimizer_steps(engine):
         def after_step(_opt, _args, _kwargs):
             for e in list(_FOREIGN_ENGINES):
                 e._params_dirty = True
-        torch.optim.optimizer.register_optimizer_step_post_hook(after_step)
+        from torch.optim.optimizer import register_optimizer_step_post_hook
+        register_optimizer_step_post_hook(after_step)
     _FOREIGN_ENGINES.add(engine)
 
 
