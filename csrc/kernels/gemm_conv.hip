@@ -1182,6 +1182,23 @@ MI_API int mi_register_aux_stream(hipStream_t st) {
   return 0;
 }
 
+// A stream whose kernels may only use `ncu` of the device's CUs (hipExtStreamCreateWithCUMask):
+// spread = 1 keeps every (total / ncu)-th CU id, 0 keeps the first ncu ids.  For the A/B of a
+// weight-gradient stream confined to part of the chip (the compute stream keeps every CU).
+MI_API int mi_create_cu_masked_stream(int ncu, int spread, hipStream_t* out) {
+  int dev = 0, total = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || total <= 0)
+    return (int)hipErrorInvalidValue;
+  ncu = std::max(1, std::min(ncu, total));
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (int k = 0; k < ncu; ++k) {
+    const int cu = spread ? (int)((int64_t)k * total / ncu) : k;
+    mask[cu / 32] |= 1u << (cu % 32);
+  }
+  return (int)hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+}
+
 MI_API int mi_set_tn_slabs(int on) {
   g_tn_slabs = on ? 1 : 0;
   return 0;

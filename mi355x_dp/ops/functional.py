@@ -116,8 +116,17 @@ class WgradStream:
             # MI355X_DP_WGRAD_PRIORITY=-1: the side stream's workgroups are dispatched ahead of the
             # compute stream's (default 0: equal priority; profiles/rn50_bs256_wgrad_stream.md)
             with torch.cuda.device(idx):
-                st = torch.cuda.Stream(device=self.device,
-                                       priority=int(os.environ.get("MI355X_DP_WGRAD_PRIORITY", "0")))
+                cus = int(os.environ.get("MI355X_DP_WGRAD_CUS", "0"))
+                if cus > 0:
+                    # A/B knob: the side stream confined to `cus` CUs (spread over the CU ids; the
+                    # compute stream keeps every CU), MI355X_DP_WGRAD_CU_BLOCK=1: the first `cus` ids
+                    h = ctypes.c_void_p()
+                    _lib.call("mi_create_cu_masked_stream", cus, int(os.environ.get("MI355X_DP_WGRAD_CU_BLOCK", "0")
+                                                                      != "1"), ctypes.addressof(h))
+                    st = torch.cuda.ExternalStream(h.value, device=self.device)
+                else:
+                    st = torch.cuda.Stream(device=self.device,
+                                           priority=int(os.environ.get("MI355X_DP_WGRAD_PRIORITY", "0")))
                 # its own split-K slab workspace (gemm_conv.hip)
                 _lib.call("mi_register_wgrad_stream", ctypes.c_void_p(st.cuda_stream))
             WgradStream._streams[idx] = st

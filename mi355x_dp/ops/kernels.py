@@ -21,6 +21,7 @@ signature("mi_gemm_tn", P, P, P, I, I, I, I, I, I, P)
 signature("mi_gemm_tn_bias", P, P, P, P, I, I, I, I, I, I, P)
 signature("mi_register_wgrad_stream", P)
 signature("mi_register_aux_stream", P)
+signature("mi_create_cu_masked_stream", I, I, P)
 
 # norm_act.hip
 signature("mi_bn_partial_rows", I, I)
