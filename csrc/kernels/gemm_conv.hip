@@ -1092,6 +1092,9 @@ static float* splitk_workspace(size_t floats, hipStream_t st) {
   }
   return w.p;
 }
+// the same per-stream slab workspace for the other kernels of this library that reduce per-block
+// partials deterministically (stem_conv.hip's weight gradient); nullptr -> their atomic path
+extern "C" float* mi_partials_workspace(size_t floats, hipStream_t st) { return splitk_workspace(floats, st); }
 static int g_tn_slabs = -1;
 static bool tn_slabs_on() {
   if (g_tn_slabs < 0) {

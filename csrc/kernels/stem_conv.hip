@@ -20,6 +20,9 @@
 #include <algorithm>
 #include <cstdlib>
 
+// gemm_conv.hip: per-stream slab workspace (allocated on first use; nullptr on failure)
+extern "C" float* mi_partials_workspace(size_t floats, hipStream_t st);
+
 namespace {
 
 constexpr int SR = 7, SS = 7, SSTR = 2;            // kernel 7x7, stride 2
@@ -219,11 +222,13 @@ __global__ __launch_bounds__(STEM_T, 1) void stem_conv_kernel(StemArgs a) {
 // its partial dW in registers across all its rows and adds it into the fp32 gradient once.
 constexpr int NUT = (NTAP + 1) / 2;                 // 25 n-tiles of 2 taps x 8 channels
 constexpr int DYPX = 128;                           // staged pixels per output row (Q <= 128)
+constexpr int STEM_WELEMS = KOUT * NTAP * 8;        // dW elements (64 x 49 taps x 8 channels)
 
 struct StemWArgs {
   const bf16_t* x;    // [Nb][H][W][8]
   const bf16_t* dy;   // [Nb][P][Q][64]
   float* dw;          // [64][7][7][8] fp32, accumulated
+  float* ws;          // [blocks][64 * 7 * 7 * 8] per-block partials (deterministic path) or null (atomics)
   int Nb, H, W, P, Q, pad;
   int pairs_per_img, total_pairs, pairs_per_block;
   int x_bytes, dy_bytes;
@@ -350,7 +355,11 @@ __global__ __launch_bounds__(STEM_T, 1) void stem_wgrad_kernel(StemWArgs a) {
       load_dy(img2, j2, buf);
     }
   }
-  // D[i = out channel 16m + 4g + r][j = 16u + li]: column j = tap 2u + (li >> 3), channel li & 7
+  // D[i = out channel 16m + 4g + r][j = 16u + li]: column j = tap 2u + (li >> 3), channel li & 7.
+  // Deterministic path: the block's partial dW goes to its own slab row (plain stores; every element
+  // of the row is written, zeros for blocks without work) and stem_wgrad_reduce_kernel sums the
+  // rows in a fixed order -- bitwise reproducible gradients.  Fallback: fp32 atomics into dw.
+  float* prow = a.ws ? a.ws + (size_t)blockIdx.x * STEM_WELEMS : nullptr;
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     if (v >= nv) break;
@@ -361,9 +370,38 @@ __global__ __launch_bounds__(STEM_T, 1) void stem_wgrad_kernel(StemWArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = 16 * m + 4 * g + r;
-        atomicAdd(a.dw + ((size_t)k * NTAP + tap) * 8 + (li & 7), acc[m][v][r]);
+        const size_t o = ((size_t)k * NTAP + tap) * 8 + (li & 7);
+        if (prow) prow[o] = acc[m][v][r];
+        else atomicAdd(a.dw + o, acc[m][v][r]);
       }
   }
+}
+
+// dw[e] += sum over rows b of ws[b][e], b ascending in G interleaved groups combined in LDS in a
+// fixed order.  Block: 32 float4 positions x 8 groups.
+constexpr int SWR_POS = 32, SWR_G = 8;
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float4* __restrict__ ws, float4* __restrict__ dw,
+                                                                int rows) {
+  __shared__ float4 red[SWR_G][SWR_POS];
+  const int pl = threadIdx.x % SWR_POS, grp = threadIdx.x / SWR_POS;
+  const int pos = blockIdx.x * SWR_POS + pl;
+  constexpr int NV = STEM_WELEMS / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (pos < NV)
+    for (int b = grp; b < rows; b += SWR_G) {
+      const float4 v = ws[(size_t)b * NV + pos];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  red[grp][pl] = s;
+  __syncthreads();
+  if (grp != 0 || pos >= NV) return;
+  for (int gg = 1; gg < SWR_G; ++gg) {
+    const float4 v = red[gg][pl];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float4 d = dw[pos];
+  d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
+  dw[pos] = d;
 }
 
 constexpr size_t stem_wgrad_lds_bytes() { return (size_t)(NRING * ROWPX + 2 * 2 * DYPX * 8) * 16; }
@@ -435,6 +473,14 @@ MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H
   a.pairs_per_block = cdiv(a.total_pairs, blocks);
   a.x_bytes = (int)xb;
   a.dy_bytes = (int)db;
+  // deterministic per-block partials (MI355X_DP_STEM_ATOMIC=1: the fp32-atomic path instead)
+  static int atomic_mode = -1;
+  if (atomic_mode < 0) {
+    const char* e = std::getenv("MI355X_DP_STEM_ATOMIC");
+    atomic_mode = (e && e[0] == '1') ? 1 : 0;
+  }
+  a.ws = (!atomic_mode && ((uintptr_t)dw & 15) == 0) ? mi_partials_workspace((size_t)blocks * STEM_WELEMS, st)
+                                                     : nullptr;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -442,5 +488,8 @@ MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H
     attr = true;
   }
   hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(STEM_T), stem_wgrad_lds_bytes(), st, a);
+  if (a.ws)
+    hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(STEM_WELEMS / 4, SWR_POS)), dim3(256), 0, st,
+                       (const float4*)a.ws, (float4*)dw, blocks);
   return (int)hipGetLastError();
 }

@@ -126,7 +126,7 @@ def test_reference_script_engine_ddp_matches_stock_ddp(tmp_path):
     torch.nn.parallel.DistributedDataParallel(model) is the flat-buffer engine (gradients written
     by the backward kernels into one buffer, no DDP copy-in/out, bf16 copies refreshed once per
     step) driven by the script's own stock optim.SGD.  One epoch at the reference's per-rank batch
-    (32) gives the same model.pth -- keys, layout, values -- as torch's stock DDP."""
+    (32) gives the same model.pth -- keys, layout, values (bitwise) -- as torch's stock DDP."""
     out_e, sd_e = _run_reference_script(tmp_path, "engine", True)
     out_s, sd_s = _run_reference_script(tmp_path, "stock", False)
     assert "mi355x_dp.parallel.engine_ddp" in out_e and "Test set: Average loss:" in out_e
@@ -138,7 +138,10 @@ def test_reference_script_engine_ddp_matches_stock_ddp(tmp_path):
             assert torch.equal(a, b), k
             continue
         err = float((a - b).norm() / b.norm().clamp_min(1e-12))
-        assert err < 2e-2, (k, err)  # 32 steps through bf16 kernels; different fp32 summation orders
+        # the native ResNet kernels are deterministic (no fp32 atomics), and the engine computes
+        # exactly what stock DDP + SGD compute: 32 steps stay bit-identical (this configuration is
+        # chaotic -- any nondeterminism would show as O(1) differences, tests/test_determinism_gpu.py)
+        assert err == 0.0, (k, err)
 
 
 def test_two_ranks_one_gpu_gloo(tmp_path):
