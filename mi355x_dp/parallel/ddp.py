@@ -615,6 +615,8 @@ class DataParallel(nn.Module):
 
     def _final_callback(self):
         self._final_cb_pending = False
+        if self.__dict__.pop("_graph_backward_ran", False) and self.comm_on:
+            self._mark_all_ready()
         self.finish_gradient_sync(average=True)
 
     def _arm_final_callback(self, out):
@@ -641,7 +643,9 @@ class DataParallel(nn.Module):
         self._reset()
         self.wait_param_sync()
         self._wait_buffer_sync()
-        out = self.module(*args, **kwargs)
+        out = self._graphed_forward(args, kwargs) if self.foreign_optimizer else None
+        if out is None:
+            out = self.module(*args, **kwargs)
         if self.foreign_optimizer and torch.is_grad_enabled():
             self._arm_final_callback(out)
         if self.broadcast_buffers and self.buffers.buffers and self.module.training:
@@ -653,6 +657,44 @@ class DataParallel(nn.Module):
             # touches the buffers, and the broadcast precedes every bucket collective on all ranks.
             self._buf_works.append(dist.broadcast(self.buffers.data, 0, group=self.process_group, async_op=True))
         return out
+
+    # ------------------------------------- foreign optimizer: graphed forward + backward
+    def _capture_stream(self):
+        s = getattr(self, "_cap_stream", None)
+        if s is None:
+            s = self._cap_stream = torch.cuda.Stream(device=self.flat.grad.device)
+        return s
+
+    def _graphed_forward(self, args, kwargs):
+        """Replay of the captured forward (+ its backward at ``loss.backward()``) for a small,
+        launch-bound step (parallel/step_graph.py); None: run the module eagerly."""
+        from . import step_graph
+        if not step_graph.eligible(self, args, kwargs):
+            return None
+        x = args[0]
+        key = step_graph.signature(x)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        st = graphs.get(key)
+        if st is None:
+            seen = self.__dict__.setdefault("_graph_seen", {})
+            seen[key] = seen.get(key, 0) + 1
+            if seen[key] <= step_graph.AFTER:
+                return None
+            st = graphs[key] = step_graph.CapturedStep(self, x)
+        elif any(g.busy() for g in graphs.values()):
+            return None
+        tok = self.__dict__.get("_graph_token")
+        if tok is None:
+            tok = self._graph_token = torch.zeros((), device=x.device, requires_grad=True)
+        return st(tok, x)
+
+    def _mark_all_ready(self):
+        """after a graph replay: the captured backward wrote every gradient; launch the buckets"""
+        for i in range(len(self.flat.params)):
+            if self.reducer is not None:
+                self._ready_native(i)
+            else:
+                self._mark_ready(i)
 
     def _wait_buffer_sync(self):
         for w in self._buf_works:
