@@ -96,6 +96,11 @@ struct NTArgs {
   // (0, 0) alone) and reads as 0 elsewhere
   int cls_map[4], ncls;
   int aux_even;
+  // split-K (small grids, see launch_nt): SPLIT 1 blocks (blockIdx.z = split) accumulate k-steps
+  // [z * ksplit, (z + 1) * ksplit) and store their fp32 tiles to ws; SPLIT 2 blocks sum the
+  // splits in order and run the ordinary epilogue
+  float* ws;
+  int splits, ksplit;
   ConvGeom g;
 };
 
@@ -148,8 +153,9 @@ constexpr int nt_occupancy() {
 // into LDS and all nine taps read their A fragments from it (shifted row addresses), with the
 // weight tile of the next tap loading into the other B buffer during each tap's MFMAs.  The
 // per-tap gather re-reads every input pixel ~9x through L2; the halo reads it ~(rp+2)/rp x.
-template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false>
+template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false, int SPLIT = 0>
 __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_kernel(NTArgs a) {
+  static_assert(SPLIT == 0 || (STAGES == 1 && !SMALLC && !HALO), "split-K: single-stage gather/plain tiles only");
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   const int Mlim = HALO ? m0 + hrows : Mrows;
   if (m0 >= Mrows) {
     // empty tile of a parity class: its statistics rows still have to be defined
-    if (a.stats) {
+    if (SPLIT != 1 && a.stats) {
       const int prow = cy * a.tiles_m + tm;
       for (int c = threadIdx.x; c < 2 * BN; c += 256) {
         const int which = c / BN, col = c - which * BN;
@@ -245,9 +251,21 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   constexpr uint32_t OOB = 0xFFFFFFF0u;
 
   const int nS = (a.mode == 3) ? ns : a.g.S;
-  const int nk = (a.mode == 3) ? nr * ns * (int)a.g.fCpt.d : (a.K + BK - 1) / BK;
+  int nk = (a.mode == 3) ? nr * ns * (int)a.g.fCpt.d : (a.K + BK - 1) / BK;
   // wave-uniform k position: gather-space tap (kr, ks) and channel-chunk base kc
   int kr = 0, ks = 0, kc = 0;
+  int kt0 = 0;  // first k-step of this block (split-K)
+  if constexpr (SPLIT == 1) {
+    kt0 = blockIdx.z * a.ksplit;
+    nk = min(nk, kt0 + a.ksplit);
+    if (a.mode != 0) {  // (kr, ks, kc) of k-step kt0: channel chunks fastest, then taps of a row
+      const int cpt = (int)a.g.fCpt.d;
+      const int t = kt0 / cpt;
+      kc = (kt0 - t * cpt) * 64;
+      ks = t % nS;
+      kr = t / nS;
+    }
+  }
   // mode 4 (SMALLC): per-LANE tap t = 8*kt + lc -> (tr4, ts4), advanced by 8 taps per k-step
   int tr4 = 0, ts4 = 0, dts4 = 0, dtr4 = 0, ntaps = 0;
   if constexpr (SMALLC) {
@@ -406,8 +424,18 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         __syncthreads();
       }
     }
+  } else if constexpr (SPLIT == 2) {
+    // sum of the splits' partial tiles, in split order (deterministic)
+    const int tl = cy * gridDim.x + tile;
+    const f32x4* src = (const f32x4*)a.ws + (size_t)tl * a.splits * (MI * NJ * 256) + tid;
+    for (int z = 0; z < a.splits; ++z) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] += src[(size_t)(z * MI * NJ + i * NJ + j) * 256];
+    }
   } else if constexpr (STAGES == 1) {
-    for (int kt = 0; kt < nk; ++kt) {
+    for (int kt = kt0; kt < nk; ++kt) {
 #if MI_NT_PROBE == 2  // timing probe only: no operand loads (LDS left as is)
       if (kt < 0) issue_loads(kt, 0);
 #else
@@ -429,6 +457,16 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  }
+
+  if constexpr (SPLIT == 1) {
+    const int tl = cy * gridDim.x + tile;
+    f32x4* dst = (f32x4*)a.ws + ((size_t)tl * a.splits + blockIdx.z) * (MI * NJ * 256) + tid;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) dst[(size_t)(i * NJ + j) * 256] = acc[i][j];
+    return;
   }
 
   // output row offset (elements) of tile row m
@@ -963,6 +1001,24 @@ static int nt_stages() {
   return g_nt_stages;
 }
 
+static float* splitk_workspace(size_t floats, hipStream_t st);
+
+// split-K of the NT kernel for small grids: a layer-4 conv of ResNet-18 on 32x32 images at batch
+// 32 is 8 output tiles of 72 k-steps each -- 8 of 256 CUs walking a latency-bound serial chain.
+// With fewer than MI355X_DP_NT_SPLIT_BLOCKS (default 128) blocks, the k-steps are split over
+// blockIdx.z (>= 2 k-steps per split, about 256 blocks in all), the partial tiles go to the
+// stream's slab workspace and a second launch sums them in split order and runs the epilogue.
+// MI355X_DP_NT_SPLITK=0 disables.
+static int g_nt_split_blocks = -1;
+static int nt_split_blocks() {
+  if (g_nt_split_blocks < 0) {
+    const char* e = std::getenv("MI355X_DP_NT_SPLITK");
+    const char* b = std::getenv("MI355X_DP_NT_SPLIT_BLOCKS");
+    g_nt_split_blocks = (e && e[0] == '0') ? 0 : (b ? std::max(0, std::atoi(b)) : 128);
+  }
+  return g_nt_split_blocks;
+}
+
 template <int BM, int BN>
 hipError_t launch_nt(NTArgs& a, hipStream_t st) {
   int classes = 1, mrows = a.M;
@@ -977,6 +1033,23 @@ hipError_t launch_nt(NTArgs& a, hipStream_t st) {
   if (a.halo_rp > 0) a.tiles_m = (a.M / (a.g.P * a.g.Q)) * a.halo_pb;
   int grid = a.tiles_m * cdiv(a.N, BN);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
+  if (a.halo_rp == 0 && a.mode != 4 && grid * classes < nt_split_blocks()) {
+    const int cpt = a.mode == 0 ? 0 : (int)a.g.fCpt.d;
+    const int nk = a.mode == 0 ? cdiv(a.K, BK)
+                 : a.mode == 3 ? cdiv(a.g.R, a.g.stride) * cdiv(a.g.S, a.g.stride) * cpt : a.g.R * a.g.S * cpt;
+    int splits = std::min(nk / 2, 256 / std::max(grid * classes, 1));
+    if (splits >= 2) {
+      a.ksplit = cdiv(nk, splits);
+      a.splits = cdiv(nk, a.ksplit);
+      a.ws = splitk_workspace((size_t)grid * classes * a.splits * BM * BN, st);
+      if (a.ws) {
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, false, 1>), dim3(grid, classes, a.splits), dim3(256), 0, st,
+                           a);
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, false, 2>), dim3(grid, classes), dim3(256), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+  }
   if (a.halo_rp > 0)
     hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, true>), dim3(grid), dim3(256), 0, st, a);
   else if (a.mode == 4)
@@ -1209,6 +1282,12 @@ MI_API int mi_set_tn_slabs(int on) {
 
 MI_API int mi_set_glds(int on) {
   g_nt_glds = on ? 1 : 0;
+  return 0;
+}
+
+// NT split-K threshold: grids below this many blocks split their k-steps (0 disables; tests).
+MI_API int mi_set_nt_split_blocks(int blocks) {
+  g_nt_split_blocks = std::max(0, blocks);
   return 0;
 }
 

@@ -114,6 +114,22 @@ def native_attention_ok(T, head_dim):
     return head_dim == 64 and 0 < T <= 256
 
 
+_SDPA_WARNED = set()
+
+
+def _warn_sdpa(T, Dh):
+    """The native kernel covers head dim 64 with T <= 256 (ViT-B/16); anything else runs torch's
+    scaled_dot_product_attention -- said once per shape, so a non-native path is never silent.
+    MI355X_DP_STRICT_NATIVE=1 makes it an error instead."""
+    if _os.environ.get("MI355X_DP_STRICT_NATIVE", "0") == "1":
+        raise RuntimeError(f"attention: no native kernel for T={T}, head_dim={Dh} (MI355X_DP_STRICT_NATIVE=1)")
+    if (T, Dh) not in _SDPA_WARNED:
+        _SDPA_WARNED.add((T, Dh))
+        import warnings
+        warnings.warn(f"mi355x_dp attention: T={T}, head_dim={Dh} is outside the native kernel "
+                      f"(head_dim 64, T <= 256); using torch scaled_dot_product_attention", stacklevel=3)
+
+
 def _attn_fwd(qkv2, B, T, H, need_grad):
     """softmax(q kᵀ/√d) v over the packed [B·T][3·H·Dh] projection; returns o [B·T][H·Dh].
     Native kernel (csrc/kernels/attention.hip) for Dh = 64, T <= 256 (ViT-B/16: T = 197)."""
@@ -125,6 +141,7 @@ def _attn_fwd(qkv2, B, T, H, need_grad):
         lse = torch.empty((B * H * T,), dtype=F32, device=qkv2.device)
         _lib.call("mi_attn_fwd", ptr(qkv2), ptr(o), ptr(lse), B, T, H, float(scale), stream_of(qkv2))
         return o, (("native", lse, o) if need_grad else None)
+    _warn_sdpa(T, Dh)
     if not need_grad:
         q, k, v = qkv2.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
         o4 = F.scaled_dot_product_attention(q, k, v)

@@ -458,3 +458,47 @@ def test_flat_transposed_conv_weights_follow_sgd():
     sd = {k: v.clone() * 0.5 for k, v in eng.module.state_dict().items()}
     eng.module.load_state_dict(sd)
     check()
+
+
+# ResNet-18 on 32x32 images at batch 32 (the reference's per-GPU shape): grids of 8-64 tiles with
+# 9-72 k-steps each -> the NT kernel's split-K path (partial tiles + in-order sum + epilogue)
+SPLITK_SHAPES = [
+    (32, 512, 1, 512, 3, 1, 1),   # layer4 3x3 at 1x1 spatial: 8 tiles x 72 k-steps
+    (32, 256, 2, 512, 3, 2, 1),   # stride-2 3x3: parity-class dgrad (mode 3) split
+    (32, 64, 8, 64, 3, 1, 1),     # layer1 3x3 at 8x8
+    (32, 128, 4, 256, 1, 2, 0),   # 1x1 / stride-2 projection
+]
+
+
+@pytest.mark.parametrize("shape", SPLITK_SHAPES)
+def test_conv_splitk_small_grids(shape):
+    from mi355x_dp.ops import _lib, conv2d
+    N, C, H, K, R, s, p = shape
+    torch.manual_seed(2)
+    x0 = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    w0 = (torch.randn(K, C, R, R, device="cuda") * (2.0 / (C * R * R)) ** 0.5).to(BF).float()
+    w0 = w0.contiguous(memory_format=CL)
+    out = {}
+    lib = _lib.load(True)
+    try:
+        for blocks in (128, 0):  # split-K on (default threshold), off
+            lib.mi_set_nt_split_blocks(blocks)
+            x = x0.clone().requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            y = conv2d(x, w, None, s, p)
+            gy = torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+            y.backward(gy.to(BF).contiguous(memory_format=CL))
+            out[blocks] = (y.detach().float(), x.grad.float(), w.grad.float(), gy)
+    finally:
+        lib.mi_set_nt_split_blocks(128)
+    xr = x0.float().requires_grad_(True)
+    wr = w0.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, p)
+    yr.backward(out[128][3].to(BF).float())
+    for blocks in (128, 0):
+        y, dx, dw, _ = out[blocks]
+        assert rel_err(y, yr) < 1e-2, blocks
+        assert rel_err(dx, xr.grad) < 2e-2, blocks
+        assert rel_err(dw, wr.grad) < 2e-2, blocks
+    assert rel_err(out[128][0], out[0][0]) < 1e-2
+    assert rel_err(out[128][1], out[0][1]) < 1e-2
