@@ -43,6 +43,10 @@
 #include <mutex>
 #include <cstdlib>
 
+#ifndef MI_FENCE_HANDOFF
+#define MI_FENCE_HANDOFF 0  // 1: tail split-K hand-off through a __threadfence pair (A/B only)
+#endif
+
 namespace {
 
 constexpr int G_BM = 256, G_BN = 256, G_BK = 64;
@@ -294,16 +298,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   // ---- tail split-K: publish this split's partial; the last arriver of the tile reduces
   if (tail_tile >= 0) {
     // partial layout [acc index][thread] (16 B per thread): every store / load wave-instruction
-    // covers 1 KB contiguous.  One thread fences (device-scope release after the barrier, cumulative
-    // over the workgroup's stores) and counts arrivals; the last arriver acquires and reduces.
+    // covers 1 KB contiguous.  Fence-free hand-off (MI355X_MICROARCH.md, inter-workgroup
+    // visibility, first table row): every wave stores its partial with sc1 (write-through, dropped
+    // from the XCD's L2) and waits for the stores, then behind a barrier one lane counts the
+    // arrival with an agent-scope atomic; the last arriver reads the partials with sc1 loads.  The
+    // acq_rel __threadfence pair this replaces cost ~3.5 us per fence.
     const size_t tile_f = (size_t)G_BM * G_BN;
-    f32x4* mine = (f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + split) * tile_f) + tid;
+#if MI_FENCE_HANDOFF  // A/B build: the former plain stores + acq_rel fence pair
+    f32x4* mine0 = (f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + split) * tile_f) + tid;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mine[(i * 4 + j) * 512] = acc[i][j];
+      for (int j = 0; j < 4; ++j) mine0[(i * 4 + j) * 512] = acc[i][j];
     __syncthreads();
-    int* flag = (int*)smem;  // LDS is free after the loop (no second __shared__ object)
+    int* flag = (int*)smem;
     if (tid == 0) {
       __threadfence();
       flag[0] = atomicAdd(a.counters + tail_tile, 1) == a.tail_split - 1;
@@ -311,8 +319,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     }
     __syncthreads();
     if (!flag[0]) return;
-    // sum the partials in split order 0, 1, ... -- this block's own one re-read from the workspace
-    // -- so the result does not depend on which split arrived last (fp32 adds do not associate)
     for (int q = 0; q < a.tail_split; ++q) {
       const f32x4* part = (const f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + q) * tile_f) + tid;
 #pragma unroll
@@ -323,6 +329,34 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
           acc[i][j] = q == 0 ? v : acc[i][j] + v;
         }
     }
+#else
+    const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
+        a.ws + (size_t)tail_tile * a.tail_split * tile_f, (short)0, (int)(a.tail_split * tile_f * 4), 0x00020000);
+    constexpr int SC1 = 16;  // cache-policy bits of the buffer intrinsics: sc1
+    const uint32_t mine = (uint32_t)(split * tile_f * 4) + tid * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rsw, mine + (i * 4 + j) * 8192, 0, SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;  // LDS is free after the loop (no second __shared__ object)
+    if (tid == 0) flag[0] = atomicAdd(a.counters + tail_tile, 1) == a.tail_split - 1;
+    __syncthreads();
+    if (!flag[0]) return;
+    // sum the partials in split order 0, 1, ... -- this block's own one re-read from the workspace
+    // -- so the result does not depend on which split arrived last (fp32 adds do not associate)
+    for (int q = 0; q < a.tail_split; ++q) {
+      const uint32_t part = (uint32_t)(q * tile_f * 4) + tid * 16;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsw, part + (i * 4 + j) * 8192, 0, SC1);
+          acc[i][j] = q == 0 ? v : acc[i][j] + v;
+        }
+    }
+#endif
     if (tid == 0) a.counters[tail_tile] = 0;  // ready for the next launch (stream order)
     __syncthreads();
   }
