@@ -47,6 +47,9 @@
 #ifndef MI_TN_BLOCKS_PER_CU
 #define MI_TN_BLOCKS_PER_CU 3
 #endif
+#ifndef MI_TN_CONV_BLOCKS_PER_CU
+#define MI_TN_CONV_BLOCKS_PER_CU 3  // conv weight-gradient variant (A/B: 4)
+#endif
 #ifndef MI_TN_NOATOMIC
 #define MI_TN_NOATOMIC 0  // timing experiment only: split-K partials stored, not added (wrong results)
 #endif
@@ -659,8 +662,13 @@ __device__ __forceinline__ int tr_swz(int k) {
   return (4 * (k & 3) + 16 * ((k >> 3) & 1)) & (UNITS - 1);
 }
 
-template <int BM, int BN, int STAGES>
-__global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn_kernel(TNArgs a) {
+// MODE: 0 plain [K][N] B operand, 1 conv weight gradient (B gathered from the NHWC input); CS: the
+// fused bias-gradient column sums (Linear layers only).  Both are compile-time so that neither the
+// gather bookkeeping nor the colsum accumulators occupy registers in the variants that do not use
+// them (the conv variant fits 128 VGPRs and runs 4 blocks per CU).
+template <int BM, int BN, int STAGES, int MODE = 1, bool CS = false>
+__global__ __launch_bounds__(256, STAGES == 1 ? (MODE == 1 && !CS ? MI_TN_CONV_BLOCKS_PER_CU : MI_TN_BLOCKS_PER_CU) : 2)
+void tn_kernel(TNArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int AU = BM / 4, BU = BN / 4;            // 8-byte units per LDS row
@@ -697,7 +705,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
 
   // conv-mode B column geometry: this thread's 8 columns n0 + 8*b_lc .. +7 = (tap, channel c0..c0+7)
   int tap_r = 0, tap_s = 0, c0 = 0;
-  if (a.mode == 1) {
+  if constexpr (MODE == 1) {
     const int ncol = n0 + b_lc * 8;
     const int tap = ncol / a.g.Cs;
     c0 = ncol - tap * a.g.Cs;
@@ -712,7 +720,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
 #pragma unroll
   for (int i = 0; i < B_CH; ++i) {
     const uint32_t k = (uint32_t)min(kbeg + b_r + B_RSTEP * i, a.K - 1);
-    if (a.mode == 1) {
+    if constexpr (MODE == 1) {
       const uint32_t img = fdiv(k, a.g.fPQ);
       const uint32_t rem = k - img * a.g.fPQ.d;
       const uint32_t p = fdiv(rem, a.g.fQ);
@@ -743,7 +751,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
     for (int i = 0; i < B_CH; ++i) {
       const int k = k0 + b_r + B_RSTEP * i;
       uint32_t vo = OOB;
-      if (a.mode == 0) {
+      if constexpr (MODE == 0) {
         if (k < kend && b_n < a.N) vo = (uint32_t)(k * a.ldb + b_n) * 2u;
       } else {
         const int ih = b_p[i] * st - pad + tap_r, iw = b_q[i] * st - pad + tap_s;
@@ -769,10 +777,10 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   // fused bias gradient: the first column-tile's blocks also reduce their A fragments against a
   // ones operand (one extra MFMA per 16 rows in the wn == 0 waves): D[m][*] = sum_k A[k][m]
-  const bool do_cs = a.colsum != nullptr && (tile % nbn) == 0 && wn == 0;
-  f32x4 acc_cs[MI];
+  const bool do_cs = CS && (tile % nbn) == 0 && wn == 0;
+  f32x4 acc_cs[CS ? MI : 1];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) acc_cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < (CS ? MI : 1); ++i) acc_cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   short ones_s __attribute__((ext_vector_type(8))) = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
                                                       0x3F80, 0x3F80, 0x3F80, 0x3F80};
   const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_s);
@@ -803,7 +811,8 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      if (do_cs) {
+      if constexpr (CS) {
+        if (do_cs)
 #pragma unroll
         for (int i = 0; i < MI; ++i) acc_cs[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, acc_cs[i], 0, 0, 0);
       }
@@ -862,7 +871,7 @@ __global__ __launch_bounds__(256, STAGES == 1 ? MI_TN_BLOCKS_PER_CU : 2) void tn
       }
     }
   }
-  if (do_cs && li == 0) {  // every column of the ones-product holds the sum; lane li == 0 adds it
+  if constexpr (CS) if (do_cs && li == 0) {  // every column of the ones-product holds the sum; lane li == 0 adds it
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1191,10 +1200,17 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   a.ws = nullptr;
   if (splits > 1 && a.colsum == nullptr && tn_slabs_on())
     a.ws = splitk_workspace((size_t)tiles * splits * BM * BN, st);
-  if (glds_on())
-    hipLaunchKernelGGL((tn_kernel<BM, BN, 1>), dim3(tiles * splits), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((tn_kernel<BM, BN, 2>), dim3(tiles * splits), dim3(256), 0, st, a);
+  const int st_n = glds_on() ? 1 : 2;
+  if (a.mode == 1) {
+    if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
+  } else if (a.colsum) {
+    if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 0, true>), dim3(tiles * splits), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 0, true>), dim3(tiles * splits), dim3(256), 0, st, a);
+  } else {
+    if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 0, false>), dim3(tiles * splits), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 0, false>), dim3(tiles * splits), dim3(256), 0, st, a);
+  }
   if (a.ws) {
     // split groups per position: ~8 slab reads per thread, at most 64 groups, and enough blocks
     int log2g = 0;
