@@ -2,10 +2,41 @@
 #pragma once
 #include "common.h"
 
+#ifndef MI_GELU_OCML
+#define MI_GELU_OCML 0  // 1: the device library's erff (A/B builds)
+#endif
+
+// erf(z) without branches (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 -- far below the bf16
+// output's 2^-9 relative rounding): one reciprocal, one exp, five FMAs.  The device library's erff
+// is a multi-range routine that made the GELU epilogues of the ViT GEMMs VALU-bound (fc1 +0.22 ms,
+// fc2 data gradient +0.22 ms per layer over the plain GEMM; tools/bench_vit_layer_gemms.py).
+// e_out = exp(-z*z), which the GELU derivative reuses (exp(-x^2/2) at z = x/sqrt(2)).
+__device__ __forceinline__ float erf_fast(float z, float& e_out) {
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * az);
+  const float e = __expf(-az * az);
+  const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  e_out = e;
+  return copysignf(1.f - p * e, z);
+}
+
 // erf-form GELU (nn.GELU default) and its derivative
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678f)); }
+__device__ __forceinline__ float gelu_f(float x) {
+#if MI_GELU_OCML
+  return 0.5f * x * (1.f + erff(x * 0.70710678f));
+#else
+  float e;
+  return 0.5f * x * (1.f + erf_fast(x * 0.70710678f, e));
+#endif
+}
 __device__ __forceinline__ float gelu_grad_f(float x) {
+#if MI_GELU_OCML
   return 0.5f * (1.f + erff(x * 0.70710678f)) + x * 0.39894228f * __expf(-0.5f * x * x);
+#else
+  float e;  // exp(-x^2 / 2)
+  const float r = erf_fast(x * 0.70710678f, e);
+  return 0.5f * (1.f + r) + x * 0.39894228f * e;
+#endif
 }
 
 // elementwise op on one 16-byte chunk (8 bf16) of the bf16 epilogue; aux has C's layout.
