@@ -202,15 +202,15 @@ __global__ __launch_bounds__(512, 1) void gemm256p_nt_kernel(G256PArgs a) {
       // N % 8 == 0: a 16-byte chunk is all in or all out
       const uint32_t off = (m < a.M && col < a.N) ? (uint32_t)(m * a.ldc + col) * 2u : P_OOB;
       if constexpr (EPI == 1) {
-        // aux = bf16(acc + bias); C = bf16(gelu(aux)) -- gemm256.hip's rounding points
-        float f[8];
+        // u = bf16(acc + bias); C = bf16(gelu(u)), aux = bf16(gelu'(u)) -- gemm256.hip's rounding points
+        float f[8], d[8];
         unpack8(o, f);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          f[r] = gelu_f(f[r]);
+          f[r] = gelu_fg(f[r], d[r]);
           __builtin_amdgcn_sched_barrier(0);  // one erf at a time (register pressure)
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsX, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(d)), rsX, off, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(f)), rsC, off, 0, 0);
       } else {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsC, off, 0, 0);

@@ -11,6 +11,7 @@ with an explicit backward, so every elementwise op rides on a kernel that runs a
   y = x + o Woᵀ   NT, residual epilogue     dy -> proj: TN(+bias), NT -> do -> attention bwd -> dqkv
   ln_2            mi_layernorm_fwd          dqkv -> TN(+bias), NT -> dh1
   g = gelu(h2W1ᵀ) NT, GELU epilogue         dx = dy + ln_1ᵀ(dh1)       (LN bwd, residual add fused)
+                  (+ gelu' kept for the backward's epilogue, which only multiplies by it)
   z = y + g W2ᵀ   NT, residual epilogue
 
 No torch elementwise kernels, no autograd-inserted residual-gradient adds, and the bias
@@ -204,7 +205,7 @@ def _layer_forward(x2, B, T, heads, eps, params, need_grad):
     o, attn = _attn_fwd(qkv, B, T, heads, need_grad)
     y = _gemm(o, weight_bf16(wo), bo, EPI_RESIDUAL, x2)
     h2, m2, r2 = _ln_fwd(y, ln2w, ln2b, eps)
-    g, u = _gemm(h2, weight_bf16(w1), b1, EPI_GELU)
+    g, u = _gemm(h2, weight_bf16(w1), b1, EPI_GELU)  # u = gelu'(pre-activation): all the backward needs
     z = _gemm(g, weight_bf16(w2), b2, EPI_RESIDUAL, y)
     saved = (x2, h1, m1, r1, qkv, o, y, h2, m2, r2, u, g) if need_grad else None
     return z, saved, attn
