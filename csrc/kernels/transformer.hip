@@ -11,6 +11,9 @@
 namespace {
 
 constexpr int LN_MAXV = 8;  // 4-element (8-byte) vectors per lane: D <= 64 * 4 * 8 = 2048
+#ifndef MI_LN_REPLICAS
+#define MI_LN_REPLICAS 32  // LayerNorm parameter-gradient replicas (0: atomics straight into dw / db)
+#endif
 #ifndef MI_LN_BWD_RW
 #define MI_LN_BWD_RW 2  // LayerNorm backward rows in flight per wave (D <= 1024); A/B knob
 #endif
@@ -37,15 +40,23 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   if (row >= M) return;
   const int nv = D >> 2;
   const bf16_t* xr = x + (size_t)row * D;
+  // every load of the row (x, and the affine parameters the store loop needs) issued up front,
+  // branch-free (chunks past D read a clamped address and are discarded): one memory latency
+  // per row instead of one for x and another for w / b after the reductions
   float v[LN_V][4];
+  float4 wv[LN_V], bv[LN_V];
+#pragma unroll
+  for (int i = 0; i < LN_V; ++i) {
+    const int c = min(lane + 64 * i, nv - 1);
+    load4(xr + 4 * c, v[i]);
+    wv[i] = *(const float4*)(w + 4 * c);
+    bv[i] = *(const float4*)(b + 4 * c);
+  }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < LN_V; ++i) {
     const int c = lane + 64 * i;
-    if (c < nv) {
-      load4(xr + 4 * c, v[i]);
-      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-    }
+    if (c < nv) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   }
   const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
@@ -63,10 +74,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   for (int i = 0; i < LN_V; ++i) {
     const int c = lane + 64 * i;
     if (c < nv) {
-      const float4 wv = *(const float4*)(w + 4 * c);
-      const float4 bv = *(const float4*)(b + 4 * c);
-      float o[4] = {(v[i][0] - mean) * rstd * wv.x + bv.x, (v[i][1] - mean) * rstd * wv.y + bv.y,
-                    (v[i][2] - mean) * rstd * wv.z + bv.z, (v[i][3] - mean) * rstd * wv.w + bv.w};
+      float o[4] = {(v[i][0] - mean) * rstd * wv[i].x + bv[i].x, (v[i][1] - mean) * rstd * wv[i].y + bv[i].y,
+                    (v[i][2] - mean) * rstd * wv[i].z + bv[i].z, (v[i][3] - mean) * rstd * wv[i].w + bv[i].w};
       store4(yr + 4 * c, o);
     }
   }
@@ -75,13 +84,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 
 // dx = dres + rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 // dw += sum_rows dy * xhat, db += sum_rows dy: per-lane register partials over the rows this
-// wave visits (grid-stride), reduced across the block's 4 waves in LDS, one atomic per column.
+// wave visits (grid-stride), reduced across the block's 4 waves in LDS, then one atomic per column
+// into replica (block mod R) of a [R][2][D] workspace -- every block of a resident-sized grid (768
+// at D = 768) adding into the same 6 KB of dw / db serialised the kernel's tail on atomic
+// contention (MI355X_MICROARCH.md: one shared row ~14x slower); ln_rep_reduce_kernel then sums the
+// R replicas into dw / db and re-zeroes them.  rep == nullptr: atomics straight into dw / db.
 template <int LN_V>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in,
                                                      const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
-                                                     float* __restrict__ dw, float* __restrict__ db, int M, int D) {
+                                                     float* __restrict__ dw, float* __restrict__ db, int M, int D,
+                                                     float* __restrict__ rep, int R) {
   extern __shared__ float red[];  // [4][D]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nv = D >> 2;
@@ -92,27 +106,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int e = 0; e < 4; ++e) { pw[i][e] = 0.f; pb[i][e] = 0.f; }
 
   // A wave owns RW adjacent rows per iteration and issues every load of them (dy, x and the
-  // residual gradient, kept packed) before the first cross-lane reduction: 2x the bytes in
-  // flight of a row-at-a-time loop, and the dres read no longer waits behind the reductions.
+  // residual gradient, kept packed) before the first cross-lane reduction.  The loads are
+  // branch-free -- rows past M and chunks past D read a clamped in-range address and are
+  // discarded -- so all of them are in flight together: issued under `if`s, the compiler put a
+  // vmcnt wait between every group and the row's ~20 loads paid their latency one group at a
+  // time (3.4 TB/s at D = 768).  The weight chunks are loaded once, before the row loop.
   constexpr int RW = LN_V <= 4 ? MI_LN_BWD_RW : 1;
+  float wr[LN_V][4];
+#pragma unroll
+  for (int i = 0; i < LN_V; ++i) {
+    const int c = min(lane + 64 * i, nv - 1);
+    const float4 wq = *(const float4*)(w + 4 * c);
+    wr[i][0] = wq.x; wr[i][1] = wq.y; wr[i][2] = wq.z; wr[i][3] = wq.w;
+  }
+  const bf16_t* rsrc = dres ? dres : dy;  // no residual gradient: loaded, then ignored
   for (int row0 = (blockIdx.x * 4 + wv) * RW; row0 < M; row0 += gridDim.x * 4 * RW) {
     uint2 qd[RW][LN_V], qx[RW][LN_V], qr[RW][LN_V];
     float mean[RW], rstd[RW];
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
-      const int row = row0 + r;
-      if (row < M) {
-        mean[r] = mean_in[row];
-        rstd[r] = rstd_in[row];
+      const size_t row = (size_t)min(row0 + r, M - 1);
+      mean[r] = mean_in[row];
+      rstd[r] = rstd_in[row];
 #pragma unroll
-        for (int i = 0; i < LN_V; ++i) {
-          const int c = lane + 64 * i;
-          if (c < nv) {
-            qd[r][i] = *(const uint2*)(dy + (size_t)row * D + 4 * c);
-            qx[r][i] = *(const uint2*)(x + (size_t)row * D + 4 * c);
-            qr[r][i] = dres ? *(const uint2*)(dres + (size_t)row * D + 4 * c) : make_uint2(0u, 0u);
-          }
-        }
+      for (int i = 0; i < LN_V; ++i) {
+        const int c = min(lane + 64 * i, nv - 1);
+        qd[r][i] = *(const uint2*)(dy + row * D + 4 * c);
+        qx[r][i] = *(const uint2*)(x + row * D + 4 * c);
+        qr[r][i] = *(const uint2*)(rsrc + row * D + 4 * c);
       }
     }
 #pragma unroll
@@ -128,12 +149,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
           float d[4];
           load4((const bf16_t*)&qd[r][i], d);
           load4((const bf16_t*)&qx[r][i], xh[i]);
-          const float4 wq = *(const float4*)(w + 4 * c);
-          const float wa[4] = {wq.x, wq.y, wq.z, wq.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             xh[i][e] = (xh[i][e] - mean[r]) * rstd[r];
-            g[i][e] = d[e] * wa[e];
+            g[i][e] = d[e] * wr[i][e];
             s1 += g[i][e];
             s2 += g[i][e] * xh[i][e];
             pw[i][e] += d[e] * xh[i][e];
@@ -147,8 +166,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       for (int i = 0; i < LN_V; ++i) {
         const int c = lane + 64 * i;
         if (c < nv) {
-          float o[4], rv[4];
-          load4((const bf16_t*)&qr[r][i], rv);
+          float o[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (dres) load4((const bf16_t*)&qr[r][i], rv);
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = rv[e] + rstd[r] * (g[i][e] - m1 - xh[i][e] * m2);
           store4(dxr + 4 * c, o);
@@ -168,10 +187,30 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
     __syncthreads();
-    float* dst = pass ? db : dw;
+    float* dst = rep ? rep + ((size_t)(blockIdx.x % R) * 2 + pass) * D : (pass ? db : dw);
     for (int col = threadIdx.x; col < D; col += 256)
       atomicAdd(dst + col, red[col] + red[D + col] + red[2 * D + col] + red[3 * D + col]);
   }
+}
+
+// dw[c] += sum_r rep[r][0][c], db[c] += sum_r rep[r][1][c] (fixed order), replicas zeroed again
+__global__ __launch_bounds__(256) void ln_rep_reduce_kernel(float* __restrict__ rep, int R, int D,
+                                                            float* __restrict__ dw, float* __restrict__ db) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * D) return;
+  const int pass = i / D, col = i - pass * D;
+  constexpr int RMAX = MI_LN_REPLICAS > 0 ? MI_LN_REPLICAS : 1;
+  float v[RMAX];  // every replica's load in flight at once, then the fixed-order sum
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) v[r] = r < R ? rep[((size_t)r * 2 + pass) * D + col] : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) s += v[r];
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r)
+    if (r < R) rep[((size_t)r * 2 + pass) * D + col] = 0.f;
+  float* dst = pass ? db : dw;
+  if (dst) dst[col] += s;
 }
 
 // out[n] += sum_m X[m][n] (bf16 X, row stride ld): lane owns an 8-column chunk, the block's 4
@@ -199,6 +238,34 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
     const int col = blockIdx.x * 512 + c;
     if (col < N) atomicAdd(out + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
   }
+}
+
+// [LN_REPLICAS][2][D] zeroed fp32 replicas of the LayerNorm parameter gradients, one per (device,
+// stream), grown on demand (the first call of a shape allocates and zeroes: never inside a graph
+// capture -- a warm-up step runs first); ln_rep_reduce_kernel leaves them zeroed for the next call.
+constexpr int LN_REPLICAS = MI_LN_REPLICAS;
+struct LnRep { float* p = nullptr; int D = 0; };
+static std::mutex g_lnrep_mu;
+static std::map<std::pair<int, hipStream_t>, LnRep> g_lnrep;
+static float* ln_rep_workspace(int D, hipStream_t st) {
+  if (LN_REPLICAS <= 0) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_lnrep_mu);
+  LnRep& w = g_lnrep[{dev, st}];
+  if (w.D < D) {
+    float* p = nullptr;
+    const size_t bytes = sizeof(float) * LN_REPLICAS * 2 * (size_t)D;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, bytes) != hipSuccess) return nullptr;
+    if (w.p) {
+      hipDeviceSynchronize();
+      hipFree(w.p);
+    }
+    w.p = p;
+    w.D = D;
+  }
+  return w.p;
 }
 
 }  // namespace
@@ -249,16 +316,20 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
     return cus * per_cu;
   };
   const int rw = nvec <= 4 ? MI_LN_BWD_RW : 1;
+  float* rep = (dw && db) ? ln_rep_workspace(D, st) : nullptr;
+  const int R = LN_REPLICAS;
 #define MI_LN_BWD(V)                                                                                    \
   case V:                                                                                               \
     hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(min(cdiv(M, 4 * rw), cap((const void*)ln_bwd_kernel<V>))),  \
                        dim3(256), lds, st, (const bf16_t*)dy,                                            \
-                       (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, dw, db, M, D);  \
+                       (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, dw, db, M, D,  \
+                       rep, R);                                                                          \
     break;
   switch (cdiv(D, 256)) {
     MI_LN_BWD(1) MI_LN_BWD(2) MI_LN_BWD(3) MI_LN_BWD(4) MI_LN_BWD(5) MI_LN_BWD(6) MI_LN_BWD(7) MI_LN_BWD(8)
   }
 #undef MI_LN_BWD
+  if (rep) hipLaunchKernelGGL(ln_rep_reduce_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, rep, R, D, dw, db);
   return (int)hipGetLastError();
 }
 
