@@ -43,6 +43,9 @@
 #include <mutex>
 #include <cstdlib>
 
+#ifndef MI_G256_EPI_U0
+#define MI_G256_EPI_U0 8  // plain-GEMM epilogue: row steps per group of batched operand loads (A/B)
+#endif
 #ifndef MI_FENCE_HANDOFF
 #define MI_FENCE_HANDOFF 0  // 1: tail split-K hand-off through a __threadfence pair (A/B only)
 #endif
@@ -394,9 +397,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   }
   const int cc = lane & 7;
   const int n = n0 + wn * 64 + cc * 8;
+  // plain GEMMs (MODE 0: transformer layers) never carry BN statistics or the BN-backward
+  // epilogues: compiled out, their registers go to a deeper batch of epilogue operand loads
+  constexpr bool BN_EPI = MODE != 0;
+  const bool has_stats = BN_EPI && a.stats != nullptr;
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[8];
-  if (a.epi >= 4 && a.stats && n < a.N) {
+  if (BN_EPI && a.epi >= 4 && a.stats && n < a.N) {
     *(float4*)&mu[0] = *(const float4*)(a.mean + n);
     *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
   }
@@ -415,7 +422,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     // 8 row steps in 2 groups of EPI_U: a group's global operand loads (residual C, relu source,
     // BN input) are all issued before its first store, so their HBM latency overlaps instead of
     // serialising behind each step's store (the compiler cannot move a load across a store to C)
-    constexpr int EPI_U = 4;
+    constexpr int EPI_U = MODE == 0 ? MI_G256_EPI_U0 : 4;
 #pragma unroll
     for (int s0 = 0; s0 < 8; s0 += EPI_U) {
       uint4 cv[EPI_U], yq[EPI_U], xq[EPI_U];
@@ -428,12 +435,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         ok[u] = m < a.M && n < a.N;
         offs[u] = ok[u] ? (size_t)m * a.ldc + n : 0;
         bool acc_ok = true;
-        if (ok[u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
+        if (BN_EPI && ok[u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
           const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
           const uint32_t h = fdiv(rem, a.fQ), w = rem - h * a.fQ.d;
           acc_ok = ((h | w) & 1u) == 0u;
         }
-        if (ok[u] && a.epi >= 4) {
+        if (BN_EPI && ok[u] && a.epi >= 4) {
           if (a.epi == 5) cv[u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[u]) : make_uint4(0, 0, 0, 0);
 #if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
           if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
@@ -455,7 +462,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const size_t off = offs[u];
         MI_ASSERT(n + 8 <= a.N, n);
         uint4 o = v;
-        if (a.epi >= 4) {
+        if (BN_EPI && a.epi >= 4) {
           float f[8];
           unpack8(v, f);
           if (a.epi == 5) {  // dy = this dgrad + the gradient already in C (residual sum)
@@ -479,7 +486,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
           }
         } else {
           if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[u]);
-          if (a.stats) {
+          if (has_stats) {
             float f[8];
             unpack8(v, f);
 #pragma unroll
@@ -495,7 +502,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     }
     lgkm_wait0();  // this wave's reads of the slice retire before the next quadrant row overwrites it
   }
-  if (a.stats) {
+  if (has_stats) {
     // reduce over the 8 lanes sharing a column chunk (lane >> 3), lanes 0..7 write the slab row
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
