@@ -181,6 +181,9 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16
     const int q = qt * 16 + li;
     const bool qv = q < T;
     const size_t orow = ((size_t)b * T + q) * D + h * HD;
+    // the row's LSE is loaded with its operands (clamped index, discarded past T), not after the
+    // dd reduction: issued there under `qv ?` it was a second memory round trip per query tile
+    const float lse_q = lse[(size_t)bh * T + min(q, T - 1)];
     bf16x8 qf[2], df[2];
     float dd = 0.f;
 #pragma unroll
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16
     }
     dd += __shfl_xor(dd, 16, 64);
     dd += __shfl_xor(dd, 32, 64);
-    const float l2 = qv ? lse[(size_t)bh * T + q] * LOG2E : 0.f;
+    const float l2 = qv ? lse_q * LOG2E : 0.f;
     if (qv && g == 0) dvec[(size_t)bh * T + q] = dd;
     f32x4 dq[4];
 #pragma unroll
@@ -213,8 +216,11 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          // exp evaluated unconditionally and selected: a conditional exp2f compiled to an
+          // exec-masked branch inside the key loop
           const bool valid = qv && (kt * 16 + 4 * g + r < T);
-          const float p = valid ? exp2f(s[r] * sl2 - l2) : 0.f;
+          const float e = exp2f(s[r] * sl2 - l2);
+          const float p = valid ? e : 0.f;
           ds[t][r] = p * (dp[r] - dd);
         }
       }
@@ -281,7 +287,8 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dkv_kernel(const bf1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qq = (2 * qs + t) * 16 + 4 * g + r;
-          const float p = kv ? exp2f(s[r] * sl2 - Ls[qq]) : 0.f;
+          const float e = exp2f(s[r] * sl2 - Ls[qq]);  // unconditional + select (see the dQ kernel)
+          const float p = kv ? e : 0.f;
           P[t][r] = p;
           S[t][r] = p * (dp[r] - Dv[qq]);
         }
