@@ -444,3 +444,18 @@ def test_smddp_ipc_mesh_collectives_multi_rank(world):
                        timeout=150, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("MESH_OK") == world
+
+
+@pytest.mark.skipif(REF_CODE is None, reason="reference scripts not staged (run build())")
+def test_reference_job_per_gpu_shape():
+    """tools/reference_job.py: the unmodified reference script as a local job at the reference's
+    per-GPU batch (32), one epoch, through the engine-backed DDP with graphed steps -- faster than
+    the reference's own per-A100 throughput (>= 565 img/s) by a wide margin."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "reference_job.py"), "--batch-size", "32",
+                        "--epochs", "1", "--tag", "test"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["loop_seconds"] and res["loop_seconds"] > 0
+    assert res["img_per_s_lower_bound"] > 4 * 565, res
+    assert res["final_accuracy"] is not None and res["final_accuracy"] > 0.3
