@@ -50,6 +50,9 @@
 #ifndef MI_TN_CONV_BLOCKS_PER_CU
 #define MI_TN_CONV_BLOCKS_PER_CU 3  // conv weight-gradient variant (A/B: 4)
 #endif
+#ifndef MI_REDUCE_OLD
+#define MI_REDUCE_OLD 0
+#endif
 #ifndef MI_TN_NOATOMIC
 #define MI_TN_NOATOMIC 0  // timing experiment only: split-K partials stored, not added (wrong results)
 #endif
@@ -899,11 +902,28 @@ __global__ __launch_bounds__(256) void tn_splitk_reduce_kernel(const f32x4* __re
   const int pl = threadIdx.x & (PB - 1), grp = threadIdx.x >> (8 - log2g);
   const int p = blockIdx.x * PB + pl;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+#if MI_REDUCE_OLD  // A/B build: the former loop
   if (p < PER) {
     const f32x4* src = ws + (size_t)tile * splits * PER + p;
 #pragma unroll 4
     for (int s = grp; s < splits; s += G) v += src[(size_t)s * PER];
   }
+#else
+  {
+    // 8 split reads per chunk all in flight (clamped indices, selected after the loads): the
+    // unrolled `v += src[...]` loop left a vmcnt(0) behind every other load -- a reduce of 8
+    // splits per thread paid ~8 memory latencies
+    const f32x4* src = ws + (size_t)tile * splits * PER + min(p, PER - 1);
+    for (int s0 = grp; s0 < splits; s0 += 8 * G) {
+      f32x4 r[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = src[(size_t)min(s0 + i * G, splits - 1) * PER];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (s0 + i * G < splits) v += r[i];
+    }
+  }
+#endif
   part[threadIdx.x] = v;
   __syncthreads();
   if (grp != 0 || p >= PER) return;
@@ -914,10 +934,14 @@ __global__ __launch_bounds__(256) void tn_splitk_reduce_kernel(const f32x4* __re
   const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
   const int n = n0 + wn * WN + 16 * j + li;
   if (n >= N) return;
+  // the four gradient rows read together (clamped), then written back
+  float c[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[r] = C[(size_t)min(m0 + wm * WM + 16 * i + 4 * g + r, M - 1) * ldc + n];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + wm * WM + 16 * i + 4 * g + r;
-    if (m < M) C[(size_t)m * ldc + n] += v[r];
+    if (m < M) C[(size_t)m * ldc + n] = c[r] + v[r];
   }
 }
 
