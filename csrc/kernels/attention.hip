@@ -61,6 +61,21 @@ __device__ __forceinline__ void store4bf(bf16_t* p, f32x4 v, float s) {
 // rows [0, TP) of two [T][ld] bf16 matrices (64 columns each) -> LDS [TP][KSTR], zero rows >= T.
 // All of a thread's global loads are issued before any LDS store (fully unrolled, fixed trip
 // count), so the staging costs one memory latency instead of one per 16-byte chunk.
+#ifndef MI_ATT_LIBEXP
+#define MI_ATT_LIBEXP 0  // 1: the device library's exp2f (A/B)
+#endif
+// softmax exponentials: every argument is <= 0 (scores minus the row max / the saved LSE), so
+// the hardware v_exp_f32 is exact enough and its flush of results below 2^-126 to zero is
+// harmless; the library exp2f wraps it in denormal range scaling (~10 VALU per call, 56 calls
+// per 16-query tile and wave in the forward)
+__device__ __forceinline__ float att_exp2(float x) {
+#if MI_ATT_LIBEXP
+  return exp2f(x);
+#else
+  return __builtin_amdgcn_exp2f(x);
+#endif
+}
+
 template <int TP, int NW>
 __device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, int ld0, bf16_t* dst1,
                                             const bf16_t* src1, int ld1, int T) {
@@ -133,7 +148,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_fwd_kernel(const bf16_t*
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kt][r] * sl2 - ms);
+        const float p = att_exp2(s[kt][r] * sl2 - ms);
         s[kt][r] = p;
         l += p;
       }
@@ -219,7 +234,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16
           // exp evaluated unconditionally and selected: a conditional exp2f compiled to an
           // exec-masked branch inside the key loop
           const bool valid = qv && (kt * 16 + 4 * g + r < T);
-          const float e = exp2f(s[r] * sl2 - l2);
+          const float e = att_exp2(s[r] * sl2 - l2);
           const float p = valid ? e : 0.f;
           ds[t][r] = p * (dp[r] - dd);
         }
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dkv_kernel(const bf1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qq = (2 * qs + t) * 16 + 4 * g + r;
-          const float e = exp2f(s[r] * sl2 - Ls[qq]);  // unconditional + select (see the dQ kernel)
+          const float e = att_exp2(s[r] * sl2 - Ls[qq]);  // unconditional + select (see the dQ kernel)
           const float p = kv ? e : 0.f;
           P[t][r] = p;
           S[t][r] = p * (dp[r] - Dv[qq]);
