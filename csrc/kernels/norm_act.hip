@@ -12,6 +12,7 @@
 #include "common.h"
 #include <mutex>
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -856,6 +857,140 @@ inline void launch_bn_bwd_apply(const void* dy, const void* y, const void* x, co
                        (const bf16_t*)x, coef, (bf16_t*)dx, (bf16_t*)dres, nvec, C, relu);
 }
 
+// Small BatchNorm layers (ResNet-18 on 32x32 images at 32 per GPU: 32-2048 rows): the slab
+// finalize and the apply in ONE launch.  Block (cg, rb) reduces the slab for channels
+// [64 cg, 64 cg + 64) itself -- a few KB, read by every row block of the channel group, in a fixed
+// order, so every block computes identical coefficients -- and applies them to its rows; only
+// row block 0 writes the statistics outputs (running statistics, saved mean / invstd, scale /
+// shift; backward: dgamma / dbeta).  Saves a launch and a dependent kernel boundary per BN per
+// direction (~40 per step of the reference's per-GPU shape, where each cost ~5 us).
+constexpr int SMALL_T = 256, SMALL_G = SMALL_T / 64;
+#ifndef MI_BN_SMALL_ELEMS
+#define MI_BN_SMALL_ELEMS (1 << 20)  // M * C at or below which the fused path runs (0: never)
+#endif
+
+__device__ __forceinline__ void small_slab_reduce(const float* __restrict__ part, int nblk, int C, int c, double& s,
+                                                  double& q, double (*red)[SMALL_G][64]) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int i = rg; i < nblk; i += SMALL_G) {
+      a += part[(size_t)(2 * i) * C + c];
+      b += part[(size_t)(2 * i + 1) * C + c];
+    }
+  red[0][rg][cl] = a;
+  red[1][rg][cl] = b;
+  __syncthreads();
+  s = red[0][0][cl]; q = red[1][0][cl];
+  for (int g = 1; g < SMALL_G; ++g) { s += red[0][g][cl]; q += red[1][g][cl]; }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(SMALL_T) void bn_small_fin_apply_kernel(const bf16_t* __restrict__ x,
+                                                                     const bf16_t* __restrict__ res_or_dz,
+                                                                     bf16_t* __restrict__ out, const float* part,
+                                                                     int nblk, FinArgs f, int rows_per, int relu) {
+  __shared__ double red[2][SMALL_G][64];
+  __shared__ float k[3][64];
+  const int C = f.C, M = f.M;
+  const int cl = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + cl;
+  double s, q;
+  small_slab_reduce(part, nblk, C, c, s, q, red);
+  if (threadIdx.x < 64 && c < C) {
+    // every row block computes the same coefficients; row block 0 also publishes the outputs
+    float tmp[3];
+    if (BWD) {
+      const float is = f.invstd[c];
+      const float sum_dz = (float)s, sum_dzx = (float)q * is;
+      const float gm = f.gamma ? f.gamma[c] : 1.f;
+      const float k0 = gm * is, mdz = sum_dz / M, mdzx = sum_dzx / M;
+      const float k1 = -k0 * is * mdzx;
+      tmp[0] = k0; tmp[1] = k1; tmp[2] = -k0 * mdz - k1 * f.mean[c];
+      if (blockIdx.y == 0) {
+        if (f.dgamma) f.dgamma[c] += sum_dzx;
+        if (f.dbeta) f.dbeta[c] += sum_dz;
+      }
+    } else {
+      const double mean = s / M;
+      double var = q / M - mean * mean;
+      if (var < 0) var = 0;
+      const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+      const float gm = f.gamma ? f.gamma[c] : 1.f, bt = f.beta ? f.beta[c] : 0.f;
+      tmp[0] = gm * invstd;
+      tmp[1] = bt - (float)mean * gm * invstd;
+      tmp[2] = 0.f;
+      if (blockIdx.y == 0) {
+        f.save_mean[c] = (float)mean;
+        f.save_invstd[c] = invstd;
+        f.scale[c] = tmp[0];
+        f.shift[c] = tmp[1];
+        if (f.rmean) {
+          const double unbiased = M > 1 ? var * M / (M - 1) : var;
+          f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (float)mean;
+          f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * (float)unbiased;
+        }
+        if (cl == 0 && blockIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+      }
+    }
+    k[0][cl] = tmp[0]; k[1][cl] = tmp[1]; k[2][cl] = tmp[2];
+  }
+  __syncthreads();
+  // apply: 8 threads per row (8 channels each), 32 rows per pass
+  const int ch = (threadIdx.x & 7) * 8, rsub = threadIdx.x >> 3;
+  const int cbase = blockIdx.x * 64 + ch;
+  if (cbase >= C) return;
+  float a0[8], a1[8], a2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a0[j] = k[0][ch + j]; a1[j] = k[1][ch + j]; a2[j] = k[2][ch + j]; }
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  for (int r = r0 + rsub; r < r1; r += SMALL_T / 8) {
+    const size_t off = (size_t)r * C + cbase;
+    float v[8], o[8];
+    unpack8(*(const uint4*)(x + off), v);
+    if (BWD) {  // dx = k0 dz + k1 x + k2
+      float d[8];
+      unpack8(*(const uint4*)(res_or_dz + off), d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = a0[j] * d[j] + a1[j] * v[j] + a2[j];
+    } else {   // y = act(x scale + shift (+ res))
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[j] * a0[j] + a1[j];
+      if (res_or_dz) {
+        float rv[8];
+        unpack8(*(const uint4*)(res_or_dz + off), rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += rv[j];
+      }
+      if (relu)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    *(uint4*)(out + off) = pack8(o);
+  }
+}
+
+static int64_t g_bn_small_elems = -1;  // MI355X_DP_BN_SMALL_ELEMS, or mi_bn_set_small_elems (tests)
+inline bool bn_small(int M, int C, int nblk) {
+  if (g_bn_small_elems < 0) {
+    const char* e = std::getenv("MI355X_DP_BN_SMALL_ELEMS");
+    g_bn_small_elems = e ? std::max(0LL, std::atoll(e)) : (int64_t)MI_BN_SMALL_ELEMS;
+  }
+  return (int64_t)M * C <= g_bn_small_elems && C % 64 == 0 && nblk <= 256 && M > 0;
+}
+
+inline void launch_bn_small(bool bwd, const void* x, const void* res_or_dz, void* out, const float* part, int nblk,
+                            const FinArgs& f, int relu, hipStream_t st) {
+  const int rows_per = 128;
+  const dim3 grid(cdiv(f.C, 64), cdiv(f.M, rows_per));
+  if (bwd)
+    hipLaunchKernelGGL(bn_small_fin_apply_kernel<true>, grid, dim3(SMALL_T), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)res_or_dz, (bf16_t*)out, part, nblk, f, rows_per, relu);
+  else
+    hipLaunchKernelGGL(bn_small_fin_apply_kernel<false>, grid, dim3(SMALL_T), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)res_or_dz, (bf16_t*)out, part, nblk, f, rows_per, relu);
+}
+
 inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3& grid) {
   SlabGeom g = slab_geom(C);
   int ncs = C / g.cw;
@@ -964,6 +1099,12 @@ inline FinArgs fin_bwd_args(int M, int C, const float* gamma, const float* mean,
 
 MI_API int mi_bn_slab_extra_rows() { return SLAB_EXTRA_ROWS; }
 
+// threshold (M * C elements) of the fused small-layer finalize + apply path; 0 disables (tests)
+MI_API int mi_bn_set_small_elems(long long n) {
+  g_bn_small_elems = n < 0 ? 0 : (int64_t)n;
+  return 0;
+}
+
 // Allocate the current device's finalize-counter table (zeroed, synchronously).  Idempotent; call
 // before any graph capture (the Python loader does, at library load).
 MI_API int mi_bn_init_counters() {
@@ -1001,8 +1142,13 @@ MI_API int mi_bn_fwd_train(const void* x, const void* res, void* y, int M, int C
   } else {
     hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)x, part, M, C, rpb);
   }
-  slab_finalize<false>(part, nblk, fin_fwd_args(M, C, eps, momentum, gamma, beta, rmean, rvar, nbt, save_mean,
-                                               save_invstd, scale, shift), st);
+  const FinArgs fa = fin_fwd_args(M, C, eps, momentum, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd, scale,
+                                  shift);
+  if (y && bn_small(M, C, nblk)) {  // finalize + apply in one launch
+    launch_bn_small(false, x, res, y, part, nblk, fa, relu, st);
+    return (int)hipGetLastError();
+  }
+  slab_finalize<false>(part, nblk, fa, st);
   if (!y) return (int)hipGetLastError();  // statistics + coefficients only (the consumer applies them)
   int64_t nvec = (int64_t)M * C / 8;
   launch_bn_apply<false>(x, res, y, scale, shift, nullptr, nullptr, nvec, C, relu, st);
@@ -1053,7 +1199,12 @@ MI_API int mi_bn_bwd_train_pre(const void* dz, const void* x, void* dx, void* dr
                                const float* save_mean, const float* save_invstd, float* dgamma, float* dbeta,
                                float* coef, float* part, int pre_rows, hipStream_t st) {
   if (C % 8 != 0 || pre_rows <= 0) return (int)hipErrorInvalidValue;
-  slab_finalize<true>(part, pre_rows, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
+  const FinArgs fb = fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  if (!dres && bn_small(M, C, pre_rows)) {  // finalize + apply in one launch
+    launch_bn_small(true, x, dz, dx, part, pre_rows, fb, 0, st);
+    return (int)hipGetLastError();
+  }
+  slab_finalize<true>(part, pre_rows, fb, st);
   int64_t nvec = (int64_t)M * C / 8;
   launch_bn_bwd_apply(dz, nullptr, x, coef, dx, dres, nvec, C, 0, st);
   return (int)hipGetLastError();

@@ -27,6 +27,7 @@ signature("mi_create_cu_masked_stream", I, I, P)
 # norm_act.hip
 signature("mi_bn_partial_rows", I, I)
 signature("mi_bn_slab_extra_rows")
+signature("mi_bn_set_small_elems", L)
 signature("mi_bn_init_counters")
 signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_bn_apply_dual", P, P, P, I, I, P, P, P, P, I, P)

@@ -502,3 +502,34 @@ def test_conv_splitk_small_grids(shape):
         assert rel_err(dw, wr.grad) < 2e-2, blocks
     assert rel_err(out[128][0], out[0][0]) < 1e-2
     assert rel_err(out[128][1], out[0][1]) < 1e-2
+
+
+def test_bn_small_fused_matches_two_launch():
+    """BatchNorm finalize fused into the apply for small layers (norm_act.hip bn_small_fin_apply_kernel,
+    the reference's per-GPU shape: ResNet-18 on 32x32 at batch 32) == the two-launch path: loss,
+    every gradient, running statistics and num_batches_tracked."""
+    from mi355x_dp.models import get_model
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.parallel import DataParallel
+    lib = _lib.load(True)
+    res = {}
+    try:
+        for elems in (1 << 20, 0):
+            lib.mi_bn_set_small_elems(elems)
+            torch.manual_seed(0)
+            eng = DataParallel(get_model("resnet18", num_classes=10).cuda(), wgrad_stream=False)
+            g = torch.Generator().manual_seed(1)
+            x = torch.randn(32, 3, 32, 32, generator=g).cuda()
+            y = torch.randint(0, 10, (32,), generator=g).cuda()
+            loss = F.cross_entropy(eng(x).float(), y)
+            loss.backward()
+            torch.cuda.synchronize()
+            res[elems] = (float(loss), eng.flat.grad.clone(), eng.buffers.data.clone(),
+                          [b.clone() for b in eng.buffers.others])
+    finally:
+        lib.mi_bn_set_small_elems(1 << 20)
+    (l1, g1, b1, o1), (l0, g0, b0, o0) = res[1 << 20], res[0]
+    assert l1 == pytest.approx(l0, rel=1e-4)
+    assert rel_l2(g1, g0) < 1e-2
+    assert rel_err(b1, b0) < 1e-4
+    assert all(torch.equal(a, b) for a, b in zip(o1, o0))
