@@ -107,6 +107,7 @@ struct NTArgs {
   // splits in order and run the ordinary epilogue
   float* ws;
   int splits, ksplit;
+  int* cnt;          // SPLIT 3: per-tile arrival counters (zero between launches)
   ConvGeom g;
 };
 
@@ -162,6 +163,8 @@ constexpr int nt_occupancy() {
 template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false, int SPLIT = 0>
 __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_kernel(NTArgs a) {
   static_assert(SPLIT == 0 || (STAGES == 1 && !SMALLC && !HALO), "split-K: single-stage gather/plain tiles only");
+  // SPLIT 3: as SPLIT 1, then the last-arriving split of each tile sums all the partial tiles (in
+  // split order) and runs the epilogue -- one launch instead of SPLIT 1 + SPLIT 2
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   // wave-uniform k position: gather-space tap (kr, ks) and channel-chunk base kc
   int kr = 0, ks = 0, kc = 0;
   int kt0 = 0;  // first k-step of this block (split-K)
-  if constexpr (SPLIT == 1) {
+  if constexpr (SPLIT == 1 || SPLIT == 3) {
     kt0 = blockIdx.z * a.ksplit;
     nk = min(nk, kt0 + a.ksplit);
     if (a.mode != 0) {  // (kr, ks, kc) of k-step kt0: channel chunks fastest, then taps of a row
@@ -488,6 +491,54 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
 #pragma unroll
       for (int j = 0; j < NJ; ++j) dst[(size_t)(i * NJ + j) * 256] = acc[i][j];
     return;
+  }
+  if constexpr (SPLIT == 3) {
+    // fence-free hand-off to the last-arriving split (MI355X_MICROARCH.md, first table row; as
+    // gemm256.hip's tail split-K): every wave stores its partial with sc1 and waits for the
+    // stores, one lane counts the arrival behind a barrier, the last arriver reads with sc1
+    const int tl = cy * gridDim.x + tile;
+    constexpr int FR = MI * NJ * 256;  // f32x4 per partial tile
+    const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
+        a.ws + (size_t)tl * a.splits * FR * 4, (short)0, a.splits * FR * 16, 0x00020000);
+    constexpr int SC1 = 16;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rsw,
+                                               (uint32_t)(((blockIdx.z * MI * NJ + i * NJ + j) * 256 + tid) * 16), 0, SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int last_flag;
+    if (tid == 0) last_flag = atomicAdd(a.cnt + tl, 1) == a.splits - 1;
+    __syncthreads();
+    if (!last_flag) return;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int ZU = (MI * NJ) <= 4 ? 4 : ((MI * NJ) <= 8 ? 2 : 1);
+    for (int z0 = 0; z0 < a.splits; z0 += ZU) {
+      f32x4 r[ZU][MI][NJ];
+#pragma unroll
+      for (int u = 0; u < ZU; ++u) {
+        const int z = min(z0 + u, a.splits - 1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            r[u][i][j] = __builtin_amdgcn_raw_buffer_load_b128(
+                rsw, (uint32_t)(((z * MI * NJ + i * NJ + j) * 256 + tid) * 16), 0, SC1);
+      }
+#pragma unroll
+      for (int u = 0; u < ZU; ++u)
+        if (z0 + u < a.splits)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] += r[u][i][j];
+    }
+    if (tid == 0) a.cnt[tl] = 0;  // ready for the next launch (stream order)
   }
 
   // output row offset (elements) of tile row m
@@ -1050,6 +1101,7 @@ static int nt_stages() {
 }
 
 static float* splitk_workspace(size_t floats, hipStream_t st);
+static int* splitk_counters(hipStream_t st);
 
 // split-K of the NT kernel for small grids: a layer-4 conv of ResNet-18 on 32x32 images at batch
 // 32 is 8 output tiles of 72 k-steps each -- 8 of 256 CUs walking a latency-bound serial chain.
@@ -1058,6 +1110,16 @@ static float* splitk_workspace(size_t floats, hipStream_t st);
 // stream's slab workspace and a second launch sums them in split order and runs the epilogue.
 // MI355X_DP_NT_SPLITK=0 disables.
 static int g_nt_split_blocks = -1;
+// MI355X_DP_NT_SPLIT_FUSED=0: the two-launch split-K (partials, then a reduce + epilogue launch)
+static int g_nt_split_fused = -1;
+static bool nt_split_fused() {
+  if (g_nt_split_fused < 0) {
+    const char* e = std::getenv("MI355X_DP_NT_SPLIT_FUSED");
+    g_nt_split_fused = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_nt_split_fused != 0;
+}
+constexpr int SPLITK_COUNTERS = 4096;
 static int nt_split_blocks() {
   if (g_nt_split_blocks < 0) {
     const char* e = std::getenv("MI355X_DP_NT_SPLITK");
@@ -1090,6 +1152,12 @@ hipError_t launch_nt(NTArgs& a, hipStream_t st) {
       a.ksplit = cdiv(nk, splits);
       a.splits = cdiv(nk, a.ksplit);
       a.ws = splitk_workspace((size_t)grid * classes * a.splits * BM * BN, st);
+      a.cnt = nt_split_fused() ? splitk_counters(st) : nullptr;
+      if (a.ws && a.cnt && grid * classes <= SPLITK_COUNTERS) {
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, false, 3>), dim3(grid, classes, a.splits), dim3(256), 0, st,
+                           a);
+        return hipGetLastError();
+      }
       if (a.ws) {
         hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, false, 1>), dim3(grid, classes, a.splits), dim3(256), 0, st,
                            a);
@@ -1212,6 +1280,22 @@ static float* splitk_workspace(size_t floats, hipStream_t st) {
     w.n = n;
   }
   return w.p;
+}
+// per-tile arrival counters of the fused NT split-K (SPLIT 3), one zeroed table per (device, slot)
+// like the slab workspace; allocated on first use (a warm-up step runs before any capture) and
+// left zeroed by every launch's last arrivers
+static int* g_splitk_cnt[16][3];
+static int* splitk_counters(hipStream_t st) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_splitk_mu);
+  const int slot = st == nullptr ? 0 : st == g_wgrad_stream[dev & 15] ? 1 : st == g_aux_stream[dev & 15] ? 2 : 0;
+  int*& p = g_splitk_cnt[dev & 15][slot];
+  if (!p) {
+    if (hipMalloc(&p, sizeof(int) * SPLITK_COUNTERS) != hipSuccess) { p = nullptr; return nullptr; }
+    if (hipMemset(p, 0, sizeof(int) * SPLITK_COUNTERS) != hipSuccess) return nullptr;
+  }
+  return p;
 }
 // the same per-stream slab workspace for the other kernels of this library that reduce per-block
 // partials deterministically (stem_conv.hip's weight gradient); nullptr -> their atomic path
@@ -1337,6 +1421,12 @@ MI_API int mi_set_tn_slabs(int on) {
 
 MI_API int mi_set_glds(int on) {
   g_nt_glds = on ? 1 : 0;
+  return 0;
+}
+
+// NT split-K reduction: 1 = fused last-arriver launch (default), 0 = partials + reduce launch (tests).
+MI_API int mi_set_nt_split_fused(int on) {
+  g_nt_split_fused = on ? 1 : 0;
   return 0;
 }
 

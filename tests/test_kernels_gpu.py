@@ -481,27 +481,35 @@ def test_conv_splitk_small_grids(shape):
     out = {}
     lib = _lib.load(True)
     try:
-        for blocks in (128, 0):  # split-K on (default threshold), off
+        # split-K fused (default: last-arriving split reduces + epilogue), two-launch, off
+        for blocks, fused in ((128, 1), (-1, 0), (0, 1)):
+            lib.mi_set_nt_split_fused(fused)
+            blocks = 128 if blocks < 0 else blocks
+            key = (blocks, fused)
             lib.mi_set_nt_split_blocks(blocks)
             x = x0.clone().requires_grad_(True)
             w = w0.clone().requires_grad_(True)
             y = conv2d(x, w, None, s, p)
             gy = torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(3))
             y.backward(gy.to(BF).contiguous(memory_format=CL))
-            out[blocks] = (y.detach().float(), x.grad.float(), w.grad.float(), gy)
+            out[key] = (y.detach().float(), x.grad.float(), w.grad.float(), gy)
     finally:
         lib.mi_set_nt_split_blocks(128)
+        lib.mi_set_nt_split_fused(1)
     xr = x0.float().requires_grad_(True)
     wr = w0.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, None, s, p)
-    yr.backward(out[128][3].to(BF).float())
-    for blocks in (128, 0):
-        y, dx, dw, _ = out[blocks]
-        assert rel_err(y, yr) < 1e-2, blocks
-        assert rel_err(dx, xr.grad) < 2e-2, blocks
-        assert rel_err(dw, wr.grad) < 2e-2, blocks
-    assert rel_err(out[128][0], out[0][0]) < 1e-2
-    assert rel_err(out[128][1], out[0][1]) < 1e-2
+    yr.backward(out[(128, 1)][3].to(BF).float())
+    for key in out:
+        y, dx, dw, _ = out[key]
+        assert rel_err(y, yr) < 1e-2, key
+        assert rel_err(dx, xr.grad) < 2e-2, key
+        assert rel_err(dw, wr.grad) < 2e-2, key
+    assert rel_err(out[(128, 1)][0], out[(0, 1)][0]) < 1e-2
+    assert rel_err(out[(128, 1)][1], out[(0, 1)][1]) < 1e-2
+    # the fused last-arriver reduction adds the same partials in the same order as the reduce launch
+    assert torch.equal(out[(128, 1)][0], out[(128, 0)][0])
+    assert torch.equal(out[(128, 1)][1], out[(128, 0)][1])
 
 
 def test_bn_small_fused_matches_two_launch():
