@@ -669,7 +669,7 @@ class DataParallel(nn.Module):
         """Replay of the captured forward (+ its backward at ``loss.backward()``) for a small,
         launch-bound step (parallel/step_graph.py); None: run the module eagerly."""
         from . import step_graph
-        if not step_graph.eligible(self, args, kwargs):
+        if self.__dict__.get("_graph_disabled") or not step_graph.eligible(self, args, kwargs):
             return None
         x = args[0]
         key = step_graph.signature(x)
@@ -680,7 +680,14 @@ class DataParallel(nn.Module):
             seen[key] = seen.get(key, 0) + 1
             if seen[key] <= step_graph.AFTER:
                 return None
-            st = graphs[key] = step_graph.CapturedStep(self, x)
+            try:
+                st = graphs[key] = step_graph.CapturedStep(self, x)
+            except Exception as e:  # never fail a training step over the optimisation: run eagerly
+                import warnings
+                self._graph_disabled = True
+                warnings.warn(f"mi355x_dp: graph capture of the forward/backward failed ({e!r}); "
+                              "running this engine eagerly", stacklevel=3)
+                return None
         elif any(g.busy() for g in graphs.values()):
             return None
         tok = self.__dict__.get("_graph_token")
