@@ -43,3 +43,14 @@ def test_docs_site_builds(tmp_path):
     assert 'src="../images/xgmi_mesh.svg"' in concepts
     appendix = open(os.path.join(out, "Appendix", "index.html")).read()
     assert 'class="run-local"' in appendix and "build_docs.py" in appendix
+
+
+def test_docs_notice_shortcode():
+    """the learn theme's notice admonitions (reference content uses tip / info / warning)"""
+    import build_docs
+    from markdown_it import MarkdownIt
+    md = MarkdownIt("commonmark", {"html": True})
+    out = build_docs._shortcodes("a\n\n{{% notice warning %}}\nNeeds **8** GPUs.\n{{% /notice %}}\n\n"
+                                 "{{% notice bogus %}}x{{% /notice %}}", md)
+    assert '<div class="notice notice-warning"><p class="notice-title">Warning</p><p>Needs <strong>8</strong>' in out
+    assert 'notice notice-note' in out and "{{%" not in out

@@ -21,7 +21,8 @@ plus markdown-it).
   ``{{< tabs >}}{{< tab name="..." >}}...{{< /tab >}}{{< /tabs >}}`` renders a tab set (CSS radio
   tabs, no JavaScript); ``{{< mermaid >}}...{{< /mermaid >}}`` keeps the diagram source in a
   ``<pre class="mermaid">`` block (rendered by mermaid.js where a page loads it, readable as text
-  otherwise); ``{{< year >}}`` and ``{{< github repo="..." >}}``;
+  otherwise); ``{{< year >}}`` and ``{{< github repo="..." >}}``; ``{{% notice tip|info|note|warning %}}
+  ...{{% /notice %}}`` renders a coloured admonition with a markdown body;
 * a table of contents per page from its ``##`` / ``###`` headings (the reference's ``toc`` partial);
 * links: ``x.md`` -> ``x.html`` and root-relative ``/...`` made page-relative (``relative_urls``).
 """
@@ -177,6 +178,9 @@ def _run_local_box(cmd):
 
 
 _TABSET = [0]
+# the learn theme's ``{{% notice <kind> %}}...{{% /notice %}}`` admonitions (reference content uses
+# tip / info / warning, e.g. content/2_distributed_training/pytorch_smddp_dist_training.md:6-20)
+_NOTICE_KINDS = {"note": "Note", "info": "Info", "tip": "Tip", "warning": "Warning"}
 
 
 def _shortcodes(text, md=None):
@@ -191,6 +195,12 @@ def _shortcodes(text, md=None):
     text = re.sub(r'\{\{<\s*github\s+repo="([^"]*)"\s*>\}\}',
                   lambda m: f'<a class="github" href="https://github.com/{html.escape(m.group(1))}">'
                             f'{html.escape(m.group(1))}</a>', text)
+
+    def notice(m):
+        kind = m.group(1) if m.group(1) in _NOTICE_KINDS else "note"
+        inner = md.render(m.group(2).strip()) if md is not None else html.escape(m.group(2).strip())
+        return f'<div class="notice notice-{kind}"><p class="notice-title">{_NOTICE_KINDS[kind]}</p>{inner}</div>'
+    text = re.sub(r'\{\{%\s*notice\s+(\w+)\s*%\}\}(.*?)\{\{%\s*/notice\s*%\}\}', notice, text, flags=re.S)
 
     def mermaid(m):
         return f'<pre class="mermaid">{html.escape(m.group(1).strip())}</pre>'
