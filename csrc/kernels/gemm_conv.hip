@@ -122,6 +122,7 @@ struct TNArgs {
   int a_bytes, b_bytes;
   float* colsum;    // optional [M] fp32 += column sums of A (a Linear layer's bias gradient)
   float* ws;        // split-K partial slabs [tiles][splits][BM*BN] (fragment order), or null: atomics
+  int* cnt;         // per-tile arrival counters: the last-arriving split sums the slabs (no reduce launch)
   ConvGeom g;
 };
 
@@ -916,6 +917,69 @@ void tn_kernel(TNArgs a) {
     // split-K: this block's partial tile goes to its own slab in fragment order -- every store is one
     // fully coalesced 1 KB wave-instruction (64 lanes x float4) -- and tn_splitk_reduce_kernel sums
     // the splits into C: deterministic, and no fp32 atomics (~1.3 TB/s chip-wide) on the hot path
+    if (STAGES == 1 && !CS && a.cnt) {  // GLDS (default) slab variants only (no colsum: no slabs there)
+      // one launch: fence-free hand-off to the last-arriving split of the tile (as nt_kernel's
+      // SPLIT 3): sc1 partial stores, wait, barrier, one arrival count; the last arriver sums the
+      // partials in split order from 0 -- what tn_splitk_reduce_kernel does for fewer than 8
+      // splits (one split group), so both paths are bit-identical
+      constexpr int FR = BM * BN / 4;  // f32x4 per partial tile
+      constexpr int SC1 = 16;
+      const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
+          a.ws + (size_t)tile * nsplit * FR * 4, (short)0, nsplit * FR * 16, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              acc[i][j], rsw, (uint32_t)((split * FR + ((i * NJ + j) * 4 + wid) * 64 + lane) * 16), 0, SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      __shared__ int last_flag;
+      if (tid == 0) last_flag = atomicAdd(a.cnt + tile, 1) == nsplit - 1;
+      __syncthreads();
+      if (!last_flag) return;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // half a partial tile's fragments in flight at a time: the whole tile's (64 VGPRs next to
+      // the 64 accumulators) spilled the 3-blocks-per-CU conv variant
+      constexpr int IU = MI >= 2 ? MI / 2 : 1;
+      for (int z = 0; z < nsplit; ++z) {
+#pragma unroll
+        for (int i0 = 0; i0 < MI; i0 += IU) {
+          f32x4 r[IU][NJ];
+#pragma unroll
+          for (int i = 0; i < IU; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              r[i][j] = __builtin_amdgcn_raw_buffer_load_b128(
+                  rsw, (uint32_t)((z * FR + (((i0 + i) * NJ + j) * 4 + wid) * 64 + lane) * 16), 0, SC1);
+#pragma unroll
+          for (int i = 0; i < IU; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i0 + i][j] += r[i][j];
+        }
+      }
+      if (tid == 0) a.cnt[tile] = 0;  // ready for the next launch (stream order)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = n0 + wn * WN + 16 * j + li;
+          if (n >= a.N) continue;
+          float c[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c[r] = a.C[(size_t)min(m0 + wm * WM + 16 * i + 4 * g + r, a.M - 1) * a.ldc + n];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WM + 16 * i + 4 * g + r;
+            if (m < a.M) a.C[(size_t)m * a.ldc + n] = c[r] + acc[i][j][r];
+          }
+        }
+      }
+      return;
+    }
     f32x4* slab = (f32x4*)a.ws + ((size_t)tile * nsplit + split) * (BM * BN / 4);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -1120,6 +1184,19 @@ static bool nt_split_fused() {
   return g_nt_split_fused != 0;
 }
 constexpr int SPLITK_COUNTERS = 4096;
+// TN (weight-gradient) split-K reduced by the last-arriving split, opt-in (MI355X_DP_TN_SPLIT_FUSED=1).
+// Bit-identical to the reduce launch but not faster: ResNet-50 / -152 bs256 neutral (12,617 vs
+// 12,627, 5,523 vs 5,521 img/s), ResNet-18 @ 32x32 bs32 graphed -4 % (26.1k vs 27.4k, three
+// interleaved pairs, profiles/raw/r3_tnf*.log) -- one block summing up to 7 partial tiles is a
+// longer tail than the chip-wide reduce kernel
+static int g_tn_split_fused = -1;
+static bool tn_split_fused() {
+  if (g_tn_split_fused < 0) {
+    const char* e = std::getenv("MI355X_DP_TN_SPLIT_FUSED");
+    g_tn_split_fused = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_tn_split_fused != 0;
+}
 static int nt_split_blocks() {
   if (g_nt_split_blocks < 0) {
     const char* e = std::getenv("MI355X_DP_NT_SPLITK");
@@ -1321,9 +1398,13 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
              a.M, a.N, a.K, a.g.Cs, a.g.R, a.g.stride, 0, 0, tiles, splits);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
   a.ws = nullptr;
+  a.cnt = nullptr;
   if (splits > 1 && a.colsum == nullptr && tn_slabs_on())
     a.ws = splitk_workspace((size_t)tiles * splits * BM * BN, st);
+  // fewer than 8 splits: the reduce is one split group (in-order sum), which the last-arriving
+  // split runs itself -- no reduce launch; more splits keep the chip-wide reduce kernel
   const int st_n = glds_on() ? 1 : 2;
+  if (a.ws && splits < 8 && tiles <= SPLITK_COUNTERS && st_n == 1 && tn_split_fused()) a.cnt = splitk_counters(st);
   if (a.mode == 1) {
     if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
@@ -1334,7 +1415,7 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
     if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 0, false>), dim3(tiles * splits), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 0, false>), dim3(tiles * splits), dim3(256), 0, st, a);
   }
-  if (a.ws) {
+  if (a.ws && !a.cnt) {
     // split groups per position: ~8 slab reads per thread, at most 64 groups, and enough blocks
     int log2g = 0;
     while (log2g < 6 && (splits >> (log2g + 3)) > 0) ++log2g;
@@ -1425,6 +1506,10 @@ MI_API int mi_set_glds(int on) {
 }
 
 // NT split-K reduction: 1 = fused last-arriver launch (default), 0 = partials + reduce launch (tests).
+MI_API int mi_set_tn_split_fused(int on) {
+  g_tn_split_fused = on ? 1 : 0;
+  return 0;
+}
 MI_API int mi_set_nt_split_fused(int on) {
   g_nt_split_fused = on ? 1 : 0;
   return 0;

@@ -14,6 +14,7 @@ signature("mi_set_glds", I)
 signature("mi_set_nt_stages", I)
 signature("mi_set_nt_split_blocks", I)
 signature("mi_set_nt_split_fused", I)
+signature("mi_set_tn_split_fused", I)
 signature("mi_conv2d_dgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_wgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv_wtrans", P, P, I, I, I, P)

@@ -541,3 +541,37 @@ def test_bn_small_fused_matches_two_launch():
     assert rel_l2(g1, g0) < 1e-2
     assert rel_err(b1, b0) < 1e-4
     assert all(torch.equal(a, b) for a, b in zip(o1, o0))
+
+
+@pytest.mark.parametrize("shape", [(32, 512, 7, 512, 3, 1, 1), (16, 512, 14, 512, 3, 2, 1)])
+def test_tn_splitk_fused_reduce_bit_identical(shape):
+    """Weight gradient with fewer than 8 K-splits: the last-arriving split sums the partial slabs
+    (one launch) -- bit-identical to the separate reduce launch, and close to fp32."""
+    from mi355x_dp.ops import _lib, conv2d
+    N, C, H, K, R, s, p = shape
+    torch.manual_seed(4)
+    x0 = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    w0 = (torch.randn(K, C, R, R, device="cuda") * (2.0 / (C * R * R)) ** 0.5).to(BF).float()
+    w0 = w0.contiguous(memory_format=CL)
+    gy = None
+    out = {}
+    lib = _lib.load(True)
+    try:
+        for fused in (1, 0, 1):
+            lib.mi_set_tn_split_fused(fused)
+            x = x0.clone().requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            y = conv2d(x, w, None, s, p)
+            if gy is None:
+                gy = torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(5)).to(BF)
+            y.backward(gy.contiguous(memory_format=CL))
+            torch.cuda.synchronize()
+            out.setdefault(fused, []).append(w.grad.float().clone())
+    finally:
+        lib.mi_set_tn_split_fused(0)  # the default (opt-in path)
+    assert torch.equal(out[1][0], out[0][0])
+    assert torch.equal(out[1][0], out[1][1])  # counters were left zeroed by the first fused launch
+    xr = x0.float().requires_grad_(True)
+    wr = w0.clone().requires_grad_(True)
+    F.conv2d(xr, wr, None, s, p).backward(gy.float())
+    assert rel_err(out[1][0], wr.grad) < 2e-2
