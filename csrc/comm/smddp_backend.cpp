@@ -397,7 +397,8 @@ class SmddpBackend : public c10d::Backend {
     const int64_t S = out.numel();
     const size_t esz = in.element_size();
     const int dt = in.scalar_type() == at::kFloat ? 0 : 4;
-    const int64_t per = std::max<int64_t>(1, (int64_t)(ipc_cap_ / esz / size_) & ~(int64_t)3);
+    // a multiple of 8 elements: every piece of a chunk starts 16-byte aligned in the slot
+    const int64_t per = std::max<int64_t>(8, (int64_t)(ipc_cap_ / esz / size_) & ~(int64_t)7);
     for (int64_t off = 0; off < S || (S == 0 && off == 0); off += per) {
       const int64_t cnt = std::min(per, S - off);
       const uint32_t epoch = ++ipc_epoch_;

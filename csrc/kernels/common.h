@@ -6,6 +6,36 @@
 
 #define MI_API extern "C" __attribute__((visibility("default")))
 
+#include <cstdio>
+#include <mutex>
+#include <vector>
+
+// ---- workspaces and captured HIP graphs (host side)
+// A HIP graph bakes in the device pointers of every workspace its kernels used at capture time.
+// A workspace that grows therefore never frees its old buffer: it is retired (kept allocated for
+// the life of the process) so that any graph captured earlier still replays into live memory, and
+// growth needs no device synchronisation.  A workspace that would have to grow INSIDE a capture
+// does not (no allocation may happen there): the caller falls back to its workspace-free schedule
+// and says so once on stderr.
+inline void mi_ws_retire(void* p) {
+  static std::mutex mu;
+  static std::vector<void*> retired;
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(mu);
+  retired.push_back(p);
+}
+inline bool mi_stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &s) == hipSuccess && s != hipStreamCaptureStatusNone;
+}
+inline void mi_ws_capture_warn(const char* what) {
+  static bool once = false;
+  if (once) return;
+  once = true;
+  fprintf(stderr, "[mi355x_dp] %s workspace would have to grow inside a HIP graph capture: using the "
+          "workspace-free schedule for this launch (run one eager step of the shape before capturing)\n", what);
+}
+
 // Device-side invariant checks of the debug build (-DMI_DEBUG, MI355X_DP_DEBUG_KERNELS=1): print
 // the failing condition with the block / thread and a value, then trap.  Compiled out otherwise.
 #ifdef MI_DEBUG

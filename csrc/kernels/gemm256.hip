@@ -768,23 +768,33 @@ static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
     // host-blocking takeover of another stream's slot, which would abort a graph capture)
     if (!wp) split = 1;
   }
+  const size_t need = (size_t)tail * split * G_BM * G_BN;
+  // growth inside a graph capture: no allocation there -- the unsplit schedule (common.h)
+  if (split > 1 && (wp->ws_floats < need || wp->cnt_n < tail) && mi_stream_capturing(st)) {
+    mi_ws_capture_warn("gemm256 tail split-K");
+    split = 1;
+  }
   a.full_blocks = split > 1 ? full : tiles;
   a.tail_split = split;
   if (split <= 1) return hipSuccess;
   TailWs& w = *wp;
-  const size_t need = (size_t)tail * split * G_BM * G_BN;
+  // a grown buffer retires the old one (graphs captured earlier may still replay into it)
   if (w.ws_floats < need) {
-    if (w.ws) hipFree(w.ws);
-    hipError_t e = hipMalloc(&w.ws, need * sizeof(float));
-    if (e != hipSuccess) { w.ws = nullptr; w.ws_floats = 0; return e; }
+    float* p = nullptr;
+    hipError_t e = hipMalloc(&p, need * sizeof(float));
+    if (e != hipSuccess) return e;
+    mi_ws_retire(w.ws);
+    w.ws = p;
     w.ws_floats = need;
   }
   if (w.cnt_n < tail) {
-    if (w.cnt) hipFree(w.cnt);
-    hipError_t e = hipMalloc(&w.cnt, sizeof(int) * tail);
-    if (e != hipSuccess) { w.cnt = nullptr; w.cnt_n = 0; return e; }
-    hipMemset(w.cnt, 0, sizeof(int) * tail);
+    int* p = nullptr;
+    hipError_t e = hipMalloc(&p, sizeof(int) * tail);
+    if (e != hipSuccess) return e;
+    hipMemset(p, 0, sizeof(int) * tail);
     hipDeviceSynchronize();
+    mi_ws_retire(w.cnt);
+    w.cnt = p;
     w.cnt_n = tail;
   }
   a.ws = w.ws;
@@ -795,6 +805,34 @@ static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
 static int grid_of(const G256Args& a) {
   const int tiles = a.tiles_m * a.tiles_n;
   return a.tail_split > 1 ? a.full_blocks + (tiles - a.full_blocks) * a.tail_split : tiles;
+}
+
+// test hook (tests/test_graph_workspaces_gpu.py): grow this stream's tail split-K workspace
+MI_API int mi_g256_tail_ws_reserve(size_t floats, int tail, hipStream_t st) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_tail_mu);
+  TailWs* wp = nullptr;
+  for (auto& e : g_tail_ws[dev & 15])
+    if (e.used && e.st == st) { wp = &e; break; }
+  if (!wp) return 1;
+  if (wp->ws_floats < floats) {
+    float* p = nullptr;
+    if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return 2;
+    mi_ws_retire(wp->ws);
+    wp->ws = p;
+    wp->ws_floats = floats;
+  }
+  if (wp->cnt_n < tail) {
+    int* p = nullptr;
+    if (hipMalloc(&p, sizeof(int) * tail) != hipSuccess) return 2;
+    hipMemset(p, 0, sizeof(int) * tail);
+    hipDeviceSynchronize();
+    mi_ws_retire(wp->cnt);
+    wp->cnt = p;
+    wp->cnt_n = tail;
+  }
+  return 0;
 }
 
 // Returns hipErrorInvalidValue when the shape is outside this kernel's contract (caller falls

@@ -1331,8 +1331,10 @@ hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
 // TN work and must not share slabs with it; likewise the residual blocks' auxiliary (shortcut)
 // stream (mi_register_aux_stream), whose shortcut weight gradient can run concurrently with
 // compute-stream TN work when the weight-gradient stream is off.  Contract: the first call that needs a given size
-// allocates (hipMalloc) -- it must not run inside a HIP graph capture; GraphedStep's eager warm-up
-// step makes every allocation first (capture streams use the shared slot, like the warm-up).
+// allocates (hipMalloc) -- never inside a HIP graph capture (the launch then takes the workspace-free
+// schedule); GraphedStep's eager warm-up step makes every allocation first (capture streams use the
+// shared slot, like the warm-up).  A grown workspace retires its old buffer instead of freeing it
+// (common.h): graphs captured before the growth keep replaying into live memory.
 // MI355X_DP_TN_SLABS=0 selects the fp32-atomic split-K path instead.
 struct SplitkWs { float* p = nullptr; size_t n = 0; };
 static SplitkWs g_splitk_ws[16][3];  // [device][0: any other stream, 1: wgrad stream, 2: aux stream]
@@ -1346,13 +1348,14 @@ static float* splitk_workspace(size_t floats, hipStream_t st) {
   const int slot = st == nullptr ? 0 : st == g_wgrad_stream[dev & 15] ? 1 : st == g_aux_stream[dev & 15] ? 2 : 0;
   SplitkWs& w = g_splitk_ws[dev & 15][slot];
   if (w.n < floats) {
+    if (mi_stream_capturing(st)) {  // common.h: never allocate inside a capture
+      mi_ws_capture_warn("split-K slab");
+      return nullptr;  // -> unsplit / atomic path
+    }
     const size_t n = std::max(floats, (size_t)16 << 20);  // >= 64 MB: every RN50 / RN152 wgrad fits
     float* p = nullptr;
     if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return nullptr;  // -> atomic path
-    if (w.p) {
-      hipDeviceSynchronize();  // the old slabs may still be read by an in-flight reduce
-      hipFree(w.p);
-    }
+    mi_ws_retire(w.p);  // graphs captured earlier may still replay into it (common.h)
     w.p = p;
     w.n = n;
   }
@@ -1377,6 +1380,8 @@ static int* splitk_counters(hipStream_t st) {
 // the same per-stream slab workspace for the other kernels of this library that reduce per-block
 // partials deterministically (stem_conv.hip's weight gradient); nullptr -> their atomic path
 extern "C" float* mi_partials_workspace(size_t floats, hipStream_t st) { return splitk_workspace(floats, st); }
+// test hook (tests/test_graph_workspaces_gpu.py): grow this stream's split-K slab to at least `floats`
+MI_API int mi_splitk_ws_reserve(size_t floats, hipStream_t st) { return splitk_workspace(floats, st) ? 0 : 1; }
 static int g_tn_slabs = -1;
 static bool tn_slabs_on() {
   if (g_tn_slabs < 0) {

@@ -10,8 +10,8 @@
 //   * a flag array in fine-grained / uncached device memory (hipExtMallocWithFlags, see the
 //     backend): every flag store and poll goes to memory, never to a stale cache line of another
 //     XCD's L2 or another GPU.
-// Protocol of one call (epoch e, this rank r, block b; every rank launches the same grid because
-// the grid depends only on the element count):
+// Protocol of one call (epoch e, this rank r, block b; every rank launches the same grid and cuts
+// the payload into the same 16-byte units per block, both from the payload size alone):
 //   1. copy-in: block b copies exactly the input elements that blocks with index b on every rank
 //      will read into slot[e & 1] of r's buffer -- the waves that write the data are the ones that
 //      release it (no separate hipMemcpyAsync, no reliance on a kernel boundary for visibility);
@@ -97,34 +97,76 @@ int ipc_grid(int64_t work) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(MI_IPC_MAX_GRID, (work + 255) / 256));
 }
 
+// ------------------------------------------------------------------ partition of a payload
+// Every one-shot kernel below cuts its payload into 16-byte units; unit u is moved by thread
+// u mod (grid x 256), so the block that copies a unit in, releases it and reads it back on every
+// rank is a function of the payload size alone (the grid is too).  Where THIS rank's tensor sits
+// only picks how the owning thread moves the bytes (one 16-byte access, dwords, or bytes): ranks
+// whose tensors differ in alignment still cut the payload identically (an alignment-
+// chosen vector width used to change the grid and the block-to-element map per rank).
+__device__ __forceinline__ void unit_copy(char* dst, const char* src, int bytes) {
+  if (bytes == 16 && (((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    *(u32x4*)dst = *(const u32x4*)src;
+  } else if (((bytes | (int)(uintptr_t)dst | (int)(uintptr_t)src) & 3) == 0) {
+    for (int i = 0; i < bytes; i += 4) *(uint32_t*)(dst + i) = *(const uint32_t*)(src + i);
+  } else {
+    for (int i = 0; i < bytes; ++i) dst[i] = src[i];
+  }
+}
+
+// a unit held in registers, stored to a local tensor
+__device__ __forceinline__ void unit_put(char* dst, u32x4 w, int bytes) {
+  if (bytes == 16 && ((uintptr_t)dst & 15) == 0) {
+    *(u32x4*)dst = w;
+  } else if (((bytes | (int)(uintptr_t)dst) & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * i < bytes) *(uint32_t*)(dst + 4 * i) = w[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < bytes) dst[i] = (char)(w[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+// a unit of a peer's slot: slots and unit offsets are 16-byte aligned (slot bytes past the payload
+// are read but never stored anywhere)
+__device__ __forceinline__ u32x4 slot_unit(const void* slot, int64_t u) {
+  return __builtin_nontemporal_load((const u32x4*)slot + u);
+}
+
+template <typename T>
+__device__ __forceinline__ void unit_store(T* dst, const T (&v)[16 / sizeof(T)], int bytes) {
+  constexpr int E = 16 / sizeof(T);
+  if (bytes == 16 && ((uintptr_t)dst & 15) == 0) {
+    *(u32x4*)dst = __builtin_bit_cast(u32x4, v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (e * (int)sizeof(T) < bytes) dst[e] = v[e];
+  }
+}
+
+__host__ __device__ __forceinline__ int64_t ipc_units(int64_t nbytes) { return (nbytes + 15) / 16; }
+
 // ------------------------------------------------------------------ one-shot fp32 all-reduce
-template <bool VEC>
 __global__ __launch_bounds__(256) void ipc_allreduce_kernel(IpcRaw p, int rank, int world, const float* in,
                                                             float* out, int64_t n, uint32_t epoch, float scale,
                                                             int* err, uint32_t spin_limit) {
-  float* mine = (float*)p.data[rank];
+  char* mine = (char*)p.data[rank];
+  const int64_t nb = n * 4, U = ipc_units(nb);
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if constexpr (VEC) {
-    for (int64_t i = 4 * t0; i < n; i += 4 * step) *(f32x4*)(mine + i) = *(const f32x4*)(in + i);
-  } else {
-    for (int64_t i = t0; i < n; i += step) mine[i] = in[i];
-  }
+  for (int64_t u = t0; u < U; u += step)
+    unit_copy(mine + 16 * u, (const char*)in + 16 * u, (int)min<int64_t>(16, nb - 16 * u));
   if (!ipc_block_sync(p, rank, world, IPC_FLAG_IN_OFF, false, epoch, err, spin_limit)) return;
-  if constexpr (VEC) {
-    for (int64_t i = 4 * t0; i < n; i += 4 * step) {
-      f32x4 s = __builtin_nontemporal_load((const f32x4*)((const float*)p.data[0] + i));
+  for (int64_t u = t0; u < U; u += step) {
+    f32x4 s = __builtin_bit_cast(f32x4, slot_unit(p.data[0], u));
 #pragma unroll 1
-      for (int q = 1; q < world; ++q) s += __builtin_nontemporal_load((const f32x4*)((const float*)p.data[q] + i));
-      *(f32x4*)(out + i) = s * scale;
-    }
-  } else {
-    for (int64_t i = t0; i < n; i += step) {
-      float s = 0.f;
-#pragma unroll 1
-      for (int q = 0; q < world; ++q) s += __builtin_nontemporal_load((const float*)p.data[q] + i);
-      out[i] = s * scale;
-    }
+    for (int q = 1; q < world; ++q) s += __builtin_bit_cast(f32x4, slot_unit(p.data[q], u));
+    s *= scale;
+    float v[4] = {s[0], s[1], s[2], s[3]};
+    unit_store<float>(out + 4 * u, v, (int)min<int64_t>(16, nb - 16 * u));
   }
 }
 
@@ -224,29 +266,34 @@ __device__ __forceinline__ Bf16 ipc_combine<Bf16, IPC_MIN>(Bf16 a, Bf16 b) { ret
 
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void ipc_oneshot_kernel(IpcRaw p, int rank, int world, const T* in,
-                                                          T* __restrict__ out, int64_t n, int root, uint32_t epoch,
-                                                          int* err, uint32_t spin_limit) {
+                                                          T* __restrict__ out, int64_t nbytes, int root,
+                                                          uint32_t epoch, int* err, uint32_t spin_limit) {
+  constexpr int E = 16 / sizeof(T);
+  const int64_t U = ipc_units(nbytes);
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (OP != IPC_COPY || rank == root) {
-    T* mine = (T*)p.data[rank];
-    for (int64_t i = t0; i < n; i += step) mine[i] = in[i];
+    char* mine = (char*)p.data[rank];
+    for (int64_t u = t0; u < U; u += step)
+      unit_copy(mine + 16 * u, (const char*)in + 16 * u, (int)min<int64_t>(16, nbytes - 16 * u));
   }
   if (!ipc_block_sync(p, rank, world, IPC_FLAG_IN_OFF, false, epoch, err, spin_limit)) return;
   if (OP == IPC_COPY && rank == root) return;  // the root's tensor is the source
-  for (int64_t i = t0; i < n; i += step) {
+  for (int64_t u = t0; u < U; u += step) {
+    const int bytes = (int)min<int64_t>(16, nbytes - 16 * u);
     if constexpr (OP == IPC_COPY) {
-      out[i] = __builtin_nontemporal_load((const T*)p.data[root] + i);
-    } else if constexpr (sizeof(T) == 2) {  // Bf16: plain loads (no 2-byte non-temporal struct load)
-      T v = ((const T*)p.data[0])[i];
-#pragma unroll 1
-      for (int q = 1; q < world; ++q) v = ipc_combine<T, OP>(v, ((const T*)p.data[q])[i]);
-      out[i] = v;
+      unit_put((char*)out + 16 * u, slot_unit(p.data[root], u), bytes);
     } else {
-      T v = __builtin_nontemporal_load((const T*)p.data[0] + i);
+      T v[E];
+      *(u32x4*)v = slot_unit(p.data[0], u);
 #pragma unroll 1
-      for (int q = 1; q < world; ++q) v = ipc_combine<T, OP>(v, __builtin_nontemporal_load((const T*)p.data[q] + i));
-      out[i] = v;
+      for (int q = 1; q < world; ++q) {
+        T w[E];
+        *(u32x4*)w = slot_unit(p.data[q], u);
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = ipc_combine<T, OP>(v[e], w[e]);
+      }
+      unit_store<T>(out + E * u, v, bytes);
     }
   }
 }
@@ -254,8 +301,9 @@ __global__ __launch_bounds__(256) void ipc_oneshot_kernel(IpcRaw p, int rank, in
 template <typename T, int OP>
 void launch_oneshot(const IpcRaw& p, int rank, int world, const void* in, void* out, int64_t n, int root,
                     uint32_t epoch, int* err, uint32_t spin_limit, hipStream_t st) {
-  hipLaunchKernelGGL((ipc_oneshot_kernel<T, OP>), dim3(ipc_grid(n)), dim3(256), 0, st, p, rank, world, (const T*)in,
-                     (T*)out, n, root, epoch, err, spin_limit);
+  // n: payload BYTES (the grid and the unit partition depend on them alone)
+  hipLaunchKernelGGL((ipc_oneshot_kernel<T, OP>), dim3(ipc_grid(ipc_units(n))), dim3(256), 0, st, p, rank, world,
+                     (const T*)in, (T*)out, n, root, epoch, err, spin_limit);
 }
 
 template <typename T>
@@ -279,61 +327,66 @@ int dispatch_oneshot(int op, const IpcRaw& p, int rank, int world, const void* i
 //       slots (fp32 accumulation, rank order) into out[0, c);
 //   all-gather: copy-in puts this rank's piece into its slot; rank r copies every rank q's slot into
 //       out[q * stride, q * stride + c).
-__device__ __forceinline__ float ld_f(const float* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ float ld_f(const bf16_t* p) { return bf2f(*p); }
-__device__ __forceinline__ void st_f(float* p, float v) { *p = v; }
-__device__ __forceinline__ void st_f(bf16_t* p, float v) { *p = f2bf(v); }
+// slot layout of the reduce-scatter: piece q at q * piece_bytes(c), 16-byte aligned
+__host__ __device__ __forceinline__ int64_t piece_bytes(int64_t c, int esz) { return (c * esz + 15) & ~(int64_t)15; }
 
-template <typename T, bool VEC>
+template <typename T>
 __global__ __launch_bounds__(256) void ipc_rs_kernel(IpcRaw p, int rank, int world, const T* in, int64_t in_stride,
                                                      T* __restrict__ out, int64_t c, float scale, uint32_t epoch,
                                                      int* err, uint32_t spin_limit) {
+  constexpr int E = 16 / sizeof(T);
+  const int64_t nb = c * (int64_t)sizeof(T), pb = piece_bytes(c, sizeof(T)), U = ipc_units(nb);
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  T* mine = (T*)p.data[rank];
-  for (int q = 0; q < world; ++q) {
-    if constexpr (VEC) {
-      for (int64_t i = 4 * t0; i < c; i += 4 * step)
-        *(f32x4*)((float*)mine + q * c + i) = *(const f32x4*)((const float*)in + q * in_stride + i);
-    } else {
-      for (int64_t i = t0; i < c; i += step) mine[q * c + i] = in[q * in_stride + i];
-    }
-  }
+  char* mine = (char*)p.data[rank];
+  for (int q = 0; q < world; ++q)
+    for (int64_t u = t0; u < U; u += step)
+      unit_copy(mine + q * pb + 16 * u, (const char*)(in + q * in_stride) + 16 * u, (int)min<int64_t>(16, nb - 16 * u));
   if (!ipc_block_sync(p, rank, world, IPC_FLAG_IN_OFF, false, epoch, err, spin_limit)) return;
-  const int64_t base = (int64_t)rank * c;
-  if constexpr (VEC) {
-    for (int64_t i = 4 * t0; i < c; i += 4 * step) {
-      f32x4 s = __builtin_nontemporal_load((const f32x4*)((const float*)p.data[0] + base + i));
+  const int64_t ub = rank * pb / 16;  // this rank's piece, in units of every slot
+  for (int64_t u = t0; u < U; u += step) {
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
 #pragma unroll 1
-      for (int q = 1; q < world; ++q) s += __builtin_nontemporal_load((const f32x4*)((const float*)p.data[q] + base + i));
-      *(f32x4*)((float*)out + i) = s * scale;
+    for (int q = 0; q < world; ++q) {  // fp32 accumulation in rank order
+      T w[E];
+      *(u32x4*)w = slot_unit(p.data[q], ub + u);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if constexpr (sizeof(T) == 4) acc[e] += w[e];
+        else acc[e] += bf2f(w[e]);
+      }
     }
-  } else {
-    for (int64_t i = t0; i < c; i += step) {
-      float s = 0.f;
-#pragma unroll 1
-      for (int q = 0; q < world; ++q) s += ld_f((const T*)p.data[q] + base + i);
-      st_f(out + i, s * scale);
+    T v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if constexpr (sizeof(T) == 4) v[e] = acc[e] * scale;
+      else v[e] = f2bf(acc[e] * scale);
+    }
+    unit_store<T>(out + E * u, v, (int)min<int64_t>(16, nb - 16 * u));
+  }
+}
+
+__global__ __launch_bounds__(256) void ipc_ag_kernel(IpcRaw p, int rank, int world, const char* in,
+                                                     char* __restrict__ out, int64_t nbytes, int64_t stride,
+                                                     uint32_t epoch, int* err, uint32_t spin_limit) {
+  const int64_t U = ipc_units(nbytes);
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  char* mine = (char*)p.data[rank];
+  for (int64_t u = t0; u < U; u += step)
+    unit_copy(mine + 16 * u, in + 16 * u, (int)min<int64_t>(16, nbytes - 16 * u));
+  if (!ipc_block_sync(p, rank, world, IPC_FLAG_IN_OFF, false, epoch, err, spin_limit)) return;
+  for (int q = 0; q < world; ++q) {
+    char* dst = out + (int64_t)q * stride;
+    for (int64_t u = t0; u < U; u += step) {
+      unit_put(dst + 16 * u, slot_unit(p.data[q], u), (int)min<int64_t>(16, nbytes - 16 * u));
     }
   }
 }
 
-template <typename W>
-__global__ __launch_bounds__(256) void ipc_ag_kernel(IpcRaw p, int rank, int world, const W* in, W* __restrict__ out,
-                                                     int64_t c, int64_t stride, uint32_t epoch, int* err,
-                                                     uint32_t spin_limit) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  W* mine = (W*)p.data[rank];
-  for (int64_t i = t0; i < c; i += step) mine[i] = in[i];
-  if (!ipc_block_sync(p, rank, world, IPC_FLAG_IN_OFF, false, epoch, err, spin_limit)) return;
-  for (int q = 0; q < world; ++q) {
-    const W* src = (const W*)p.data[q];
-    W* dst = out + (int64_t)q * stride;
-    for (int64_t i = t0; i < c; i += step) dst[i] = __builtin_nontemporal_load(src + i);
-  }
-}
-
+// slots must be 16-byte aligned (the backend's hipMalloc'd buffers and 256-byte-rounded slot sizes)
 bool make_peers(IpcRaw& p, const void* const* data, uint32_t* const* flags, int world) {
   bool al16 = true;
   for (int q = 0; q < world; ++q) {
@@ -358,14 +411,9 @@ MI_API int mi_ipc_allreduce_f32(const float* const* data, uint32_t* const* flags
                                 hipStream_t st) {
   if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || n < 0) return (int)hipErrorInvalidValue;
   IpcRaw p{};
-  const bool vec = make_peers(p, (const void* const*)data, flags, world) && n % 4 == 0 &&
-                   ((uintptr_t)out & 15) == 0 && ((uintptr_t)in & 15) == 0;
-  if (vec)
-    hipLaunchKernelGGL(ipc_allreduce_kernel<true>, dim3(ipc_grid(n / 4)), dim3(256), 0, st, p, rank, world, in, out,
-                       n, epoch, scale, err, spin_limit);
-  else
-    hipLaunchKernelGGL(ipc_allreduce_kernel<false>, dim3(ipc_grid(n)), dim3(256), 0, st, p, rank, world, in, out, n,
-                       epoch, scale, err, spin_limit);
+  if (!make_peers(p, (const void* const*)data, flags, world)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(ipc_grid(ipc_units(n * 4))), dim3(256), 0, st, p, rank, world, in, out,
+                     n, epoch, scale, err, spin_limit);
   return (int)hipGetLastError();
 }
 
@@ -400,28 +448,24 @@ MI_API int mi_ipc_oneshot(const void* const* data, uint32_t* const* flags, int r
       op < 0 || op > IPC_COPY)
     return (int)hipErrorInvalidValue;
   IpcRaw p{};
-  const bool al16 = make_peers(p, data, flags, world) && ((uintptr_t)out & 15) == 0 && ((uintptr_t)in & 15) == 0;
-  if (op == IPC_COPY) {
-    if (al16 && nbytes % 16 == 0)
-      launch_oneshot<u32x4, IPC_COPY>(p, rank, world, in, out, nbytes / 16, root, epoch, err, spin_limit, st);
-    else if (nbytes % 4 == 0)
-      launch_oneshot<uint32_t, IPC_COPY>(p, rank, world, in, out, nbytes / 4, root, epoch, err, spin_limit, st);
-    else
-      launch_oneshot<uint8_t, IPC_COPY>(p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
+  if (!make_peers(p, data, flags, world)) return (int)hipErrorInvalidValue;
+  if (op == IPC_COPY) {  // a byte copy, whatever the dtype
+    launch_oneshot<uint32_t, IPC_COPY>(p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
     return (int)hipGetLastError();
   }
   switch (dtype) {
-    case 0: return dispatch_oneshot<float>(op, p, rank, world, in, out, nbytes / 4, root, epoch, err, spin_limit, st);
-    case 1: return dispatch_oneshot<double>(op, p, rank, world, in, out, nbytes / 8, root, epoch, err, spin_limit, st);
-    case 2: return dispatch_oneshot<int32_t>(op, p, rank, world, in, out, nbytes / 4, root, epoch, err, spin_limit, st);
-    case 3: return dispatch_oneshot<int64_t>(op, p, rank, world, in, out, nbytes / 8, root, epoch, err, spin_limit, st);
-    case 4: return dispatch_oneshot<Bf16>(op, p, rank, world, in, out, nbytes / 2, root, epoch, err, spin_limit, st);
+    case 0: return dispatch_oneshot<float>(op, p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
+    case 1: return dispatch_oneshot<double>(op, p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
+    case 2: return dispatch_oneshot<int32_t>(op, p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
+    case 3: return dispatch_oneshot<int64_t>(op, p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
+    case 4: return dispatch_oneshot<Bf16>(op, p, rank, world, in, out, nbytes, root, epoch, err, spin_limit, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
 
 // c: elements of the output piece; in: this rank's `world` pieces, piece q at in + q * in_stride;
-// dtype 0 f32, 4 bf16; scale 1/world for AVG.  Every rank's slot must hold world * c elements.
+// dtype 0 f32, 4 bf16; scale 1/world for AVG.  Every rank's slot must hold world * piece_bytes(c) bytes
+// (pieces start 16-byte aligned).
 MI_API int mi_ipc_reduce_scatter(const void* const* data, uint32_t* const* flags, int rank, int world, const void* in,
                                  int64_t in_stride, void* out, int64_t c, int dtype, float scale, uint32_t epoch,
                                  int* err, uint32_t spin_limit, hipStream_t st) {
@@ -429,17 +473,15 @@ MI_API int mi_ipc_reduce_scatter(const void* const* data, uint32_t* const* flags
       (dtype != 0 && dtype != 4))
     return (int)hipErrorInvalidValue;
   IpcRaw p{};
-  const bool vec = make_peers(p, data, flags, world) && dtype == 0 && c % 4 == 0 && in_stride % 4 == 0 &&
-                   ((uintptr_t)out & 15) == 0 && ((uintptr_t)in & 15) == 0;
-  if (vec)
-    hipLaunchKernelGGL((ipc_rs_kernel<float, true>), dim3(ipc_grid(c / 4)), dim3(256), 0, st, p, rank, world,
-                       (const float*)in, in_stride, (float*)out, c, scale, epoch, err, spin_limit);
-  else if (dtype == 0)
-    hipLaunchKernelGGL((ipc_rs_kernel<float, false>), dim3(ipc_grid(c)), dim3(256), 0, st, p, rank, world,
-                       (const float*)in, in_stride, (float*)out, c, scale, epoch, err, spin_limit);
+  if (!make_peers(p, data, flags, world)) return (int)hipErrorInvalidValue;
+  const int esz = dtype == 0 ? 4 : 2;
+  const dim3 grid(ipc_grid(ipc_units(c * esz)));
+  if (dtype == 0)
+    hipLaunchKernelGGL(ipc_rs_kernel<float>, grid, dim3(256), 0, st, p, rank, world, (const float*)in, in_stride,
+                       (float*)out, c, scale, epoch, err, spin_limit);
   else
-    hipLaunchKernelGGL((ipc_rs_kernel<bf16_t, false>), dim3(ipc_grid(c)), dim3(256), 0, st, p, rank, world,
-                       (const bf16_t*)in, in_stride, (bf16_t*)out, c, scale, epoch, err, spin_limit);
+    hipLaunchKernelGGL(ipc_rs_kernel<bf16_t>, grid, dim3(256), 0, st, p, rank, world, (const bf16_t*)in, in_stride,
+                       (bf16_t*)out, c, scale, epoch, err, spin_limit);
   return (int)hipGetLastError();
 }
 
@@ -451,18 +493,8 @@ MI_API int mi_ipc_all_gather(const void* const* data, uint32_t* const* flags, in
   if (world < 1 || world > IPC_MAX_PEERS || rank < 0 || rank >= world || nbytes < 0 || stride_bytes < nbytes)
     return (int)hipErrorInvalidValue;
   IpcRaw p{};
-  const bool al = make_peers(p, data, flags, world);
-  const bool al16 = al && ((uintptr_t)out & 15) == 0 && ((uintptr_t)in & 15) == 0 && nbytes % 16 == 0 &&
-                    stride_bytes % 16 == 0;
-  const bool al4 = ((uintptr_t)out & 3) == 0 && ((uintptr_t)in & 3) == 0 && nbytes % 4 == 0 && stride_bytes % 4 == 0;
-  if (al16)
-    hipLaunchKernelGGL(ipc_ag_kernel<u32x4>, dim3(ipc_grid(nbytes / 16)), dim3(256), 0, st, p, rank, world,
-                       (const u32x4*)in, (u32x4*)out, nbytes / 16, stride_bytes / 16, epoch, err, spin_limit);
-  else if (al4)
-    hipLaunchKernelGGL(ipc_ag_kernel<uint32_t>, dim3(ipc_grid(nbytes / 4)), dim3(256), 0, st, p, rank, world,
-                       (const uint32_t*)in, (uint32_t*)out, nbytes / 4, stride_bytes / 4, epoch, err, spin_limit);
-  else
-    hipLaunchKernelGGL(ipc_ag_kernel<uint8_t>, dim3(ipc_grid(nbytes)), dim3(256), 0, st, p, rank, world,
-                       (const uint8_t*)in, (uint8_t*)out, nbytes, stride_bytes, epoch, err, spin_limit);
+  if (!make_peers(p, data, flags, world)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ipc_ag_kernel, dim3(ipc_grid(ipc_units(nbytes))), dim3(256), 0, st, p, rank, world,
+                     (const char*)in, (char*)out, nbytes, stride_bytes, epoch, err, spin_limit);
   return (int)hipGetLastError();
 }

@@ -254,14 +254,16 @@ static float* ln_rep_workspace(int D, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_lnrep_mu);
   LnRep& w = g_lnrep[{dev, st}];
   if (w.D < D) {
+    if (mi_stream_capturing(st)) {  // common.h: never allocate inside a capture
+      mi_ws_capture_warn("LayerNorm replica");
+      return nullptr;  // -> the replica-free parameter-gradient path
+    }
     float* p = nullptr;
     const size_t bytes = sizeof(float) * LN_REPLICAS * 2 * (size_t)D;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
     if (hipMemset(p, 0, bytes) != hipSuccess) return nullptr;
-    if (w.p) {
-      hipDeviceSynchronize();
-      hipFree(w.p);
-    }
+    hipDeviceSynchronize();  // the zeroing is complete before any stream uses the replicas
+    mi_ws_retire(w.p);       // graphs captured earlier may still replay into it (common.h)
     w.p = p;
     w.D = D;
   }
@@ -269,6 +271,9 @@ static float* ln_rep_workspace(int D, hipStream_t st) {
 }
 
 }  // namespace
+
+// test hook (tests/test_graph_workspaces_gpu.py): grow this stream's LayerNorm replicas to width D
+MI_API int mi_ln_ws_reserve(int D, hipStream_t st) { return ln_rep_workspace(D, st) ? 0 : 1; }
 
 MI_API int mi_layernorm_fwd(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
                             int M, int D, float eps, hipStream_t st) {

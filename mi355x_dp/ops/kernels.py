@@ -25,6 +25,7 @@ signature("mi_gemm_tn_bias", P, P, P, P, I, I, I, I, I, I, P)
 signature("mi_register_wgrad_stream", P)
 signature("mi_register_aux_stream", P)
 signature("mi_create_cu_masked_stream", I, I, P)
+signature("mi_splitk_ws_reserve", ctypes.c_size_t, P)
 
 # norm_act.hip
 signature("mi_bn_partial_rows", I, I)
@@ -53,6 +54,10 @@ signature("mi_augment", P, P, I, I, I, I, I, I, I, U32, P, P, P)
 signature("mi_im2col", P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_add_bf16", P, P, P, L, P)
 signature("mi_checksum", P, L, P, P)
+signature("mi_flags_alloc", I, P)
+signature("mi_flag_bump", P, P)
+signature("mi_flag_gate", P, U32, P, I, P)
+signature("mi_host_word_alloc", P, P)
 
 # gemm_conv.hip (epilogue-fused NT GEMM)
 signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)
@@ -61,6 +66,7 @@ signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)
 signature("mi_layernorm_fwd", P, P, P, P, P, P, I, I, F, P)
 signature("mi_layernorm_bwd", P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_colsum_bf16", P, P, I, I, I, P)
+signature("mi_ln_ws_reserve", I, P)
 
 # attention.hip
 signature("mi_attn_max_seq")
@@ -74,6 +80,7 @@ signature("mi_gemm256p_nt", P, P, P, P, P, I, I, I, I, I, I, I, P)
 signature("mi_set_gemm_persist", I)
 signature("mi_set_tail_split", I)
 signature("mi_set_gemm256", I)
+signature("mi_g256_tail_ws_reserve", ctypes.c_size_t, I, P)
 signature("mi_gemm256_tn", P, P, P, I, I, I, I, I, I, P)
 signature("mi_dgrad_stat_rows", I, I, I, I, I, I, I, I, I)
 signature("mi_conv_stat_rows", I, I, I, I)

@@ -340,6 +340,7 @@ class DataParallel(nn.Module):
         self._py_comm_calls = 0
 
         self.reducer = None
+        self._capture_marks = None  # graph capture of a backward: bucket-gate bookkeeping
         self._staging = {}
         if grad_comm not in ("fp32", "bf16"):
             raise ValueError(f"grad_comm must be 'fp32' or 'bf16', not {grad_comm!r}")
@@ -414,6 +415,9 @@ class DataParallel(nn.Module):
         return hook
 
     def _ready_native(self, i):
+        if self._capture_marks is not None:
+            self._capture_mark(i)
+            return
         if self._comm_hook is None:
             self.reducer.mark_ready(i)
         else:
@@ -467,6 +471,9 @@ class DataParallel(nn.Module):
                 self.reducer.enabled = old
 
     def _mark_ready(self, i):
+        if self._capture_marks is not None:
+            self._capture_mark(i)
+            return
         if not self.require_backward_grad_sync:
             return
         if self._param_ready[i]:
@@ -626,6 +633,9 @@ class DataParallel(nn.Module):
         t = out
         while isinstance(t, (tuple, list)) and t:
             t = t[0]
+        # a backward that raised after queueing the callback (an OOM the script catches and
+        # retries) never ran it: re-arm on every forward so that no later step skips its sync
+        self._final_cb_pending = False
         if not (isinstance(t, torch.Tensor) and t.requires_grad):
             return
 
@@ -694,6 +704,72 @@ class DataParallel(nn.Module):
         if tok is None:
             tok = self._graph_token = torch.zeros((), device=x.device, requires_grad=True)
         return st(tok, x)
+
+    # ------------------------------------- graphed backward: per-bucket gates (step_graph)
+    def _begin_capture_marks(self, gates, stream):
+        """Inside the capture of a backward: as each bucket's gradients complete (in bucket order,
+        like the reducer), capture a bump of that bucket's gate flag on the capture stream."""
+        self._capture_marks = {"gates": gates, "stream": stream, "seen": set(), "next": 0,
+                               "pending": [len(b) for b in self.buckets]}
+
+    def _capture_mark(self, i):
+        cm = self._capture_marks
+        if i in cm["seen"]:
+            return
+        cm["seen"].add(i)
+        cm["pending"][self.bucket_of[i]] -= 1
+        while cm["next"] < len(self.buckets) and cm["pending"][cm["next"]] == 0:
+            cm["gates"].bump(cm["next"], cm["stream"])
+            cm["next"] += 1
+
+    def _end_capture_marks(self):
+        cm, self._capture_marks = self._capture_marks, None
+        for b in range(cm["next"], len(self.buckets)):  # parameters without a gradient kernel
+            cm["gates"].bump(b, cm["stream"])
+
+    def _gate_stream(self):
+        s = getattr(self, "_gate_s", None)
+        if s is None:
+            s = self._gate_s = torch.cuda.Stream(device=self.flat.grad.device)
+        return s
+
+    def _gate_trace_begin(self):
+        if os.environ.get("MI355X_DP_GATE_TRACE", "0") != "1":
+            return None
+        t0 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        return {"t0": t0, "gates": [], "end": None}
+
+    def _gated_launch(self, step, trace=None):
+        """After a replay of a captured backward: bucket b's collective is launched from the gate
+        stream behind a gate kernel that waits for the graph's bump of b (this replay's count) --
+        the reducer's ready-marks see the gate stream as the producing stream."""
+        from .step_graph import BucketGates
+        BucketGates.check()
+        if trace is not None:
+            trace["end"] = torch.cuda.Event(enable_timing=True)
+            trace["end"].record()
+        gs = self._gate_stream()
+        with torch.cuda.stream(gs):
+            for b, idxs in enumerate(self.buckets):
+                step.gates.gate(b, step.replays, gs)
+                if trace is not None:
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record(gs)
+                    trace["gates"].append(ev)
+                for i in idxs:
+                    self.reducer.mark_ready(i)
+        if trace is not None:
+            self._last_gate_trace = trace
+
+    def gate_trace_ms(self):
+        """(ms at which each bucket's gate opened, ms at which the replayed backward ended), both
+        from the replay's start -- the last graphed step, with MI355X_DP_GATE_TRACE=1."""
+        tr = getattr(self, "_last_gate_trace", None)
+        if tr is None:
+            return None
+        torch.cuda.synchronize(self.flat.grad.device)
+        return [tr["t0"].elapsed_time(e) for e in tr["gates"]], tr["t0"].elapsed_time(tr["end"])
 
     def _mark_all_ready(self):
         """after a graph replay: the captured backward wrote every gradient; launch the buckets"""

@@ -55,8 +55,35 @@ def eligible(module: nn.Module, kwargs) -> bool:
     return any(isinstance(m, (Conv2d, Linear)) for m in module.modules())
 
 
-class DistributedDataParallel:
+class _FactoryMeta(type):
+    """Keeps the public name behaving like a class for user code:
+
+    * ``isinstance(m, torch.nn.parallel.DistributedDataParallel)`` -- the usual way scripts and
+      libraries decide to unwrap ``.module`` -- holds for both things the factory returns (the
+      engine and the stock fallback), and ``issubclass`` likewise;
+    * ``class MyDDP(torch.nn.parallel.DistributedDataParallel)`` written after the shim is
+      imported derives from torch's own class, so the subclass keeps stock semantics."""
+
+    def __new__(mcls, name, bases, ns, **kw):
+        if any(isinstance(b, _FactoryMeta) for b in bases) and ns.get("_mi355x_factory") is None:
+            stock = stock_ddp()
+            bases = tuple(stock if isinstance(b, _FactoryMeta) else b for b in bases)
+            return type(stock)(name, bases, ns, **kw)
+        return super().__new__(mcls, name, bases, ns, **kw)
+
+    def __instancecheck__(cls, obj):
+        from .ddp import DataParallel
+        return isinstance(obj, (stock_ddp(), DataParallel))
+
+    def __subclasscheck__(cls, sub):
+        from .ddp import DataParallel
+        return sub is cls or issubclass(sub, (stock_ddp(), DataParallel))
+
+
+class DistributedDataParallel(metaclass=_FactoryMeta):
     """Factory standing in for ``torch.nn.parallel.DistributedDataParallel`` (see module doc)."""
+
+    _mi355x_factory = True
 
     def __new__(cls, module, *args, **kwargs):
         if args:  # positional device_ids etc.: torch's signature order

@@ -9,12 +9,15 @@ per input signature and replays them; the user's loss, ``loss.backward()`` and s
 ``optim.SGD`` run eagerly around them exactly as written:
 
   ``output = model(data)``   -> copy ``data`` into the static input, replay the forward graph,
-                                return a detached view of the static output wired to
+                                return a copy of the static output wired to
   ``loss.backward()``        -> ``_Replay.backward``: copy the incoming gradient into the static
                                 gradient, replay the backward graph (the kernels accumulate the
                                 weight gradients straight into the flat buffer, as eagerly); the
-                                engine's end-of-backward callback then launches every bucket's
-                                collective (they were not captured) and averages.
+                                graph also bumps one flag per gradient bucket right after the
+                                bucket's last gradient kernel, and the engine's gate stream
+                                launches each bucket's collective behind its own flag
+                                (``BucketGates``) -- overlapped with the rest of the replay, as
+                                in eager mode; the end-of-backward callback joins and averages.
 
 Capture (once per signature, after ``AFTER`` eager steps with it): two warm-up passes on the
 capture stream size every lazily allocated native workspace for that stream (nothing may be
@@ -52,18 +55,71 @@ class _Replay(torch.autograd.Function):
             step.static_x.copy_(x)
         step.fwd.replay()
         ctx.step = step
-        return step.static_out.detach()
+        # a copy, not a view of the static buffer: outputs a script keeps past backward (logits
+        # saved for an accuracy count) must not change under the next replay -- stock DDP returns
+        # fresh tensors too; the copy is one small kernel next to the ~150 launches saved
+        return step.static_out.clone()
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         st = ctx.step
         st.static_gout.copy_(g)
+        eng = st.engine
+        trace = eng._gate_trace_begin() if st.gates is not None else None
         st.bwd.replay()
         st.replays += 1
         st.pending = None
-        st.engine._graph_backward_ran = True
+        if st.gates is not None:
+            eng._gated_launch(st, trace)  # every bucket's collective behind its own gate
+        else:
+            eng._graph_backward_ran = True  # launched at the end of backward
         return None, None, None
+
+
+class BucketGates:
+    """One flag word per gradient bucket of a captured backward (misc.hip ``mi_flag_bump`` /
+    ``mi_flag_gate``): the graph bumps a bucket's flag right after the bucket's last gradient
+    kernel; after a replay the engine's gate stream waits, per bucket, until the flag reaches the
+    replay count and then launches that bucket's collective -- so bucket k's all-reduce runs while
+    the rest of the replayed backward still computes, as in eager mode."""
+
+    TIMEOUT_MS = int(os.environ.get("MI355X_DP_GATE_TIMEOUT_MS", "60000"))
+
+    def __init__(self, n: int):
+        import ctypes
+        from mi355x_dp.ops import _lib
+        from mi355x_dp.ops import kernels  # noqa: F401
+        self._lib = _lib
+        lib = _lib.load(True)
+        p = ctypes.c_void_p()
+        _lib.check(lib.mi_flags_alloc(n, ctypes.byref(p)), "mi_flags_alloc")
+        self.base, self.n = p.value, n  # kept for the process's life, like the graph's pool
+        if BucketGates._err is None:
+            host, dev = ctypes.c_void_p(), ctypes.c_void_p()
+            _lib.check(lib.mi_host_word_alloc(ctypes.byref(host), ctypes.byref(dev)), "mi_host_word_alloc")
+            BucketGates._err = (ctypes.cast(host, ctypes.POINTER(ctypes.c_int)), dev)
+
+    _err = None
+
+    def _flag(self, b):
+        import ctypes
+        return ctypes.c_void_p(self.base + 4 * b)
+
+    def bump(self, b: int, stream):
+        import ctypes
+        self._lib.call("mi_flag_bump", self._flag(b), ctypes.c_void_p(stream.cuda_stream))
+
+    def gate(self, b: int, target: int, stream):
+        import ctypes
+        self._lib.call("mi_flag_gate", self._flag(b), target & 0xFFFFFFFF, BucketGates._err[1], self.TIMEOUT_MS,
+                       ctypes.c_void_p(stream.cuda_stream))
+
+    @staticmethod
+    def check():
+        if BucketGates._err is not None and BucketGates._err[0][0] != 0:
+            raise RuntimeError(f"mi355x_dp: a bucket gate waited {BucketGates.TIMEOUT_MS} ms for its gradients "
+                               "(graphed backward did not reach the bucket): the collective ran on stale data")
 
 
 class CapturedStep:
@@ -74,6 +130,10 @@ class CapturedStep:
         self.engine = engine
         self.replays = 0
         self.pending = None  # weakref to the last graphed output until its backward ran
+        # per-bucket gates (native reducer, collectives on): bucket k launches behind its own
+        # gradients instead of behind the whole replayed backward
+        self.gates = (BucketGates(len(engine.buckets)) if engine.comm_on and engine.reducer is not None
+                      and engine._comm_hook is None else None)
         mod = engine.module
         dev = x.device
         self.static_x = torch.empty_strided(tuple(x.shape), tuple(x.stride()), dtype=x.dtype, device=dev)
@@ -109,7 +169,13 @@ class CapturedStep:
                 raise TypeError("graphed forward: the module must return one tensor")
             self.static_gout = torch.empty_like(out)
             with torch.cuda.graph(self.bwd, pool=pool, stream=s):
-                torch.autograd.backward(out, self.static_gout)
+                if self.gates is not None:
+                    engine._begin_capture_marks(self.gates, s)
+                try:
+                    torch.autograd.backward(out, self.static_gout)
+                finally:
+                    if self.gates is not None:
+                        engine._end_capture_marks()  # buckets no kernel marked: bumped at the end
             self.static_out = out.detach()
             del out
         finally:

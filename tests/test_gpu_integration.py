@@ -446,6 +446,31 @@ def test_smddp_ipc_mesh_collectives_multi_rank(world):
     assert r.stdout.count("MESH_OK") == world
 
 
+def test_graphed_engine_two_ranks_gated_buckets():
+    """The graphed engine at world 2: the reference loop shape through
+    the engine-backed DDP with stock SGD, graphed vs eager on IPC-only smddp (2 ranks sharing cuda:0).
+    Graphed == eager bit for bit on every rank (losses and flat fp32 parameters), replicas
+    identical, and every bucket's collective released by its gate before the replayed backward
+    ended (the first bucket well before)."""
+    import json
+    env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC_ONLY": "1", "MI355X_DP_SMDDP_DEVICE": "0",
+           "MI355X_DP_SMDDP_IPC_MB": "4", "MI355X_DP_SMDDP_TERMINATE_TRACE": "1"}
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2",
+                        os.path.join(ROOT, "tools", "graphed_world2.py")], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = [json.loads(l[l.index("{"):]) for l in r.stdout.splitlines() if '"rank"' in l]
+    assert len(rows) == 2, r.stdout[-2000:]
+    for row in rows:
+        assert row["gated"] and row["replays"] == 6 and row["replays_eager"] == 0, row
+        assert row["losses_graphed"] == row["losses_eager"], row
+        assert row["graphed_equals_eager"] and row["replicas_identical"], row
+        opened, end = row["gate_open_ms"], row["replay_end_ms"]
+        assert len(opened) == row["buckets"] >= 2, row
+        assert opened[0] < end, row  # the first bucket's collective starts under the replay
+    assert rows[0]["losses_graphed"] != rows[1]["losses_graphed"]  # different data per rank
+
+
 @pytest.mark.skipif(REF_CODE is None, reason="reference scripts not staged (run build())")
 def test_reference_job_per_gpu_shape():
     """tools/reference_job.py: the unmodified reference script as a local job at the reference's

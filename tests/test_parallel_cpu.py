@@ -828,6 +828,9 @@ def _worker_engine_ddp(rank, world, port, q, use_engine):
         model = resnet18(num_classes=10)
         # the reference's own calls (gpu.py:148, 156-168): stock class name, stock SGD, zero_grad
         ddp = torch.nn.parallel.DistributedDataParallel(model)
+        # the unwrap idiom of scripts and libraries holds for the engine and the stock fallback
+        assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel), type(ddp)
+        assert issubclass(type(ddp), torch.nn.parallel.DistributedDataParallel)
         opt = torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
         crit = torch.nn.CrossEntropyLoss()
         g = torch.Generator().manual_seed(7)
@@ -889,6 +892,30 @@ def test_engine_ddp_substitution_matches_stock_ddp():
     # replicas identical on the engine path
     for k in sd_e:
         assert np.array_equal(res[True][0][1][k], res[True][1][1][k]), k
+
+
+def test_engine_ddp_factory_class_semantics():
+    """The installed factory behaves like torch's class for user code: subclassing the
+    public name after the shim is imported yields a genuine subclass of torch's own DDP, and
+    isinstance / issubclass accept the stock class and the engine."""
+    from mi355x_dp.parallel import engine_ddp
+    from mi355x_dp.parallel.ddp import DataParallel
+    engine_ddp.install()
+    try:
+        import torch.nn.parallel as tnp
+        stock = engine_ddp.stock_ddp()
+        assert tnp.DistributedDataParallel is not stock
+
+        class MyDDP(tnp.DistributedDataParallel):
+            marker = 1
+
+        assert issubclass(MyDDP, stock) and MyDDP.marker == 1 and MyDDP.__mro__[1] is stock
+        assert issubclass(MyDDP, tnp.DistributedDataParallel)
+        assert issubclass(DataParallel, tnp.DistributedDataParallel)
+        assert not isinstance(torch.nn.Linear(2, 2), tnp.DistributedDataParallel)
+        assert not issubclass(torch.nn.Linear, tnp.DistributedDataParallel)
+    finally:
+        engine_ddp.uninstall()
 
 
 def test_comm_path_choice_from_probe_table():

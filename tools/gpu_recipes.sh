@@ -23,7 +23,7 @@ case "$what" in
     name="$1"; shift
     bash "$here/gpu_steps.sh" "$name" 400 \
       "rocprofv3 --kernel-trace --stats -d gpurun_out/$name -o run -- python3 bench.py $*" \
-      && python tools/prof_summary.py $(find "gpurun_out/$name" -name '*results.db' | head -1) --steps "${PROF_STEPS:-1}" \
+      && python tools/prof_summary.py $(find "gpurun_out/$name" -name '*results.db' | head -1) ${PROF_MARKER:+--marker $PROF_MARKER --skip ${PROF_SKIP:-3}} --steps "${PROF_STEPS:-1}" \
          > "gpurun_out/$name.summary.md" && rm -rf "gpurun_out/$name" ;;  # the database alone can exceed what gpurun copies back
   pmc)
     name="$1"; counters="$2"; shift 2

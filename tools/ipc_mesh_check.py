@@ -1,6 +1,6 @@
 """IPC mesh collectives at world size W (IPC-only smddp; ranks may share one GPU): reduce-scatter
 (fp32 SUM / AVG, bf16, in place, chunked past the slot), all-gather (fp32, bf16, odd bytes) and the
-chunked two-shot all-reduce against exact references.  Prints MESH_OK <rank> <world>."""
+chunked two-shot all-reduce against exact references, also with rank 0's tensors misaligned.  Prints MESH_OK <rank> <world>."""
 import os
 import sys
 
@@ -37,6 +37,34 @@ for S in (1, 1000, 300_001):
     t = torch.arange(S, device="cuda", dtype=torch.float32) * (r + 1)
     dist.all_reduce(t)
     assert torch.allclose(t, torch.arange(S, device="cuda", dtype=torch.float32) * tot, rtol=1e-6)
+# rank-local misalignment: rank 0's tensors sit 4 bytes past a 16-byte boundary, the
+# others' are aligned -- every rank must still cut each payload into the same per-block pieces
+off = 1 if r == 0 else 0
+for S in (5, 1000, 65_537, 300_001):
+    buf = torch.zeros(w * S + 8, device="cuda")
+    t = buf[off:off + S]
+    t.copy_(torch.arange(S, device="cuda", dtype=torch.float32) * (r + 1))
+    dist.all_reduce(t)
+    assert torch.allclose(t, torch.arange(S, device="cuda", dtype=torch.float32) * tot, rtol=1e-6), S
+    x = buf[off:off + w * S]
+    x.copy_(torch.arange(w * S, device="cuda", dtype=torch.float32) * (r + 1))
+    o = torch.zeros(S + 8, device="cuda")[off:off + S]
+    dist.reduce_scatter_tensor(o, x)
+    assert torch.allclose(o, torch.arange(r * S, (r + 1) * S, device="cuda", dtype=torch.float32) * tot, rtol=1e-6), S
+    g = buf[off:off + w * S]
+    g.zero_()
+    g[r * S:(r + 1) * S] = torch.arange(r * S, (r + 1) * S, device="cuda", dtype=torch.float32)
+    dist.all_gather_into_tensor(g, g[r * S:(r + 1) * S].clone())
+    assert torch.equal(g, torch.arange(w * S, device="cuda", dtype=torch.float32)), S
+    b = buf[off:off + S]
+    b.fill_(float(r))
+    dist.broadcast(b, 0)
+    assert float(b.min()) == 0 and float(b.max()) == 0, S
+    hb = torch.zeros(w * S + 8, device="cuda", dtype=torch.bfloat16)[off:off + w * S]
+    hb.fill_(0.5 + r)
+    ho = torch.zeros(S + 8, device="cuda", dtype=torch.bfloat16)[off:off + S]
+    dist.reduce_scatter_tensor(ho, hb)
+    assert float(ho.float().min()) == want and float(ho.float().max()) == want, S
 u = torch.empty(w * 3, device="cuda", dtype=torch.uint8)
 dist.all_gather_into_tensor(u, torch.full((3,), 7 + r, device="cuda", dtype=torch.uint8))
 assert u.tolist() == sum(([7 + q] * 3 for q in range(w)), []), u.tolist()
