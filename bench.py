@@ -339,6 +339,16 @@ def main(argv=None):
     if use_pg:
         dist.destroy_process_group()
         use_pg = False
+    smddp_job = None
+    if rank == 0 and world > 1 and args.backend != "smddp" and os.environ.get(
+            "MI355X_DP_BENCH_SMDDP_JOB", "1" if cuda else "0") == "1":
+        # after the timed region, as its own N-rank job: the same training step through the native
+        # `smddp` c10d backend (csrc/comm/smddp_backend.cpp, the reference's backend name,
+        # gpu.py:17-23 / nb2:781,1223) -- so every multi-GPU run also exercises the product path,
+        # while the headline keeps the path most likely to succeed
+        if cuda:
+            torch.cuda.empty_cache()
+        smddp_job = run_child_bench(world, args, "smddp")
     ipc_probe = None
     if (rank == 0 and world > 1 and cuda and world <= torch.cuda.device_count()
             and os.environ.get("MI355X_DP_BENCH_IPC_PROBE", "1") == "1"):
@@ -389,11 +399,64 @@ def main(argv=None):
             "comm_calibration": engine.calibration,
             "comm_probe": comm_probe,
             "ipc_probe": ipc_probe,
+            "smddp_job": smddp_job,
             "bucket_launch_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
         }
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.destroy_process_group()
+
+
+def _child_env():
+    from mi355x_dp.launch import compat_pythonpath
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_PORT",
+                        "MASTER_ADDR", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+                        "TORCHELASTIC_MAX_RESTARTS", "MI355X_DP_BENCH_SPAWNED")}
+    env["PYTHONPATH"] = compat_pythonpath(env.get("PYTHONPATH"))
+    env["PYTHONUNBUFFERED"] = "1"
+    return env
+
+
+def run_child_bench(world: int, args, backend: str, timeout_s: int = 300):
+    """``bench.py`` again as a fresh N-rank job (native launcher) through ``backend``, a few steps of
+    the same configuration, started by rank 0 after the benchmark finished (a failure cannot cost
+    the measurement).  Returns its img/s, ranks seen, backend, replica check and step time."""
+    from mi355x_dp.launch import NATIVE_LAUNCHER, free_port
+    if not os.path.exists(NATIVE_LAUNCHER):
+        return "skipped: native launcher not built"
+    env = _child_env()
+    env["MI355X_DP_BENCH_SMDDP_JOB"] = "0"   # no nested child jobs
+    env["MI355X_DP_BENCH_IPC_PROBE"] = "0"
+    env["MI355X_DP_BENCH_COMM_PROBE"] = "0"
+    env["MI355X_DP_BENCH_SPAWNED"] = "native"
+    steps = max(1, min(args.steps, int(os.environ.get("MI355X_DP_BENCH_SMDDP_STEPS", "10"))))
+    cmd = [NATIVE_LAUNCHER, "--nproc", str(world), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           "--", sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--steps", str(steps),
+           "--warmup", str(min(max(args.warmup, 1), 3)), "--model", args.model, "--batch", str(args.batch),
+           "--image-size", str(args.image_size), "--num-classes", str(args.num_classes), "--backend", backend,
+           "--device", args.device, "--grad-comm", args.grad_comm, "--wgrad-stream", str(args.wgrad_stream)]
+    if args.shard_optimizer:
+        cmd.append("--shard-optimizer")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        out, err = proc.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        proc.terminate()  # the launcher forwards it to every rank (abort-all), then SIGKILLs them
+        try:
+            proc.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.communicate()
+        return f"failed: timeout after {timeout_s} s"
+    for line in out.splitlines():
+        if _is_result(line):
+            d = json.loads(line)
+            return {"backend": d["config"]["backend"], "comm_library": d["config"]["comm_library"],
+                    "img_s": d["value"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+                    "ranks_seen": d["ranks_seen"], "replicas_identical": d["replicas_identical"],
+                    "buckets": d["config"]["buckets"]}
+    return f"failed: rc={proc.returncode}: {(err or out)[-400:]}"
 
 
 def run_ipc_probe(world: int, timeout_s: int = 180):

@@ -93,6 +93,13 @@ static ncclDataType_t to_nccl(at::ScalarType t) {
   }
 }
 
+// the comm stream at high priority (default): its collectives dispatch ahead of backward kernels;
+// MI355X_DP_SMDDP_HIPRIO=0 makes it an ordinary stream
+static bool hiprio_env() {
+  const char* e = std::getenv("MI355X_DP_SMDDP_HIPRIO");
+  return !(e && e[0] == '0');
+}
+
 static ncclRedOp_t to_nccl(const c10d::ReduceOp& op) {
   switch (op) {
     case c10d::ReduceOp::SUM: return ncclSum;
@@ -176,7 +183,7 @@ class SmddpBackend : public c10d::Backend {
  public:
   SmddpBackend(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, int device, double timeout_s)
       : c10d::Backend(rank, size), store_(store), device_(device),
-        comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(true, (c10::DeviceIndex)device)),
+        comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(hiprio_env(), (c10::DeviceIndex)device)),
         timeout_(std::chrono::milliseconds((int64_t)(timeout_s * 1000))) {
     HIPCHECK(hipSetDevice(device));
     const std::string key = "smddp/uid";
@@ -189,7 +196,7 @@ class SmddpBackend : public c10d::Backend {
       TORCH_CHECK(v.size() == sizeof(uid_), "smddp: bad unique id from store");
       memcpy(&uid_, v.data(), sizeof(uid_));
     }
-    HIPCHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    for (auto& e : ready_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char* c = std::getenv("MI355X_DP_SMDDP_CHUNK_MB")) chunk_bytes_ = (size_t)(atof(c) * (1 << 20));
     if (const char* c = std::getenv("MI355X_DP_SMDDP_ABORT_ON_ERROR")) abort_on_error_ = c[0] != '0';
     const char* ipc = std::getenv("MI355X_DP_SMDDP_IPC");
@@ -212,7 +219,7 @@ class SmddpBackend : public c10d::Backend {
         if (b == this) b = nullptr;
     }
     stop_watchdog();
-    hipEventDestroy(ready_);
+    for (auto& e : ready_) hipEventDestroy(e);
     if (comm_) ncclCommDestroy(comm_);
     if (ipc_on_) {
       hipDeviceSynchronize();
@@ -475,8 +482,11 @@ class SmddpBackend : public c10d::Backend {
     for (auto& t : touched) TORCH_CHECK(t.is_cuda(), "smddp: tensors must live on the GPU (SMDDP is GPU-only)");
     c10::hip::HIPGuardMasqueradingAsCUDA dg((c10::DeviceIndex)device_);
     auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_);
-    HIPCHECK(hipEventRecord(ready_, cur.stream()));
-    HIPCHECK(hipStreamWaitEvent(comm_stream_.stream(), ready_, 0));
+    // a ring of producer events: an event is re-recorded only after kReady later collectives, never
+    // while the comm stream's wait on its previous record may still be pending
+    hipEvent_t ready = ready_[ready_next_++ % kReady];
+    HIPCHECK(hipEventRecord(ready, cur.stream()));
+    HIPCHECK(hipStreamWaitEvent(comm_stream_.stream(), ready, 0));
     for (auto& t : touched)
       c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(),
                                                                                        comm_stream_);
@@ -770,7 +780,9 @@ class SmddpBackend : public c10d::Backend {
   int* ipc_err_dev_ = nullptr;
   uint32_t ipc_epoch_ = 0;
   uint32_t ipc_spin_limit_ = 4000000;  // x s_sleep(8): seconds, then the error word (never a hang)
-  hipEvent_t ready_;
+  static constexpr int kReady = 64;
+  hipEvent_t ready_[kReady];
+  uint64_t ready_next_ = 0;
   size_t chunk_bytes_ = 0;
   std::mutex mu_;
   std::deque<std::shared_ptr<DoneEvent>> pending_;

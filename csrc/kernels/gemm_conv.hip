@@ -38,6 +38,12 @@
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
 #endif
+#ifndef MI_NT_EPI_PIPE
+#define MI_NT_EPI_PIPE 0  // NT epilogue operand loads software-pipelined one group ahead (A/B)
+#endif
+#ifndef MI_NT_EPI_EU
+#define MI_NT_EPI_EU 4  // NT epilogue: row steps whose operand loads are issued together
+#endif
 #ifndef MI_NT_BLOCKS_PER_CU
 #define MI_NT_BLOCKS_PER_CU 4
 #endif
@@ -606,21 +612,27 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   }
   // row steps in groups of EU: a group's global operand loads (residual C, relu source, BN input,
   // epilogue aux) are all issued before its first store, so their latency overlaps instead of
-  // serialising behind each step's store (the compiler cannot move a load across a store to C)
+  // serialising behind each step's store (the compiler cannot move a load across a store to C).
+  // MI_NT_EPI_PIPE: software-pipelined -- group g + 1's loads are issued before group g is
+  // processed and stored, so operand loads stay in flight through every store phase (two register
+  // slots of EU steps; the default EU halves so the register footprint is unchanged)
   constexpr int NSTEP = BM / RPP;
-  constexpr int EU = NSTEP < 4 ? NSTEP : 4;
-#pragma unroll
-  for (int s0 = 0; s0 < NSTEP; s0 += EU) {
-    uint4 cv[EU], yq[EU], xq[EU];
-    size_t offs[EU];
-    bool ok[EU];
+  constexpr int EU0 = MI_NT_EPI_PIPE ? (MI_NT_EPI_EU / 2 > 0 ? MI_NT_EPI_EU / 2 : 1) : MI_NT_EPI_EU;
+  constexpr int EU = NSTEP < EU0 ? NSTEP : EU0;
+  constexpr int NG = NSTEP / EU;
+  static_assert(NSTEP % EU == 0, "epilogue groups must tile the row steps");
+  constexpr int SLOTS = MI_NT_EPI_PIPE ? 2 : 1;
+  uint4 cv[SLOTS][EU], yq[SLOTS][EU], xq[SLOTS][EU];
+  size_t offs[SLOTS][EU];
+  bool ok[SLOTS][EU];
+  auto load_grp = [&](int g, int sl) {
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
-      const int m = m0 + rr + (s0 + u) * RPP;
-      ok[u] = m < Mlim && n < a.N;
-      offs[u] = ok[u] ? row_off(m) + n : 0;
+      const int m = m0 + rr + (g * EU + u) * RPP;
+      ok[sl][u] = m < Mlim && n < a.N;
+      offs[sl][u] = ok[sl][u] ? row_off(m) + n : 0;
       bool acc_ok = true;  // the accumulated-into operand exists at this pixel (aux_even)
-      if (ok[u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
+      if (ok[sl][u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
         if (a.mode == 3) {
           acc_ok = cls == 0;  // stride-2 parity class (0, 0) = even h, even w
         } else {
@@ -629,26 +641,29 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
           acc_ok = ((h | w) & 1u) == 0u;
         }
       }
-      if (ok[u] && a.epi >= 4) {
-        if (a.epi == 5) cv[u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[u]) : make_uint4(0, 0, 0, 0);
+      if (ok[sl][u] && a.epi >= 4) {
+        if (a.epi == 5)
+          cv[sl][u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
 #if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
-        if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
-        if (a.bn_relu) yq[u] = xq[u];
+        if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
+        if (a.bn_relu) yq[sl][u] = xq[sl][u];
 #else
-        if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
-        if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
+        if (a.bn_relu) yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+        if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
 #endif
-      } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
-        yq[u] = acc_ok ? *(const uint4*)(a.aux + offs[u]) : make_uint4(0, 0, 0, 0);
+      } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
+        yq[sl][u] = acc_ok ? *(const uint4*)(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
       }
     }
+  };
+  auto proc_grp = [&](int g, int sl) {
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
-      if (!ok[u]) continue;
-      const int ml = rr + (s0 + u) * RPP;
+      if (!ok[sl][u]) continue;
+      const int ml = rr + (g * EU + u) * RPP;
       uint4 v = *(const uint4*)&Ct[ml * CST + cc * 8];
       if ((ml >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // undo the write swizzle
-      const size_t off = offs[u];
+      const size_t off = offs[sl][u];
       MI_ASSERT(off + 8 <= (size_t)(a.mode == 3 ? a.M : Mrows) * a.ldc, (long long)off);
       uint4 o = v;
       if (a.epi >= 4) {
@@ -658,25 +673,25 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         unpack8(v, f);
         if (a.epi == 5) {
           float c0[8];
-          unpack8(cv[u], c0);
+          unpack8(cv[sl][u], c0);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += c0[q];
         }
         if (a.bn_relu) {
           float yv[8];
-          unpack8(yq[u], yv);
+          unpack8(yq[sl][u], yv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] = yv[q] > 0.f ? f[q] : 0.f;
         }
         o = pack8(f);
         if (a.stats) {
           float xv[8];
-          unpack8(xq[u], xv);
+          unpack8(xq[sl][u], xv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * (xv[q] - mu[q]); }
         }
       } else {
-        if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[u]);
+        if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[sl][u]);
         if (a.stats) {
           float f[8];
           unpack8(v, f);
@@ -692,6 +707,20 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       else
         *(uint4*)((bf16_t*)a.C + off) = o;
 #endif
+    }
+  };
+  if constexpr (MI_NT_EPI_PIPE) {
+    load_grp(0, 0);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) load_grp(g + 1, (g + 1) & 1);
+      proc_grp(g, g & 1);
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      load_grp(g, 0);
+      proc_grp(g, 0);
     }
   }
   if (a.stats) {

@@ -730,7 +730,8 @@ class DataParallel(nn.Module):
     def _gate_stream(self):
         s = getattr(self, "_gate_s", None)
         if s is None:
-            s = self._gate_s = torch.cuda.Stream(device=self.flat.grad.device)
+            s = self._gate_s = torch.cuda.Stream(device=self.flat.grad.device,
+                                                 priority=int(os.environ.get("MI355X_DP_GATE_PRIO", "0")))
         return s
 
     def _gate_trace_begin(self):
@@ -739,6 +740,22 @@ class DataParallel(nn.Module):
         t0 = torch.cuda.Event(enable_timing=True)
         t0.record()
         return {"t0": t0, "gates": [], "end": None}
+
+    def _smddp_comm_stream(self):
+        """the native smddp backend's comm stream (a torch ExternalStream), or None"""
+        if "_smddp_cs" not in self.__dict__:
+            cs = None
+            try:
+                from . import comm_paths
+                mod = comm_paths._native()
+                pg = self.process_group if self.process_group is not None else dist.distributed_c10d._get_default_group()
+                if mod is not None and str(dist.get_backend(pg)) == "smddp":
+                    h = int(mod.comm_stream(comm_paths.backend_of(pg)))
+                    cs = torch.cuda.ExternalStream(h, device=self.flat.grad.device)
+            except Exception:
+                cs = None
+            self._smddp_cs = cs
+        return self._smddp_cs
 
     def _gated_launch(self, step, trace=None):
         """After a replay of a captured backward: bucket b's collective is launched from the gate
@@ -750,12 +767,17 @@ class DataParallel(nn.Module):
             trace["end"] = torch.cuda.Event(enable_timing=True)
             trace["end"].record()
         gs = self._gate_stream()
+        # the native smddp backend: each gate kernel goes straight onto the backend's comm stream
+        # and the collective is issued from the (idle) gate stream, so the comm stream waits on
+        # nothing else.  (Gating through a cross-stream event from the gate stream made the smddp
+        # path ~4x slower at world 1 -- host launches stalled; profiles/graph_bucket_gates.md.)
+        comm = self._smddp_comm_stream()
         with torch.cuda.stream(gs):
             for b, idxs in enumerate(self.buckets):
-                step.gates.gate(b, step.replays, gs)
+                step.gates.gate(b, step.replays, gs if comm is None else comm)
                 if trace is not None:
                     ev = torch.cuda.Event(enable_timing=True)
-                    ev.record(gs)
+                    ev.record(gs if comm is None else comm)
                     trace["gates"].append(ev)
                 for i in idxs:
                     self.reducer.mark_ready(i)

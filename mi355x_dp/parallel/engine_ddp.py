@@ -94,7 +94,14 @@ class DistributedDataParallel(metaclass=_FactoryMeta):
             from .ddp import DataParallel
             kw = dict(kwargs)
             kw.setdefault("broadcast_buffers", True)
-            return DataParallel(module, foreign_optimizer=True, **kw)
+            eng = DataParallel(module, foreign_optimizer=True, **kw)
+            if eng.rank == 0:
+                # precision honesty: the reference trains in fp32 (TF32-class
+                # convs on A100); the engine's native kernels compute in bf16
+                print("[mi355x_dp] DistributedDataParallel -> native engine: compute dtype bf16 (MFMA, fp32 "
+                      "accumulation), fp32 master weights, fp32 gradients and all-reduce "
+                      f"({len(eng.buckets)} buckets, world {eng.world_size})", flush=True)
+            return eng
         return stock_ddp()(module, **kwargs)
 
 

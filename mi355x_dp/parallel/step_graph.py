@@ -46,6 +46,7 @@ MODE = os.environ.get("MI355X_DP_ENGINE_GRAPH", "auto")
 MAX_NUMEL = int(os.environ.get("MI355X_DP_ENGINE_GRAPH_MAX_NUMEL", str(1 << 22)))
 AFTER = int(os.environ.get("MI355X_DP_ENGINE_GRAPH_AFTER", "2"))
 WARMUP = 2
+GATES = os.environ.get("MI355X_DP_GRAPH_GATES", "1") != "0"
 
 
 class _Replay(torch.autograd.Function):
@@ -132,8 +133,9 @@ class CapturedStep:
         self.pending = None  # weakref to the last graphed output until its backward ran
         # per-bucket gates (native reducer, collectives on): bucket k launches behind its own
         # gradients instead of behind the whole replayed backward
+        # (MI355X_DP_GRAPH_GATES=0: every bucket launched after the whole replay, the round-3 path)
         self.gates = (BucketGates(len(engine.buckets)) if engine.comm_on and engine.reducer is not None
-                      and engine._comm_hook is None else None)
+                      and engine._comm_hook is None and GATES else None)
         mod = engine.module
         dev = x.device
         self.static_x = torch.empty_strided(tuple(x.shape), tuple(x.stride()), dtype=x.dtype, device=dev)
@@ -163,12 +165,14 @@ class CapturedStep:
             pool = torch.cuda.graph_pool_handle()
             self.fwd = torch.cuda.CUDAGraph()
             self.bwd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.fwd, pool=pool, stream=s):
+            # thread_local: another thread's runtime calls (the smddp backend's watchdog polling its
+            # collectives' events) must not invalidate this capture
+            with torch.cuda.graph(self.fwd, pool=pool, stream=s, capture_error_mode="thread_local"):
                 out = mod(self.static_x)
             if not isinstance(out, torch.Tensor):
                 raise TypeError("graphed forward: the module must return one tensor")
             self.static_gout = torch.empty_like(out)
-            with torch.cuda.graph(self.bwd, pool=pool, stream=s):
+            with torch.cuda.graph(self.bwd, pool=pool, stream=s, capture_error_mode="thread_local"):
                 if self.gates is not None:
                     engine._begin_capture_marks(self.gates, s)
                 try:

@@ -106,3 +106,16 @@ def test_result_line_detection(line, ok):
     sys.path.insert(0, ROOT)
     import importlib
     assert importlib.import_module("bench")._is_result(line) is ok
+
+
+def test_post_timing_smddp_job_on_cpu_ranks():
+    """after the timed region rank 0 starts the same step as a fresh N-rank job
+    through the native `smddp` backend name (on CPU ranks it falls back to gloo) and reports it in
+    the JSON line; the headline fields are the parent job's (backend gloo / nccl)."""
+    rc, lines, err = _run(["--gpus", "2"] + SMALL, env=_env(MI355X_DP_BENCH_SMDDP_JOB="1"))
+    assert rc == 0, err[-3000:]
+    d = _check(lines, 2)
+    j = d["smddp_job"]
+    assert isinstance(j, dict), j
+    assert j["backend"] == "smddp" and j["ranks_seen"] == 2 and j["replicas_identical"] is True, j
+    assert j["img_s"] > 0 and j["buckets"] == d["config"]["buckets"]

@@ -17,3 +17,18 @@ def test_training_trajectory_matches_stock_fp32():
     for i, (o, r) in enumerate(zip(ours, ref)):
         assert abs(o - r) <= 0.05 * abs(r) + 0.02, (i, ours, ref)
     assert ours[-1] < 0.7 * ours[0], ours  # it learns the batch
+
+
+def test_reference_shape_trajectory_matches_stock_fp32():
+    """the reference's own shape (ResNet-18, 1000-class head, 32x32, batch 32,
+    lr 0.01, momentum 0.9) for 150 steps of fresh learnable batches, through the engine-backed DDP
+    + stock SGD (graphed after two eager steps), against stock PyTorch fp32 on the same GPU: the
+    10-step mean losses track each other and both curves learn."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import ref_trajectory
+    ours, ref, graphed = ref_trajectory.run(150)
+    assert graphed == 148
+    wo, wr = ref_trajectory.windows(ours), ref_trajectory.windows(ref)
+    for i, (o, r) in enumerate(zip(wo, wr)):
+        assert abs(o - r) <= 0.06 * r + 0.05, (i, wo, wr)
+    assert wo[-1] < 0.75 * wo[0] and wr[-1] < 0.75 * wr[0], (wo, wr)

@@ -1,0 +1,95 @@
+#!/usr/bin/env python
+"""Trajectory parity at the reference's OWN training shape: torchvision-layout
+ResNet-18 with the 1000-class head on 32x32 CIFAR-shaped images, batch 32 per GPU, SGD lr 0.01
+momentum 0.9 (cifar10-distributed-smddp-gpu.py:145-168, hyperparameters nb2:110-115), through the
+same user-level path as the reference script -- the engine-backed DistributedDataParallel with
+stock ``optim.SGD`` (bf16 MFMA compute, fp32 master weights; graphed steps after two eager ones)
+-- against stock PyTorch fp32 (ATen / MIOpen) from the same initial weights on the same batches.
+
+The data is the synthetic CIFAR-10 stand-in (mi355x_dp/data/cifar.py: class templates +
+distractors + noise, learnable), a new batch every step, normalised with the reference's
+constants (gpu.py:55-62).  Prints one JSON line with both loss curves.
+
+    python tools/ref_trajectory.py --steps 150
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+MEAN = (0.4914, 0.4822, 0.4465)
+STD = (0.2023, 0.1994, 0.2010)
+
+
+def batches(steps, batch, seed=0):
+    from mi355x_dp.data.cifar import _class_templates, _make_split
+    rng = np.random.default_rng(seed)
+    x, y = _make_split(rng, _class_templates(rng), steps * batch)
+    x = torch.from_numpy(x).permute(0, 3, 1, 2).float().div_(255)
+    x = (x - torch.tensor(MEAN).view(1, 3, 1, 1)) / torch.tensor(STD).view(1, 3, 1, 1)
+    y = torch.from_numpy(y).long()
+    return [(x[i * batch:(i + 1) * batch], y[i * batch:(i + 1) * batch]) for i in range(steps)]
+
+
+def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1):
+    from mi355x_dp.models import get_model
+    from mi355x_dp.models.stock import stock_resnet
+    from mi355x_dp.parallel import DataParallel
+    dev = torch.device("cuda", 0)
+    data = batches(steps, batch)
+    torch.manual_seed(seed)  # the reference seeds before building the model (gpu.py:120)
+    ours = get_model("resnet18", num_classes=1000).to(dev)
+    init = {k: v.detach().clone() for k, v in ours.state_dict().items()}
+    eng = DataParallel(ours, foreign_optimizer=True)  # what the torch_smddp shim's DDP returns
+    opt = torch.optim.SGD(eng.parameters(), lr=lr, momentum=momentum)
+    crit = torch.nn.CrossEntropyLoss().to(dev)
+    ours_loss = []
+    for x, y in data:
+        x, y = x.to(dev), y.to(dev)
+        opt.zero_grad()
+        loss = crit(eng(x), y)
+        loss.backward()
+        opt.step()
+        ours_loss.append(float(loss))
+    graphed = sum(s.replays for s in getattr(eng, "_graphs", {}).values())
+
+    ref = stock_resnet("resnet18", 1000).to(dev)
+    ref.load_state_dict(init)
+    ropt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=momentum)
+    prev = torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False  # true fp32
+    ref_loss = []
+    for x, y in data:
+        x, y = x.to(dev), y.to(dev)
+        ropt.zero_grad()
+        loss = F.cross_entropy(ref(x), y)
+        loss.backward()
+        ropt.step()
+        ref_loss.append(float(loss))
+    torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = prev
+    return ours_loss, ref_loss, graphed
+
+
+def windows(v, k=10):
+    return [float(np.mean(v[i:i + k])) for i in range(0, len(v) - k + 1, k)]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=150)
+    a = p.parse_args()
+    ours, ref, graphed = run(a.steps)
+    print(json.dumps({"model": "resnet18 (1000-class head)", "image": 32, "batch": 32, "lr": 0.01, "momentum": 0.9,
+                      "steps": a.steps, "graphed_steps": graphed, "engine_bf16": ours, "stock_fp32": ref,
+                      "engine_window10": windows(ours), "stock_window10": windows(ref)}))
+
+
+if __name__ == "__main__":
+    main()
