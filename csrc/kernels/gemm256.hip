@@ -46,6 +46,12 @@
 #ifndef MI_G256_EPI_U0
 #define MI_G256_EPI_U0 8  // plain-GEMM epilogue: row steps per group of batched operand loads (A/B)
 #endif
+#ifndef MI_G256_EPI_PIPE
+#define MI_G256_EPI_PIPE 0  // conv epilogue operand loads software-pipelined one group ahead (A/B)
+#endif
+#ifndef MI_G256_EPI_UBN
+#define MI_G256_EPI_UBN 4  // conv epilogues (BN statistics / BN backward): row steps per load group
+#endif
 #ifndef MI_FENCE_HANDOFF
 #define MI_FENCE_HANDOFF 0  // 1: tail split-K hand-off through a __threadfence pair (A/B only)
 #endif
@@ -419,47 +425,54 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
             make_uint2(pack2bf(v[0] + bv[j][0], v[1] + bv[j][1]), pack2bf(v[2] + bv[j][2], v[3] + bv[j][3]));
       }
     lgkm_wait0();
-    // 8 row steps in 2 groups of EPI_U: a group's global operand loads (residual C, relu source,
+    // 8 row steps in groups of EPI_U: a group's global operand loads (residual C, relu source,
     // BN input) are all issued before its first store, so their HBM latency overlaps instead of
-    // serialising behind each step's store (the compiler cannot move a load across a store to C)
-    constexpr int EPI_U = MODE == 0 ? MI_G256_EPI_U0 : 4;
-#pragma unroll
-    for (int s0 = 0; s0 < 8; s0 += EPI_U) {
-      uint4 cv[EPI_U], yq[EPI_U], xq[EPI_U];
-      size_t offs[EPI_U];
-      bool ok[EPI_U];
+    // serialising behind each step's store (the compiler cannot move a load across a store to C).
+    // MI_G256_EPI_PIPE (conv epilogues): group g + 1's loads are issued before group g is processed
+    // and stored -- two register slots of half the group size, the same footprint
+    constexpr bool PIPE = BN_EPI && MI_G256_EPI_PIPE;
+    constexpr int EPI_U = MODE == 0 ? MI_G256_EPI_U0 : (PIPE ? MI_G256_EPI_UBN / 2 : MI_G256_EPI_UBN);
+    constexpr int NG = 8 / EPI_U;
+    constexpr int SL = PIPE ? 2 : 1;
+    uint4 cv[SL][EPI_U], yq[SL][EPI_U], xq[SL][EPI_U];
+    size_t offs[SL][EPI_U];
+    bool ok[SL][EPI_U];
+    auto load_grp = [&](int g, int sl) {
 #pragma unroll
       for (int u = 0; u < EPI_U; ++u) {
-        const int rl = (s0 + u) * 8 + (lane >> 3);
+        const int rl = (g * EPI_U + u) * 8 + (lane >> 3);
         const int m = m0 + wm * 128 + mq * 64 + rl;
-        ok[u] = m < a.M && n < a.N;
-        offs[u] = ok[u] ? (size_t)m * a.ldc + n : 0;
+        ok[sl][u] = m < a.M && n < a.N;
+        offs[sl][u] = ok[sl][u] ? (size_t)m * a.ldc + n : 0;
         bool acc_ok = true;
-        if (BN_EPI && ok[u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
+        if (BN_EPI && ok[sl][u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
           const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
           const uint32_t h = fdiv(rem, a.fQ), w = rem - h * a.fQ.d;
           acc_ok = ((h | w) & 1u) == 0u;
         }
-        if (BN_EPI && ok[u] && a.epi >= 4) {
-          if (a.epi == 5) cv[u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[u]) : make_uint4(0, 0, 0, 0);
+        if (BN_EPI && ok[sl][u] && a.epi >= 4) {
+          if (a.epi == 5)
+            cv[sl][u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
 #if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
-          if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
-          if (a.bn_relu) yq[u] = xq[u];
+          if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
+          if (a.bn_relu) yq[sl][u] = xq[sl][u];
 #else
-          if (a.bn_relu) yq[u] = *(const uint4*)(a.aux + offs[u]);
-          if (a.stats) xq[u] = *(const uint4*)(a.aux2 + offs[u]);
+          if (a.bn_relu) yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+          if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
 #endif
-        } else if (ok[u] && (a.epi == 2 || a.epi == 3)) {
-          yq[u] = acc_ok ? *(const uint4*)(a.aux + offs[u]) : make_uint4(0, 0, 0, 0);
+        } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
+          yq[sl][u] = acc_ok ? *(const uint4*)(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
         }
       }
+    };
+    auto proc_grp = [&](int g, int sl) {
 #pragma unroll
       for (int u = 0; u < EPI_U; ++u) {
-        const int rl = (s0 + u) * 8 + (lane >> 3);
+        const int rl = (g * EPI_U + u) * 8 + (lane >> 3);
         uint4 v = *(const uint4*)&Ct[rl * CST + cc * 8];
         if ((rl >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // undo the write swizzle
-        if (!ok[u]) continue;
-        const size_t off = offs[u];
+        if (!ok[sl][u]) continue;
+        const size_t off = offs[sl][u];
         MI_ASSERT(n + 8 <= a.N, n);
         uint4 o = v;
         if (BN_EPI && a.epi >= 4) {
@@ -467,25 +480,25 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
           unpack8(v, f);
           if (a.epi == 5) {  // dy = this dgrad + the gradient already in C (residual sum)
             float c0[8];
-            unpack8(cv[u], c0);
+            unpack8(cv[sl][u], c0);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] += c0[q];
           }
           if (a.bn_relu) {
             float yv[8];
-            unpack8(yq[u], yv);
+            unpack8(yq[sl][u], yv);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] = yv[q] > 0.f ? f[q] : 0.f;
           }
           o = pack8(f);
           if (a.stats) {
             float xv[8];
-            unpack8(xq[u], xv);
+            unpack8(xq[sl][u], xv);
 #pragma unroll
             for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * (xv[q] - mu[q]); }
           }
         } else {
-          if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[u]);
+          if (a.epi) o = epilogue_op_v(a.epi, v, a.aux + off, yq[sl][u]);
           if (has_stats) {
             float f[8];
             unpack8(v, f);
@@ -498,6 +511,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #else
         *(uint4*)((bf16_t*)a.C + off) = o;
 #endif
+      }
+    };
+    if constexpr (PIPE) {
+      load_grp(0, 0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (g + 1 < NG) load_grp(g + 1, (g + 1) & 1);
+        proc_grp(g, g & 1);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        load_grp(g, 0);
+        proc_grp(g, 0);
       }
     }
     lgkm_wait0();  // this wave's reads of the slice retire before the next quadrant row overwrites it
