@@ -114,6 +114,15 @@ struct NTArgs {
   float* ws;
   int splits, ksplit;
   int* cnt;          // SPLIT 3: per-tile arrival counters (zero between launches)
+  // normalize-on-load (NOL kernels): the gathered A operand of a conv forward is the raw output c
+  // of the previous conv and the kernel applies that layer's BatchNorm + ReLU as it stages it:
+  // a <- relu(c * nol_scale[ch] + nol_shift[ch]) (padding stays 0); the inner BN's output y is never
+  // written.  mask_scale / mask_shift: epi 4 takes the ReLU mask from aux2 (= c) as
+  // fma(c, scale, shift) > 0 instead of reading y (aux)
+  const float* nol_scale;
+  const float* nol_shift;
+  const float* mask_scale;
+  const float* mask_shift;
   ConvGeom g;
 };
 
@@ -129,6 +138,9 @@ struct TNArgs {
   float* colsum;    // optional [M] fp32 += column sums of A (a Linear layer's bias gradient)
   float* ws;        // split-K partial slabs [tiles][splits][BM*BN] (fragment order), or null: atomics
   int* cnt;         // per-tile arrival counters: the last-arriving split sums the slabs (no reduce launch)
+  // normalize-on-load of the gathered input (conv mode, NOL kernels): b <- relu(x * scale[c] + shift[c])
+  const float* nol_scale;
+  const float* nol_shift;
   ConvGeom g;
 };
 
@@ -141,12 +153,30 @@ constexpr int BK = 64;
 // halo tile capacity (pixels of one 64-channel chunk, 128 B each): (rp + 2) x (Q + 2) <= HALO_PX
 constexpr int HALO_PX = 256;
 
-template <int BM, int BN, int STAGES, bool HALO = false>
-constexpr int nt_smem_u4() {
-  // max(staging ring, epilogue C tile [BM][BN+8] bf16 + stats scratch [4 waves][2][BN] fp32)
-  constexpr int stage = HALO ? HALO_PX * 8 + 2 * BN * 8 : STAGES * (BM + BN) * 8;
+// normalize-on-load: per-channel (scale, shift) table of the gathered tensor, right after the
+// staging ring (the epilogue, which never needs it, may overwrite it); channels <= NOL_MAX_C
+constexpr int NOL_MAX_C = 256;
+constexpr int NOL_TAB_U4 = 2 * NOL_MAX_C * 4 / 16;
+
+template <int BM, int BN, int STAGES, bool HALO = false, bool NOL = false>
+constexpr int nt_smem_u4() {  // NOL: the forward (normalize-on-load) variant's table
+  // max(staging ring (+ NOL table), epilogue C tile [BM][BN+8] bf16 + stats scratch [4 waves][2][BN] fp32)
+  constexpr int stage = (HALO ? HALO_PX * 8 + 2 * BN * 8 : STAGES * (BM + BN) * 8) + (NOL ? NOL_TAB_U4 : 0);
   constexpr int epi = (BM * (BN + 8) * 2 + 4 * 2 * BN * 4) / 16;
   return stage > epi ? stage : epi;
+}
+
+// relu(x * s + h) on one staged 16-B chunk of 8 bf16 (channel-consecutive)
+__device__ __forceinline__ void nol_chunk(uint4* p, const float* tab, int ch) {
+  float sc[8], sh[8], f[8];
+  *(float4*)&sc[0] = *(const float4*)&tab[ch];
+  *(float4*)&sc[4] = *(const float4*)&tab[ch + 4];
+  *(float4*)&sh[0] = *(const float4*)&tab[NOL_MAX_C + ch];
+  *(float4*)&sh[4] = *(const float4*)&tab[NOL_MAX_C + ch + 4];
+  unpack8(*p, f);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) f[q] = fmaxf(fmaf(f[q], sc[q], sh[q]), 0.f);
+  *p = pack8(f);
 }
 
 // blocks per CU the NT kernel is compiled for: 4 single-stage blocks (38 KB of LDS each at 128x128,
@@ -167,17 +197,32 @@ constexpr int nt_occupancy() {
 // into LDS and all nine taps read their A fragments from it (shifted row addresses), with the
 // weight tile of the next tap loading into the other B buffer during each tap's MFMAs.  The
 // per-tap gather re-reads every input pixel ~9x through L2; the halo reads it ~(rp+2)/rp x.
-template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false, int SPLIT = 0>
+// NOL: 0 off, 1 normalize-on-load of the gathered A operand (conv forward), 2 epi-4 ReLU mask from c
+// (data gradient) -- separate instantiations, so each carries only its own registers
+template <int BM, int BN, int STAGES, bool SMALLC, bool HALO = false, int SPLIT = 0, int NOL = 0>
 __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_kernel(NTArgs a) {
   static_assert(SPLIT == 0 || (STAGES == 1 && !SMALLC && !HALO), "split-K: single-stage gather/plain tiles only");
+  static_assert(NOL == 0 || (STAGES == 1 && !SMALLC && SPLIT == 0), "normalize-on-load: single-stage gather tiles");
   // SPLIT 3: as SPLIT 1, then the last-arriving split of each tile sums all the partial tiles (in
   // split order) and runs the epilogue -- one launch instead of SPLIT 1 + SPLIT 2
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-byte chunks per thread per k-step
-  __shared__ __attribute__((aligned(16))) uint4 smem[nt_smem_u4<BM, BN, STAGES, HALO>()];
+  __shared__ __attribute__((aligned(16))) uint4 smem[nt_smem_u4<BM, BN, STAGES, HALO, NOL == 1>()];
   uint4* As = smem;                      // [STAGES][BM][8]
   uint4* Bs = smem + STAGES * BM * 8;    // [STAGES][BN][8]
+  // NOL: [scale[NOL_MAX_C], shift[NOL_MAX_C]] of the gathered tensor's channels, staged once
+  float* nol_tab = (float*)(smem + (HALO ? HALO_PX * 8 + 2 * BN * 8 : STAGES * (BM + BN) * 8));
+  const bool nol_a = NOL == 1 && a.nol_scale != nullptr && a.mode == 1;
+  if constexpr (NOL == 1) {
+    if (nol_a) {
+      for (int c = threadIdx.x; c < a.g.Cs; c += 256) {
+        nol_tab[c] = a.nol_scale[c];
+        nol_tab[NOL_MAX_C + c] = a.nol_shift[c];
+      }
+      __syncthreads();
+    }
+  }
 
   const int nbn = (a.N + BN - 1) / BN;
   // mode 3: one parity class per grid row (blockIdx.y).  Folding the classes into an XCD-aware
@@ -289,8 +334,12 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
     dts4 = 8 % a.g.S; dtr4 = 8 / a.g.S; ntaps = a.g.R * a.g.S;
   }
 
+  uint32_t a_okm = 0;  // NOL: A chunks of the last issued k-step that hold real pixels
+  int a_kc = 0;        // NOL: their channel-chunk base
   auto issue_loads = [&](int kt, int buf) {
     int r, s, koffA, kB;
+    a_okm = 0;
+    a_kc = kc;
     if (SMALLC || a.mode == 0) {
       r = 0; s = 0;
       koffA = SMALLC ? (tr4 * W + ts4) * Cs : kt * BK;
@@ -316,6 +365,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         ok = ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       }
       const uint32_t vo = ok ? (uint32_t)(a_base[i] + koffA) * 2u : OOB;
+      a_okm |= (ok ? 1u : 0u) << i;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &As[(buf * BM + 32 * i + 8 * wid) * 8]), 16, vo,
                                                0, 0, 0);
     }
@@ -432,6 +482,19 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       load_halo(kc);
       load_b(0, kc, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NOL == 1) {
+        if (nol_a) {  // each thread normalizes the halo chunks its own DMA wrote (padding stays 0)
+          for (int it = 0; it < nit; ++it) {
+            const int f = it * 256 + tid;
+            const int px = f >> 3, chp = f & 7;
+            const uint32_t hr = fdiv((uint32_t)px, a.fHW2);
+            const int hc = px - (int)hr * HW2;
+            const int ih = hp0 - 1 + (int)hr, iw = hc - 1;
+            if (px < HP && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+              nol_chunk(&Hs[f], nol_tab, kc + (chp ^ (px & 7)) * 8);
+          }
+        }
+      }
       __syncthreads();
       for (int t = 0; t < 9; ++t) {
         if (t + 1 < 9) load_b(t + 1, kc, (t + 1) & 1);
@@ -473,6 +536,13 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       issue_loads(kt, 0);
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NOL == 1) {
+        if (nol_a) {  // this thread's own A chunks (one row each, logical chunk lc), real pixels only
+#pragma unroll
+          for (int i = 0; i < A_CH; ++i)
+            if ((a_okm >> i) & 1u) nol_chunk(&As[(32 * i + 8 * wid) * 8 + lane], nol_tab, a_kc + lc * 8);
+        }
+      }
       __syncthreads();
       compute(0);
       __syncthreads();
@@ -610,6 +680,23 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
     *(float4*)&mu[0] = *(const float4*)(a.mean + n);
     *(float4*)&mu[4] = *(const float4*)(a.mean + n + 4);
   }
+  // NOL kernels, epi 4 with mask coefficients: ReLU mask from c (aux2) -- the BN output y is
+  // never read (it was never written: its consumer normalized on load)
+  // as a per-channel threshold: fma(c, s, h) > 0  <=>  c > -h/s (s > 0), c < -h/s (s < 0), h > 0 (s == 0)
+  // -- 8 thresholds and a sign mask instead of 16 coefficients in registers (the 128x128 variant
+  // spilled with the coefficients); differs from the fma only where c * s + h rounds to ~0
+  constexpr bool MASKC = NOL == 2;  // every launch of this variant takes its mask from c
+  const bool mask_c = MASKC;
+  float mthr[MASKC ? 8 : 1];
+  uint32_t mgt = 0;  // bit q: keep where c > thr[q] (else where c < thr[q])
+  if constexpr (MASKC) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float sc = n < a.N ? a.mask_scale[n + q] : 1.f, sh = n < a.N ? a.mask_shift[n + q] : 0.f;
+      mthr[q] = sc != 0.f ? -sh / sc : (sh > 0.f ? -INFINITY : INFINITY);
+      mgt |= (sc >= 0.f ? 1u : 0u) << q;
+    }
+  }
   // row steps in groups of EU: a group's global operand loads (residual C, relu source, BN input,
   // epilogue aux) are all issued before its first store, so their latency overlaps instead of
   // serialising behind each step's store (the compiler cannot move a load across a store to C).
@@ -617,7 +704,9 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   // processed and stored, so operand loads stay in flight through every store phase (two register
   // slots of EU steps; the default EU halves so the register footprint is unchanged)
   constexpr int NSTEP = BM / RPP;
-  constexpr int EU0 = MI_NT_EPI_PIPE ? (MI_NT_EPI_EU / 2 > 0 ? MI_NT_EPI_EU / 2 : 1) : MI_NT_EPI_EU;
+  // (the mask-from-c 128x128 variant loads one operand per step instead of two: half the group)
+  constexpr int EU1 = (NOL == 2 && BN == 128) ? MI_NT_EPI_EU / 2 : MI_NT_EPI_EU;
+  constexpr int EU0 = MI_NT_EPI_PIPE ? (EU1 / 2 > 0 ? EU1 / 2 : 1) : EU1;
   constexpr int EU = NSTEP < EU0 ? NSTEP : EU0;
   constexpr int NG = NSTEP / EU;
   static_assert(NSTEP % EU == 0, "epilogue groups must tile the row steps");
@@ -648,8 +737,8 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
         if (a.bn_relu) yq[sl][u] = xq[sl][u];
 #else
-        if (a.bn_relu) yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
-        if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
+        if (!MASKC && a.bn_relu) yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+        if (a.stats || mask_c) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
 #endif
       } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
         yq[sl][u] = acc_ok ? *(const uint4*)(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
@@ -677,7 +766,16 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += c0[q];
         }
-        if (a.bn_relu) {
+        if constexpr (MASKC) {
+          float xv[8];
+          unpack8(xq[sl][u], xv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float t = mthr[MASKC ? q : 0];
+            const bool keep = ((mgt >> q) & 1u) ? xv[q] > t : xv[q] < t;
+            f[q] = keep ? f[q] : 0.f;
+          }
+        } else if (a.bn_relu) {
           float yv[8];
           unpack8(yq[sl][u], yv);
 #pragma unroll
@@ -765,9 +863,10 @@ __device__ __forceinline__ int tr_swz(int k) {
 // fused bias-gradient column sums (Linear layers only).  Both are compile-time so that neither the
 // gather bookkeeping nor the colsum accumulators occupy registers in the variants that do not use
 // them (the conv variant fits 128 VGPRs and runs 4 blocks per CU).
-template <int BM, int BN, int STAGES, int MODE = 1, bool CS = false>
+template <int BM, int BN, int STAGES, int MODE = 1, bool CS = false, bool NOL = false>
 __global__ __launch_bounds__(256, STAGES == 1 ? (MODE == 1 && !CS ? MI_TN_CONV_BLOCKS_PER_CU : MI_TN_BLOCKS_PER_CU) : 2)
 void tn_kernel(TNArgs a) {
+  static_assert(!NOL || (MODE == 1 && STAGES == 1 && !CS), "normalize-on-load: conv weight gradients");
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int AU = BM / 4, BU = BN / 4;            // 8-byte units per LDS row
@@ -813,6 +912,16 @@ void tn_kernel(TNArgs a) {
   }
   const int H = a.g.H, W = a.g.W, P = a.g.P, Q = a.g.Q, Cs = a.g.Cs;
   const int st = a.g.stride, pad = a.g.pad;
+  // NOL: this thread's 8 gathered channels c0..c0+7 are fixed for the whole block
+  float nsc[NOL ? 8 : 1], nsh[NOL ? 8 : 1];
+  if constexpr (NOL) {
+    const bool live = n0 + b_lc * 8 < a.N;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      nsc[q] = live ? a.nol_scale[c0 + q] : 0.f;
+      nsh[q] = live ? a.nol_shift[c0 + q] : 0.f;
+    }
+  }
 
   // ---- per-thread B rows (mode 1): output pixel (img, p, q) of reduction row k, advanced by BK
   int b_img[B_CH], b_p[B_CH], b_q[B_CH];
@@ -837,7 +946,9 @@ void tn_kernel(TNArgs a) {
   const int a_m = m0 + a_lc * 8;
   const int b_n = n0 + b_lc * 8;
 
+  uint32_t b_okm = 0;  // NOL: B chunks of the last issued k-step that hold real input pixels
   auto issue_loads = [&](int k0, int buf) {
+    b_okm = 0;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int k = k0 + a_r + A_RSTEP * i;
@@ -856,6 +967,7 @@ void tn_kernel(TNArgs a) {
         const int ih = b_p[i] * st - pad + tap_r, iw = b_q[i] * st - pad + tap_s;
         if (k < kend && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
           vo = (b_n < a.N) ? (uint32_t)((((b_img[i] * H + ih) * W + iw) * Cs) + c0) * 2u : OOB;
+        b_okm |= (vo != OOB ? 1u : 0u) << i;
         // advance this row by BK output pixels
         int q = b_q[i] + dq, p = b_p[i] + dp, img = b_img[i] + dimg;
         if (q >= Q) { q -= Q; ++p; }
@@ -923,6 +1035,18 @@ void tn_kernel(TNArgs a) {
     for (int kt = 0; kt < nk; ++kt) {
       issue_loads(kbeg + kt * BK, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NOL) {  // this thread's own B chunks (real pixels only; padding stays 0)
+#pragma unroll
+        for (int i = 0; i < B_CH; ++i) {
+          if (!((b_okm >> i) & 1u)) continue;
+          uint4* p = (uint4*)&Bs[(B_RSTEP * i + wid * B_RPI) * BU + 2 * lane];
+          float f[8];
+          unpack8(*p, f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = fmaxf(fmaf(f[q], nsc[q], nsh[q]), 0.f);
+          *p = pack8(f);
+        }
+      }
       __syncthreads();
       compute(0);
       __syncthreads();
@@ -1249,6 +1373,24 @@ hipError_t launch_nt(NTArgs& a, hipStream_t st) {
   if (a.halo_rp > 0) a.tiles_m = (a.M / (a.g.P * a.g.Q)) * a.halo_pb;
   int grid = a.tiles_m * cdiv(a.N, BN);
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
+  if (a.nol_scale || a.mask_scale) {
+    // normalize-on-load (forward) / mask-from-c (data gradient) variants: single-stage, no split-K
+    if (a.mode == 4 || (a.nol_scale && (a.mode != 1 || a.g.Cs > NOL_MAX_C)) || (a.mask_scale && a.epi != 4) ||
+        (a.nol_scale && a.mask_scale))
+      return hipErrorNotSupported;
+    if (a.nol_scale) {
+      if (a.halo_rp > 0)
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, true, 0, 1>), dim3(grid), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, false, 0, 1>), dim3(grid, classes), dim3(256), 0, st, a);
+    } else {
+      if (a.halo_rp > 0)
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, true, 0, 2>), dim3(grid), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((nt_kernel<BM, BN, 1, false, false, 0, 2>), dim3(grid, classes), dim3(256), 0, st, a);
+    }
+    return hipGetLastError();
+  }
   if (a.halo_rp == 0 && a.mode != 4 && grid * classes < nt_split_blocks()) {
     const int cpt = a.mode == 0 ? 0 : (int)a.g.fCpt.d;
     const int nk = a.mode == 0 ? cdiv(a.K, BK)
@@ -1438,8 +1580,12 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   // fewer than 8 splits: the reduce is one split group (in-order sum), which the last-arriving
   // split runs itself -- no reduce launch; more splits keep the chip-wide reduce kernel
   const int st_n = glds_on() ? 1 : 2;
-  if (a.ws && splits < 8 && tiles <= SPLITK_COUNTERS && st_n == 1 && tn_split_fused()) a.cnt = splitk_counters(st);
-  if (a.mode == 1) {
+  if (a.ws && splits < 8 && tiles <= SPLITK_COUNTERS && st_n == 1 && tn_split_fused() && !a.nol_scale)
+    a.cnt = splitk_counters(st);
+  if (a.nol_scale) {
+    if (a.mode != 1 || st_n != 1 || a.cnt) return hipErrorNotSupported;
+    hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false, true>), dim3(tiles * splits), dim3(256), 0, st, a);
+  } else if (a.mode == 1) {
     if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
   } else if (a.colsum) {
@@ -1726,14 +1872,33 @@ MI_API int mi_conv2d_dgrad_ex(const void* dy, const void* wt, void* dx, int Nb, 
 // unwritten instead of zero-filling them (a 1x1 / stride-2 data gradient then writes only the even
 // pixels); bit 1 (epi 3 / 5) reads the accumulated-into gradient only at even (h, w) -- the
 // consumer of such a sparse write.  Together they skip 3/4 of a downsample dgrad's bytes.
+MI_API int mi_conv2d_dgrad_ex3(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                               const float* mean, int bn_relu, float* stats, int flags, const float* mask_scale,
+                               const float* mask_shift, hipStream_t st);
+
 MI_API int mi_conv2d_dgrad_ex2(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                                int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
                                const float* mean, int bn_relu, float* stats, int flags, hipStream_t st) {
+  return mi_conv2d_dgrad_ex3(dy, wt, dx, Nb, H, W, C, K, R, S, stride, pad, P, Q, epi, aux, aux2, mean, bn_relu, stats,
+                             flags, nullptr, nullptr, st);
+}
+
+// mi_conv2d_dgrad_ex2 with, for epi 4, the ReLU mask of the producing BN taken from its input c (aux2)
+// as fma(c, mask_scale, mask_shift) > 0 -- aux (the BN output) unused: normalize-on-load schedules
+// never write it.  Only where mi_conv_nol_ok holds (the 128-tile kernels).
+MI_API int mi_conv2d_dgrad_ex3(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                               const float* mean, int bn_relu, float* stats, int flags, const float* mask_scale,
+                               const float* mask_shift, hipStream_t st) {
+  const bool mask_c = mask_scale != nullptr;
+  if (mask_c && (epi != 4 || !mask_shift || !aux2 || !bn_relu)) return (int)hipErrorInvalidValue;
   if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4 || epi == 5) ||
-      (epi && !aux && bn_relu) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)) ||
+      (epi && !aux && bn_relu && !mask_c) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)) ||
       ((flags & 1) && (stride != 2 || epi != 0)) || ((flags & 2) && epi != 3 && epi != 5))
     return (int)hipErrorInvalidValue;
   const int aux_even = (flags >> 1) & 1;
+  if (mask_c && stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K)) return (int)hipErrorNotSupported;
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
     return mi_gemm256_conv2(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
                             bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, st);
@@ -1744,6 +1909,7 @@ MI_API int mi_conv2d_dgrad_ex2(const void* dy, const void* wt, void* dx, int Nb,
   a.epi = epi; a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu;
   a.stats = (epi >= 4) ? stats : nullptr;
   a.aux_even = aux_even;
+  a.mask_scale = mask_scale; a.mask_shift = mask_shift;
   a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
   a.b_bytes = rsrc_bytes((int64_t)C * a.K);
   a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);
@@ -1775,6 +1941,52 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
   a.M = K; a.N = R * S * C; a.K = Nb * P * Q;
   a.lda = K; a.ldb = 0; a.ldc = a.N; a.mode = 1;
+  a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
+  a.b_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
+  a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
+  return (int)dispatch_tn(a, st);
+}
+
+// ---- normalize-on-load (the consumer conv applies the producing BatchNorm + ReLU to its raw input c)
+// 1 if a conv of this geometry can consume a raw BN input with normalize-on-load in the forward
+// (mi_conv2d_fwd_nol), take its data gradient's ReLU mask from c (mi_conv2d_dgrad_nol) and its
+// weight gradient from c (mi_conv2d_wgrad_nol): the 128-tile NT gather / halo kernels and the TN
+// kernel; shapes routed to the stem or 256x256 kernels keep the materialised BN output.
+MI_API int mi_conv_nol_ok(int Nb, int H, int W, int C, int K, int R, int S, int stride, int pad, int P, int Q) {
+  if (C % 64 != 0 || C > NOL_MAX_C || K % 64 != 0 || stride > 2 || !glds_on()) return 0;
+  if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return 0;
+  if (use_gemm256_conv(Nb * P * Q, K, C, R * S * C)) return 0;                    // forward
+  if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K)) return 0;    // data gradient
+  return 1;
+}
+
+MI_API int mi_conv2d_fwd_nol(const void* x, const void* w, void* y, float* stats, const float* nol_scale,
+                             const float* nol_shift, int Nb, int H, int W, int C, int K, int R, int S, int stride,
+                             int pad, int P, int Q, hipStream_t st) {
+  if (!mi_conv_nol_ok(Nb, H, W, C, K, R, S, stride, pad, P, Q) || !nol_scale || !nol_shift)
+    return (int)hipErrorNotSupported;
+  NTArgs a{};
+  a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = nullptr; a.stats = stats;
+  a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
+  a.lda = 0; a.ldb = a.K; a.ldc = K; a.mode = 1; a.out_f32 = 0; a.accumulate = 0;
+  a.nol_scale = nol_scale; a.nol_shift = nol_shift;
+  a.a_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
+  a.b_bytes = rsrc_bytes((int64_t)K * a.K);
+  a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
+  return (int)dispatch_nt(a, st);
+}
+
+MI_API int mi_conv2d_wgrad_nol(const void* x, const void* dy, float* dw, const float* nol_scale,
+                               const float* nol_shift, int Nb, int H, int W, int C, int K, int R, int S, int stride,
+                               int pad, int P, int Q, hipStream_t st) {
+  if (C % 8 != 0 || K % 8 != 0 || C > NOL_MAX_C || !nol_scale || !nol_shift ||
+      use_stem_kernel(C, K, R, S, stride, pad, Q))
+    return (int)hipErrorInvalidValue;
+  TNArgs a{};
+  a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
+  a.M = K; a.N = R * S * C; a.K = Nb * P * Q;
+  a.lda = K; a.ldb = 0; a.ldc = a.N; a.mode = 1;
+  a.nol_scale = nol_scale; a.nol_shift = nol_shift;
   a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
   a.b_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
   a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);

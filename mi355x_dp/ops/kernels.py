@@ -17,6 +17,11 @@ signature("mi_set_nt_split_fused", I)
 signature("mi_set_tn_split_fused", I)
 signature("mi_conv2d_dgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_wgrad", P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
+# normalize-on-load of inner BatchNorms (ops/resblock.py)
+signature("mi_conv_nol_ok", I, I, I, I, I, I, I, I, I, I, I)
+signature("mi_conv2d_fwd_nol", P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_conv2d_wgrad_nol", P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
+signature("mi_conv2d_dgrad_ex3", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P, P, P)
 signature("mi_conv_wtrans", P, P, I, I, I, P)
 signature("mi_conv_wtrans_multi", P, P, P, I, I, P)
 signature("mi_gemm_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, P)

@@ -101,8 +101,30 @@ class _BNSpec:
         self.eps = float(bn.eps)
 
 
+# Normalize-on-load of the inner BatchNorms (bn1 / bn2 of a bottleneck, bn1 of a basic block): the
+# conv that consumes an inner BN's output reads the raw conv output c and applies relu(c * scale +
+# shift) as it stages its operand (forward and weight gradient), and the data gradient that needs
+# that BN's ReLU mask takes it from c -- the BN output y is never written nor read (VERDICT r3
+# item 2; profiles/bn_nol_r4.md).  Per consumer shape, where the 128-tile kernels serve all three
+# (mi_conv_nol_ok); elsewhere y is materialised as before.  MI355X_DP_NOL=0 disables.
+NOL = os.environ.get("MI355X_DP_NOL", "1") != "0"
+NOL_USED = [0]  # diagnostics: inner BNs whose output was normalized on load instead of written
+
+
+def _nol_ok(c, spec) -> bool:
+    """can ``spec``'s conv consume the raw tensor ``c`` (shape of its input) with normalize-on-load?"""
+    if not NOL:
+        return False
+    N, C, H, W = c.shape
+    K, _, R, S = spec.w.shape
+    P, Q = _out_hw(H, R, spec.stride, spec.pad), _out_hw(W, S, spec.stride, spec.pad)
+    return bool(_lib.load().mi_conv_nol_ok(N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q))
+
+
 # ----------------------------------------------------------------------- forward pieces
-def _conv_fwd_stats(x, spec):
+def _conv_fwd_stats(x, spec, nol=None):
+    """conv forward + BN statistics epilogue; ``nol`` = (scale, shift): ``x`` is the raw input of the
+    previous BN, normalized (+ ReLU) on load"""
     N, C, H, W = x.shape
     w16 = weight_bf16(spec.w)
     K, _, R, S = spec.w.shape
@@ -111,6 +133,10 @@ def _conv_fwd_stats(x, spec):
     rows = lib.mi_conv_stat_rows_g(N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q)
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=x.device)
     y = torch.empty((N, K, P, Q), dtype=BF16, device=x.device, memory_format=CL)
+    if nol is not None:
+        _lib.call("mi_conv2d_fwd_nol", ptr(x), ptr(w16), ptr(y), ptr(slab), ptr(nol[0]), ptr(nol[1]), N, H, W, C, K,
+                  R, S, spec.stride, spec.pad, P, Q, stream_of(x))
+        return y, slab, rows
     _lib.call("mi_conv2d_fwd", ptr(x), ptr(w16), ptr(y), ptr(None), ptr(slab), N, H, W, C, K, R, S, spec.stride,
               spec.pad, P, Q, 0, stream_of(x))
     return y, slab, rows
@@ -147,19 +173,24 @@ def _bn_fwd_dual(c, slab, rows, bn, cd, slabd, rowsd, bnd):
 
 
 # ---------------------------------------------------------------------- backward pieces
-def _wgrad(x, dy, spec):
+def _wgrad(x, dy, spec, nol=None):
     """weight gradient into the flat buffer -- on the engine's weight-gradient stream when it has
-    one (overlapping this block's data-gradient chain, see functional.WgradStream)"""
+    one (overlapping this block's data-gradient chain, see functional.WgradStream); ``nol`` =
+    (scale, shift): ``x`` is the raw input of the previous BN, normalized (+ ReLU) on load"""
     N, C, H, W = x.shape
     K, _, R, S = spec.w.shape
     P, Q = dy.shape[2], dy.shape[3]
     g = _grad_buffer(spec.w)
 
     def launch():
+        if nol is not None:
+            _lib.call("mi_conv2d_wgrad_nol", ptr(x), ptr(dy), ptr(g), ptr(nol[0]), ptr(nol[1]), N, H, W, C, K, R, S,
+                      spec.stride, spec.pad, P, Q, stream_of(dy))
+            return
         _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dy), ptr(g), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
                   stream_of(dy))
     if _side(spec.w) is not None:
-        run_wgrad(spec.w, launch, (x, dy))
+        run_wgrad(spec.w, launch, (x, dy) + (tuple(nol) if nol is not None else ()))
         return None
     launch()
     return _finish_grad(spec.w, g)
@@ -176,15 +207,23 @@ def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0
     return out
 
 
-def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev):
+def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev, mask=None):
     """conv dgrad fused with the relu mask + backward statistics of the BN that produced the conv's
-    input: returns (dz, slab, rows)."""
-    N, C, H, W = y_prev.shape
+    input: returns (dz, slab, rows).  ``mask`` = that BN's (scale, shift): the mask comes from
+    ``c_prev`` (normalize-on-load schedules never write ``y_prev``, which is then None)."""
+    N, C, H, W = c_prev.shape
     lib = _lib.load()
     rows = lib.mi_dgrad_stat_rows(N, H, W, C, dy.shape[2], dy.shape[3], spec.stride, spec.w.shape[0],
                                  spec.w.shape[2] * spec.w.shape[3])
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dy.device)
-    dz = torch.empty_like(y_prev, memory_format=CL)
+    dz = torch.empty_like(c_prev, memory_format=CL)
+    if mask is not None:
+        K, _, R, S = spec.w.shape
+        P, Q = dy.shape[2], dy.shape[3]
+        _lib.call("mi_conv2d_dgrad_ex3", ptr(dy), ptr(weight_bf16_t(spec.w)), ptr(dz), N, H, W, C, K, R, S,
+                  spec.stride, spec.pad, P, Q, EPI_BN_BWD, ptr(None), ptr(c_prev), ptr(mean_prev), 1, ptr(slab), 0,
+                  ptr(mask[0]), ptr(mask[1]), stream_of(dy))
+        return dz, slab, rows
     _dgrad(dy, spec, y_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab)
     return dz, slab, rows
 
@@ -240,8 +279,10 @@ class _ResBlock(torch.autograd.Function):
                 cd, slabd, rowsd = _conv_fwd_stats(x, convs[-1])
                 _, md, isd, sd, hd = _bn_fwd(cd, slabd, rowsd, bns[-1], relu=False, apply=False)
         h = x
+        nol = None               # (scale, shift) when h is a raw BN input normalized on load
+        saved_nol = []
         for i in range(n_main):
-            c, slab, rows = _conv_fwd_stats(h, convs[i])
+            c, slab, rows = _conv_fwd_stats(h, convs[i], nol)
             last = i == n_main - 1
             if last:
                 if has_ds and aux is not None:
@@ -256,11 +297,24 @@ class _ResBlock(torch.autograd.Function):
                     y, m, inv, md, isd = _bn_fwd_dual(c, slab, rows, bns[i], cd, slabd, rowsd, bns[-1])
                 else:
                     y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True, res=x)
+            elif _nol_ok(c, convs[i + 1]):
+                # inner BN, consumer normalizes on load: statistics / running stats / (scale, shift)
+                # only -- y is never materialised
+                _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bns[i], relu=True, apply=False)
+                y = None
+                nol = (sc, sh)
+                NOL_USED[0] += 1
             else:
                 y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True)
+                nol = None
             saved_c.append(c); saved_y.append(y); saved_m.append(m); saved_i.append(inv)
-            h = y
-        tensors = [x] + saved_c + saved_y + saved_m + saved_i
+            saved_nol.append(nol if y is None else None)
+            h = y if y is not None else c
+        # y of a normalize-on-load BN is None: its (scale, shift) ride in the y slot's place
+        ys_t = [y if y is not None else saved_nol[k][0] for k, y in enumerate(saved_y)]
+        nol_t = [saved_nol[k][1] if saved_nol[k] is not None else saved_c[k] for k in range(n_main)]
+        ctx.nol_flags = [s_ is not None for s_ in saved_nol]
+        tensors = [x] + saved_c + ys_t + saved_m + saved_i + nol_t
         if has_ds:
             tensors += [cd, md, isd]
         ctx.save_for_backward(*tensors)
@@ -291,9 +345,12 @@ class _ResBlock(torch.autograd.Function):
         n = ctx.n_main
         t = ctx.saved_tensors
         x = t[0]
-        cs, ys, ms, invs = t[1:1 + n], t[1 + n:1 + 2 * n], t[1 + 2 * n:1 + 3 * n], t[1 + 3 * n:1 + 4 * n]
+        cs, ys, ms, invs = t[1:1 + n], list(t[1 + n:1 + 2 * n]), t[1 + 2 * n:1 + 3 * n], t[1 + 3 * n:1 + 4 * n]
+        shs = t[1 + 4 * n:1 + 5 * n]
+        nols = [(ys[k], shs[k]) if ctx.nol_flags[k] else None for k in range(n)]
+        ys = [None if ctx.nol_flags[k] else ys[k] for k in range(n)]
         if has_ds:
-            cd, md, isd = t[1 + 4 * n:]
+            cd, md, isd = t[1 + 5 * n:]
         dout = _nhwc(dout)
         grads = {}
         hand = _HANDOFF.pop((dout.data_ptr(), dout.device.index), None)
@@ -324,9 +381,10 @@ class _ResBlock(torch.autograd.Function):
             with torch.cuda.stream(aux):
                 acc_flags, dsd = _ResBlock._shortcut_backward(x, dyd, dx, cd, md, isd, convs, bns, grads)
         for i in range(n - 1, 0, -1):
-            inp = ys[i - 1]
-            grads[id(convs[i].w)] = _wgrad(inp, dc, convs[i])
-            dz, slab, rows = _dgrad_bn(dc, convs[i], inp, cs[i - 1], ms[i - 1])
+            nol = nols[i - 1]
+            inp = ys[i - 1] if nol is None else cs[i - 1]
+            grads[id(convs[i].w)] = _wgrad(inp, dc, convs[i], nol)
+            dz, slab, rows = _dgrad_bn(dc, convs[i], ys[i - 1], cs[i - 1], ms[i - 1], mask=nol)
             dc, gw, gb = _bn_bwd_pre(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
             grads[id(bns[i - 1].w)], grads[id(bns[i - 1].b)] = gw, gb
         grads[id(convs[0].w)] = _wgrad(x, dc, convs[0])

@@ -575,3 +575,69 @@ def test_tn_splitk_fused_reduce_bit_identical(shape):
     wr = w0.clone().requires_grad_(True)
     F.conv2d(xr, wr, None, s, p).backward(gy.float())
     assert rel_err(out[1][0], wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("shape", [
+    # N, C, H, K, R, s, p: resnet18 @ 32 inner convs, resnet50 @ 64 / 112 / 224 consumers of inner BNs
+    (8, 64, 8, 64, 3, 1, 1), (8, 128, 4, 128, 3, 1, 1), (8, 256, 2, 256, 3, 1, 1),
+    (8, 64, 16, 64, 3, 1, 1), (8, 64, 16, 256, 1, 1, 0), (8, 128, 16, 128, 3, 2, 1),
+    (32, 64, 56, 64, 3, 1, 1), (32, 64, 56, 256, 1, 1, 0), (32, 128, 56, 128, 3, 2, 1),
+    (32, 128, 28, 128, 3, 1, 1), (32, 128, 28, 512, 1, 1, 0),
+])
+def test_normalize_on_load_kernels(shape):
+    """Normalize-on-load kernels (inner BatchNorms, ops/resblock.py NOL) against the materialised
+    path on the same raw input c: forward conv of relu(c*scale + shift), weight gradient from c,
+    and the data gradient's ReLU mask (epi 4) taken from c instead of y."""
+    import ctypes
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops import kernels  # noqa: F401
+    from mi355x_dp.ops._lib import ptr, stream_of
+    N, C, H, K, R, s, p = shape
+    P = (H + 2 * p - R) // s + 1
+    lib = _lib.load()
+    if not lib.mi_conv_nol_ok(N, H, H, C, K, R, R, s, p, P, P):
+        pytest.skip("shape routed to a kernel without normalize-on-load")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    c = torch.randn(N, C, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    scale = torch.rand(C, device="cuda", generator=g) + 0.5
+    shift = torch.randn(C, device="cuda", generator=g) * 0.5
+    scale[::7] *= -1  # negative gammas too
+    y = torch.relu(c.float() * scale.view(1, C, 1, 1) + shift.view(1, C, 1, 1)).to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, R, device="cuda", generator=g) * (2.0 / (C * R * R)) ** 0.5).to(BF)
+    w16 = w.permute(0, 2, 3, 1).contiguous()  # [K][R][S][C]
+    st = stream_of(c)
+    out_ref = torch.empty(N, K, P, P, dtype=BF, device="cuda", memory_format=CL)
+    out_nol = torch.empty_like(out_ref)
+    _lib.call("mi_conv2d_fwd", ptr(y), ptr(w16), ptr(out_ref), ptr(None), ptr(None), N, H, H, C, K, R, R, s, p, P, P,
+              0, st)
+    rows = lib.mi_conv_stat_rows_g(N, H, H, C, K, R, R, s, p, P, P)
+    slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), device="cuda")
+    _lib.call("mi_conv2d_fwd_nol", ptr(c), ptr(w16), ptr(out_nol), ptr(slab), ptr(scale), ptr(shift), N, H, H, C,
+              K, R, R, s, p, P, P, st)
+    torch.cuda.synchronize()
+    assert rel_err(out_nol, out_ref) < 1e-2, ("fwd", rel_err(out_nol, out_ref))
+    # weight gradient from c vs from y
+    dy = torch.randn(N, K, P, P, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    dw_ref = torch.zeros(K, R, R, C, device="cuda")
+    dw_nol = torch.zeros_like(dw_ref)
+    _lib.call("mi_conv2d_wgrad", ptr(y), ptr(dy), ptr(dw_ref), N, H, H, C, K, R, R, s, p, P, P, st)
+    _lib.call("mi_conv2d_wgrad_nol", ptr(c), ptr(dy), ptr(dw_nol), ptr(scale), ptr(shift), N, H, H, C, K, R, R, s, p,
+              P, P, st)
+    torch.cuda.synchronize()
+    assert rel_err(dw_nol, dw_ref) < 1e-2, ("wgrad", rel_err(dw_nol, dw_ref))
+    # data gradient with the BN-backward epilogue: mask from y (ex2) vs from c (ex3)
+    wt = w.permute(1, 2, 3, 0).contiguous()  # [C][R][S][K]
+    mean = c.float().mean((0, 2, 3))
+    rows = lib.mi_dgrad_stat_rows(N, H, H, C, P, P, s, K, R * R)
+    sl1 = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), device="cuda")
+    sl2 = torch.empty_like(sl1)
+    dz1 = torch.empty_like(c)
+    dz2 = torch.empty_like(c)
+    _lib.call("mi_conv2d_dgrad_ex2", ptr(dy), ptr(wt), ptr(dz1), N, H, H, C, K, R, R, s, p, P, P, 4, ptr(y), ptr(c),
+              ptr(mean), 1, ptr(sl1), 0, st)
+    _lib.call("mi_conv2d_dgrad_ex3", ptr(dy), ptr(wt), ptr(dz2), N, H, H, C, K, R, R, s, p, P, P, 4, ptr(None),
+              ptr(c), ptr(mean), 1, ptr(sl2), 0, ptr(scale), ptr(shift), st)
+    torch.cuda.synchronize()
+    mism = float(((dz1.float() != dz2.float()).float().mean()))
+    assert mism < 1e-3, ("dgrad mask", mism)  # only where c * scale + shift rounds to ~0
+    assert rel_err(sl2[:rows], sl1[:rows]) < 1e-2, ("dgrad stats", rel_err(sl2[:rows], sl1[:rows]))

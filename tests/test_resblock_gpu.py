@@ -76,6 +76,31 @@ def test_fused_blocks_match_per_op(name, size):
     print(sorted(worst)[-3:])
 
 
+@pytest.mark.parametrize("name,size", [("resnet18", 32), ("resnet50", 64), ("resnet50", 112)])
+def test_normalize_on_load_matches_materialised(name, size, monkeypatch):
+    """Inner BatchNorms normalized on load by their consumer convs (forward, weight gradient, ReLU
+    mask from c in the data gradient; ops/resblock.py NOL) against the same fused blocks with the
+    BN outputs materialised: losses / running statistics equal to rounding, every gradient as
+    close to fp32 PyTorch as the materialised path, and the NOL path really taken."""
+    import mi355x_dp.ops.resblock as RB
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(8, 3, size, size, device="cuda", generator=g)
+    y = torch.randint(0, 10, (8,), device="cuda", generator=g)
+    monkeypatch.setattr(RB, "NOL", False)
+    l0, g0, b0 = _run(name, True, x, y)
+    monkeypatch.setattr(RB, "NOL", True)
+    used = RB.NOL_USED[0]
+    l1, g1, b1 = _run(name, True, x, y)
+    assert RB.NOL_USED[0] > used
+    lr, gr = _fp32_ref(name, x, y)
+    assert l1 == pytest.approx(l0, rel=2e-3)
+    for n in b0:
+        assert rel_err(b1[n], b0[n]) < 2e-3, n
+    for n in g0:
+        e_mat, e_nol = rel_err(g0[n], gr[n]), rel_err(g1[n], gr[n])
+        assert e_nol <= 1.25 * e_mat + 0.01, (n, e_nol, e_mat)
+
+
 def test_fused_block_used_in_training():
     import mi355x_dp.models.resnet as R
     from mi355x_dp.models import get_model
