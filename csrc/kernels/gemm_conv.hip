@@ -1957,6 +1957,11 @@ MI_API int mi_conv_nol_ok(int Nb, int H, int W, int C, int K, int R, int S, int 
   if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return 0;
   if (use_gemm256_conv(Nb * P * Q, K, C, R * S * C)) return 0;                    // forward
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K)) return 0;    // data gradient
+  // small grids keep the materialised path: there the 128-tile kernels split K (nt_split_blocks),
+  // which the normalize-on-load variants do not -- and the bytes saved are negligible
+  const int tf = cdiv(Nb * P * Q, nt_choice(Nb * P * Q, K) == 2 ? 64 : 128) * cdiv(K, nt_choice(Nb * P * Q, K) == 0 ? 128 : 64);
+  const int td = cdiv(Nb * H * W, nt_choice(Nb * H * W, C) == 2 ? 64 : 128) * cdiv(C, nt_choice(Nb * H * W, C) == 0 ? 128 : 64);
+  if (tf < nt_split_blocks() || td < nt_split_blocks()) return 0;
   return 1;
 }
 

@@ -6,6 +6,11 @@ import mi355x_dp.ops.resblock as RB
 from mi355x_dp.models import get_model
 
 name, size, bs = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+if len(sys.argv) > 4:  # 0: the small-layer fused BN (statistics + apply in one launch) off
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops import kernels  # noqa: F401
+    _lib.load().mi_bn_set_small_elems(int(sys.argv[4]))
+    print("bn small elems", sys.argv[4])
 g = torch.Generator(device="cuda").manual_seed(7)
 x = torch.randn(bs, 3, size, size, device="cuda", generator=g)
 outs = {}
