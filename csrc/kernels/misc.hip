@@ -12,6 +12,7 @@
 //   stem im2col (C=3 input)           -> im2col_nhwc
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace {
 constexpr int NT = 256;
@@ -177,10 +178,12 @@ __global__ __launch_bounds__(NT) void ce_sum_kernel(const float* __restrict__ ro
   if (threadIdx.x == 0) loss[0] = red[0] * inv_n;
 }
 
-// dlogits[n][c] = g * inv_n * (softmax - onehot), bf16 [N][ldo] (zero in padding columns)
+// dlogits[n][c] = g * inv_n * (softmax - onehot), [N][ldo] in the logits' own dtype (fp32 logits get an fp32
+// gradient, so autograd needs no cast launch; zero in padding columns)
+template <typename T>
 __global__ __launch_bounds__(NT) void ce_bwd_kernel(const float* __restrict__ logits, const int64_t* __restrict__ y,
                                                     const float* __restrict__ lse, const float* __restrict__ gout,
-                                                    bf16_t* __restrict__ dl, int ncls, int ld, int ldo, float inv_n) {
+                                                    T* __restrict__ dl, int ncls, int ld, int ldo, float inv_n) {
   const int row = blockIdx.x;
   const float g = gout[0] * inv_n;
   const float ls = lse[row];
@@ -189,7 +192,10 @@ __global__ __launch_bounds__(NT) void ce_bwd_kernel(const float* __restrict__ lo
   for (int c = threadIdx.x; c < ldo; c += NT) {
     float v = 0.f;
     if (c < ncls) v = g * (__expf(l[c] - ls) - (c == yy ? 1.f : 0.f));
-    dl[(size_t)row * ldo + c] = f2bf(v);
+    if constexpr (std::is_same<T, float>::value)
+      dl[(size_t)row * ldo + c] = v;
+    else
+      dl[(size_t)row * ldo + c] = f2bf(v);
   }
 }
 
@@ -368,10 +374,15 @@ MI_API int mi_ce_fwd(const float* logits, const int64_t* y, float* lse, float* l
   return (int)hipGetLastError();
 }
 
+// out_f32: dl is fp32 (else bf16)
 MI_API int mi_ce_bwd(const float* logits, const int64_t* y, const float* lse, const float* gout, void* dl, int N,
-                     int ncls, int ld, int ldo, hipStream_t st) {
-  hipLaunchKernelGGL(ce_bwd_kernel, dim3(N), dim3(NT), 0, st, logits, y, lse, gout, (bf16_t*)dl, ncls, ld, ldo,
-                     1.f / N);
+                     int ncls, int ld, int ldo, int out_f32, hipStream_t st) {
+  if (out_f32)
+    hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(N), dim3(NT), 0, st, logits, y, lse, gout, (float*)dl, ncls, ld,
+                       ldo, 1.f / N);
+  else
+    hipLaunchKernelGGL(ce_bwd_kernel<bf16_t>, dim3(N), dim3(NT), 0, st, logits, y, lse, gout, (bf16_t*)dl, ncls, ld,
+                       ldo, 1.f / N);
   return (int)hipGetLastError();
 }
 

@@ -404,6 +404,40 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float4* __
   dw[pos] = d;
 }
 
+// The same fixed-order row sum for the parameter's own gradient: g[k][c][r][s] (any strides, the
+// flat buffer's kernel layout) += sum over rows of ws[.][k][tap][c] for the real channels c < Cw --
+// the padded [K][7][7][8] gradient is never materialised, cropped or permuted by extra launches.
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_to_kernel(const float* __restrict__ ws, float* __restrict__ g,
+                                                                   int rows, int Cw, int64_t sK, int64_t sC,
+                                                                   int64_t sR, int64_t sS) {
+  __shared__ float red[SWR_G][SWR_POS];
+  const int pl = threadIdx.x % SWR_POS, grp = threadIdx.x / SWR_POS;
+  const int pos = blockIdx.x * SWR_POS + pl;
+  const int ne = KOUT * NTAP * Cw;
+  const int c = pos % Cw, t = pos / Cw, tap = t % NTAP, k = t / NTAP;
+  const int o = (k * NTAP + tap) * 8 + c;
+  float s = 0.f;
+  if (pos < ne)
+    for (int b = grp; b < rows; b += SWR_G) s += ws[(size_t)b * STEM_WELEMS + o];
+  red[grp][pl] = s;
+  __syncthreads();
+  if (grp != 0 || pos >= ne) return;
+  for (int gg = 1; gg < SWR_G; ++gg) s += red[gg][pl];
+  float* d = g + k * sK + c * sC + (tap / SS) * sR + (tap % SS) * sS;
+  *d += s;
+}
+
+// Conv weight [K][Cw][R][S] bf16 (any strides) -> the stem kernel's [K][7][7][8] operand, channels
+// >= Cw zero: one launch per step instead of a zero fill plus a strided copy.
+__global__ __launch_bounds__(256) void stem_wpack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                         int total, int Cw, int R, int S, int64_t sK, int64_t sC,
+                                                         int64_t sR, int64_t sS) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int c = e & 7, t = e >> 3, tap = t % (R * S), k = t / (R * S);
+  dst[e] = c < Cw ? src[k * sK + c * sC + (tap / S) * sR + (tap % S) * sS] : (bf16_t)0;
+}
+
 constexpr size_t stem_wgrad_lds_bytes() { return (size_t)(NRING * ROWPX + 2 * 2 * DYPX * 8) * 16; }
 
 constexpr size_t stem_lds_bytes() {
@@ -458,9 +492,16 @@ MI_API int mi_stem_conv_fwd(const void* x, const void* w, void* y, float* stats,
   return (int)hipGetLastError();
 }
 
-// dw [64][7][7][8] fp32 += stem weight gradient; x [Nb][H][W][8], dy [Nb][P][Q][64] bf16.
-MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H, int W, int P, int Q, int pad,
-                         hipStream_t st) {
+// Gradient destination of stem_wgrad: dw [64][7][7][8] (to == nullptr) or the parameter's own
+// gradient g [64][Cw][7][7] with element strides (deterministic partials path only).
+struct StemWTo {
+  float* g;
+  int Cw;
+  int64_t sK, sC, sR, sS;
+};
+
+static int stem_wgrad_impl(const void* x, const void* dy, float* dw, const StemWTo* to, int Nb, int H, int W, int P,
+                           int Q, int pad, hipStream_t st) {
   if (!mi_stem_conv_ok(8, KOUT, SR, SS, SSTR, pad, Q) || Q > DYPX) return (int)hipErrorInvalidValue;
   const int64_t xb = (int64_t)Nb * H * W * 8 * 2, db = (int64_t)Nb * P * Q * KOUT * 2;
   if (xb > 0x7FFFFFF0LL || db > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
@@ -487,9 +528,43 @@ MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H
                         (int)stem_wgrad_lds_bytes());
     attr = true;
   }
+  if (to && !a.ws) return (int)hipErrorNotSupported;  // atomic mode: the caller pads and permutes
   hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(STEM_T), stem_wgrad_lds_bytes(), st, a);
-  if (a.ws)
+  if (to)
+    hipLaunchKernelGGL(stem_wgrad_reduce_to_kernel, dim3(cdiv(KOUT * NTAP * to->Cw, SWR_POS)), dim3(256), 0, st,
+                       (const float*)a.ws, to->g, blocks, to->Cw, to->sK, to->sC, to->sR, to->sS);
+  else if (a.ws)
     hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(STEM_WELEMS / 4, SWR_POS)), dim3(256), 0, st,
                        (const float4*)a.ws, (float4*)dw, blocks);
+  return (int)hipGetLastError();
+}
+
+// dw [64][7][7][8] fp32 += stem weight gradient; x [Nb][H][W][8], dy [Nb][P][Q][64] bf16.
+MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H, int W, int P, int Q, int pad,
+                         hipStream_t st) {
+  return stem_wgrad_impl(x, dy, dw, nullptr, Nb, H, W, P, Q, pad, st);
+}
+
+// g [64][Cw][7][7] fp32 (element strides sK, sC, sR, sS) += stem weight gradient of the real
+// channels.  hipErrorNotSupported when the shape is not the stem kernel's or the atomic fallback is
+// selected (the caller then uses mi_conv2d_wgrad into a padded buffer).
+MI_API int mi_stem_wgrad_to(const void* x, const void* dy, float* g, int Cw, int64_t sK, int64_t sC, int64_t sR,
+                            int64_t sS, int Nb, int H, int W, int P, int Q, int pad, hipStream_t st) {
+  if (Cw < 1 || Cw > 8) return (int)hipErrorInvalidValue;
+  const char* e = std::getenv("MI355X_DP_STEM_KERNEL");  // =0: the generic path (gemm_conv.hip)
+  if ((e && e[0] == '0') || !mi_stem_conv_ok(8, KOUT, SR, SS, SSTR, pad, Q)) return (int)hipErrorNotSupported;
+  const StemWTo to{g, Cw, sK, sC, sR, sS};
+  return stem_wgrad_impl(x, dy, nullptr, &to, Nb, H, W, P, Q, pad, st);
+}
+
+// src: conv weight [K][Cw][R][S] bf16 with element strides; dst: [K][R][S][8] bf16 (any small-channel
+// conv of the fused stem: the persistent 7x7 kernel or the generic 8-channel implicit GEMM).
+MI_API int mi_stem_wpack(const void* src, void* dst, int K, int Cw, int R, int S, int64_t sK, int64_t sC, int64_t sR,
+                         int64_t sS, hipStream_t st) {
+  if (K < 1 || R < 1 || S < 1 || Cw < 1 || Cw > 8 || (int64_t)K * R * S * 8 > 0x7FFFFFFF)
+    return (int)hipErrorInvalidValue;
+  const int total = K * R * S * 8;
+  hipLaunchKernelGGL(stem_wpack_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, (const bf16_t*)src, (bf16_t*)dst,
+                     total, Cw, R, S, sK, sC, sR, sS);
   return (int)hipGetLastError();
 }

@@ -338,6 +338,47 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
   return (int)hipGetLastError();
 }
 
+// fp32 X [M][N] -> bf16 Y (the GEMM operand) and, when out != nullptr, out[n] += sum_m X[m][n] from
+// the fp32 values (a classifier head's bias gradient from fp32 logit gradients): one pass, same
+// blocking as colsum_kernel.
+__global__ __launch_bounds__(256) void cast_colsum_f32_kernel(const float* __restrict__ X, bf16_t* __restrict__ Y,
+                                                              float* __restrict__ out, int M, int N,
+                                                              int rows_per_block) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = (blockIdx.x * 64 + lane) * 8;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (n < N) {
+    for (int m = r0 + wv; m < r1; m += 4) {
+      const float4 a = *(const float4*)(X + (size_t)m * N + n), b = *(const float4*)(X + (size_t)m * N + n + 4);
+      const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      *(uint4*)(Y + (size_t)m * N + n) = pack8(f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += f[q];
+    }
+  }
+  if (!out) return;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[wv][lane * 8 + q] = acc[q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int col = blockIdx.x * 512 + c;
+    if (col < N) atomicAdd(out + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  }
+}
+
+MI_API int mi_cast_colsum_f32(const float* X, void* Y, float* out, int M, int N, hipStream_t st) {
+  if (N % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
+  const int bx = cdiv(N, 512);
+  int by = max(1, min(cdiv(M, 64), 2048 / bx));
+  const int rpb = cdiv(M, by);
+  by = cdiv(M, rpb);
+  hipLaunchKernelGGL(cast_colsum_f32_kernel, dim3(bx, by), dim3(256), 0, st, X, (bf16_t*)Y, out, M, N, rpb);
+  return (int)hipGetLastError();
+}
+
 MI_API int mi_colsum_bf16(const void* X, float* out, int M, int N, int ld, hipStream_t st) {
   if (N % 8 != 0 || ld % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
   const int bx = cdiv(N, 512);

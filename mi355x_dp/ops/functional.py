@@ -528,10 +528,19 @@ class _Linear(torch.autograd.Function):
         N = weight.shape[0]
         Np = w16.shape[0]
         dy2 = dy.reshape(M, N)
+        gb32 = None
         if Np != N:
             dyp = torch.zeros((M, Np), dtype=BF16, device=dy.device)
             dyp[:, :N].copy_(dy2)
             dy2 = dyp
+        elif dy2.dtype == torch.float32 and dy2.is_contiguous() and N % 8 == 0:
+            # fp32 logits gradient: one native pass casts it to the bf16 GEMM operand and sums the
+            # bias gradient from the fp32 values
+            d16 = torch.empty((M, N), dtype=BF16, device=dy.device)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                gb32 = _grad_buffer(ctx.bias_param)
+            _lib.call("mi_cast_colsum_f32", ptr(dy2), ptr(d16), ptr(gb32), M, N, stream_of(dy))
+            dy2 = d16
         else:
             dy2 = dy2.to(BF16).contiguous()
         st = stream_of(dy)
@@ -553,10 +562,10 @@ class _Linear(torch.autograd.Function):
             dw = _finish_grad(weight, g)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             bias = ctx.bias_param
-            gb = _grad_buffer(bias)
-            if dy2.dtype == BF16 and Np == N and dy.dtype == BF16:
+            gb = gb32 if gb32 is not None else _grad_buffer(bias)  # gb32: summed by the cast pass
+            if gb32 is None and dy2.dtype == BF16 and Np == N and dy.dtype == BF16:
                 _lib.call("mi_colsum_bf16", ptr(dy2), ptr(gb), M, N, N, st)
-            else:
+            elif gb32 is None:
                 gb.add_(dy.reshape(M, N).float().sum(0))
             db = _finish_grad(bias, gb)
         return dx, dw, db, None
@@ -589,8 +598,10 @@ class _CrossEntropy(torch.autograd.Function):
         lg, tgt, lse = ctx.saved_tensors
         N, ncls = lg.shape
         g = gout.float().contiguous().reshape(1)
-        dl = torch.empty((N, ncls), dtype=BF16, device=lg.device)
-        _lib.call("mi_ce_bwd", ptr(lg), ptr(tgt), ptr(lse), ptr(g), ptr(dl), N, ncls, ncls, ncls, stream_of(lg))
+        f32 = ctx.in_dtype == torch.float32  # the gradient in the logits' dtype: no autograd cast launch
+        dl = torch.empty((N, ncls), dtype=torch.float32 if f32 else BF16, device=lg.device)
+        _lib.call("mi_ce_bwd", ptr(lg), ptr(tgt), ptr(lse), ptr(g), ptr(dl), N, ncls, ncls, ncls, int(f32),
+                  stream_of(lg))
         return dl.to(ctx.in_dtype), None
 
 

@@ -23,6 +23,9 @@ signature("mi_conv2d_fwd_nol", P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I
 signature("mi_conv2d_wgrad_nol", P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_dgrad_ex3", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P, P, P)
 signature("mi_conv_wtrans", P, P, I, I, I, P)
+# stem_conv.hip (ops/stem.py): weight pack and the gradient straight into the parameter's buffer
+signature("mi_stem_wpack", P, P, I, I, I, I, L, L, L, L, P)
+signature("mi_stem_wgrad_to", P, P, P, I, L, L, L, L, I, I, I, I, I, I, P)
 signature("mi_conv_wtrans_multi", P, P, P, I, I, P)
 signature("mi_gemm_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, P)
 signature("mi_gemm_tn", P, P, P, I, I, I, I, I, I, P)
@@ -52,7 +55,7 @@ signature("mi_maxpool_bwd", P, P, P, I, I, I, I, I, I, I, I, I, P)
 signature("mi_gap_fwd", P, P, I, I, I, P)
 signature("mi_gap_bwd", P, P, I, I, I, P)
 signature("mi_ce_fwd", P, P, P, P, I, I, I, P)
-signature("mi_ce_bwd", P, P, P, P, P, I, I, I, I, P)
+signature("mi_ce_bwd", P, P, P, P, P, I, I, I, I, I, P)
 signature("mi_sgd_flat", P, P, P, P, L, F, F, F, F, I, I, F, P)
 signature("mi_cast_bf16", P, P, L, P)
 signature("mi_augment", P, P, I, I, I, I, I, I, I, U32, P, P, P)
@@ -71,6 +74,7 @@ signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)
 signature("mi_layernorm_fwd", P, P, P, P, P, P, I, I, F, P)
 signature("mi_layernorm_bwd", P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_colsum_bf16", P, P, I, I, I, P)
+signature("mi_cast_colsum_f32", P, P, P, I, I, P)
 signature("mi_ln_ws_reserve", I, P)
 
 # attention.hip

@@ -106,8 +106,11 @@ class _BNSpec:
 # shift) as it stages its operand (forward and weight gradient), and the data gradient that needs
 # that BN's ReLU mask takes it from c -- the BN output y is never written nor read (VERDICT r3
 # item 2; profiles/bn_nol_r4.md).  Per consumer shape, where the 128-tile kernels serve all three
-# (mi_conv_nol_ok); elsewhere y is materialised as before.  MI355X_DP_NOL=0 disables.
-NOL = os.environ.get("MI355X_DP_NOL", "1") != "0"
+# (mi_conv_nol_ok); elsewhere y is materialised as before.  OFF by default (MI355X_DP_NOL=1 enables):
+# on MI355X the in-kernel transform costs more than the bn_apply pass it removes -- every NoL kernel
+# is slower in isolation (fwd +10-30 %, mask-from-c dgrad +2-10 %, wgrad +1-65 %,
+# tools/bench_nol.py) and the RN50 bs256 step loses ~1 % (same-box A/B, profiles/bn_nol_r4.md).
+NOL = os.environ.get("MI355X_DP_NOL", "0") == "1"
 NOL_USED = [0]  # diagnostics: inner BNs whose output was normalized on load instead of written
 
 

@@ -44,8 +44,9 @@ class _Stem(torch.autograd.Function):
         st = stream_of(x)
         lib = _lib.load()
         # conv: small-channel (8-wide tap) MFMA mode, BN statistics from the epilogue
-        wp = torch.zeros((K, R, S, 8), dtype=BF16, device=dev)
-        wp[..., :Cw].copy_(weight_bf16(wconv).permute(0, 2, 3, 1))
+        w16 = weight_bf16(wconv)
+        wp = torch.empty((K, R, S, 8), dtype=BF16, device=dev)  # zero-padded to 8 channels, one launch
+        _lib.call("mi_stem_wpack", ptr(w16), ptr(wp), K, Cw, R, S, *w16.stride(), st)
         rows = lib.mi_conv_stat_rows_g(N, H, W, 8, K, R, S, stride, pad, P, Q)
         slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, K), dtype=F32, device=dev)
         c = torch.empty((N, K, P, Q), dtype=BF16, device=dev, memory_format=CL)
@@ -86,9 +87,13 @@ class _Stem(torch.autograd.Function):
                   ptr(shift), ptr(gamma), ptr(mean), ptr(invstd), ptr(gw), ptr(gb), ptr(coef), ptr(part), st)
         dgamma, dbeta = _finish_grad(gamma, gw), _finish_grad(beta, gb)
         g = _grad_buffer(wconv)
-        gp = torch.zeros((K, R, S, 8), dtype=F32, device=dev)
-        _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dc), ptr(gp), N, H, W, 8, K, R, S, stride, pad, P, Q, st)
-        g.add_(gp[..., :Cw].permute(0, 3, 1, 2))
+        # the persistent stem kernel's fixed-order partial sums land in g's own layout; otherwise
+        # (other geometry, atomic mode) a padded buffer is cropped and permuted into g
+        rc = lib.mi_stem_wgrad_to(ptr(x), ptr(dc), ptr(g), Cw, *g.stride(), N, H, W, P, Q, pad, st)
+        if rc != 0:
+            gp = torch.zeros((K, R, S, 8), dtype=F32, device=dev)
+            _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dc), ptr(gp), N, H, W, 8, K, R, S, stride, pad, P, Q, st)
+            g.add_(gp[..., :Cw].permute(0, 3, 1, 2))
         dw = _finish_grad(wconv, g)
         return None, None, dw, dgamma, dbeta, None, None, None, None, None
 

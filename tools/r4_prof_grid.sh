@@ -11,5 +11,6 @@ db=$(find gpurun_out/$name -name '*results.db' | head -1)
 python tools/prof_summary.py $db --marker sgd_flat_kernel --skip 4 > gpurun_out/$name.summary.md
 python tools/prof_by_grid.py $db --marker sgd_flat_kernel --skip 4 --top 80 > gpurun_out/$name.grid.md
 python tools/prof_neighbors.py $db --marker sgd_flat_kernel --step 5 > gpurun_out/$name.neighbors.txt
+python tools/prof_sequence.py $db --marker sgd_flat_kernel --step 5 > gpurun_out/$name.seq.txt
 grep "^\[gemm\]" gpurun_out/$name.trace.err | sort -u > gpurun_out/$name.gemm_shapes.txt
 rm -rf gpurun_out/$name
