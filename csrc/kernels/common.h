@@ -89,6 +89,17 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// bit j set <=> bf16 element j of the octet is nonzero: the ReLU mask of a stored activation
+// (relu outputs are >= 0, so nonzero == positive) as one byte per 8 channels
+__device__ __forceinline__ uint32_t nz_bits8(const uint4& v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    b |= ((w[k] & 0x7fffu) ? 1u : 0u) << (2 * k) | ((w[k] & 0x7fff0000u) ? 1u : 0u) << (2 * k + 1);
+  return b;
+}
+
 // streaming 16-byte load (nontemporal: read once, do not keep in the caches)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_nt16(const void* base, int64_t v) {

@@ -90,6 +90,7 @@ struct G256Args {
   float* ws;
   int* counters;
   int aux_even;         // epi 3 / 5: accumulated-into gradient defined only at even (h, w) (gemm_conv.hip)
+  const uint8_t* mbits; // epi 4 / 5: ReLU mask bytes (8 channels each) instead of aux (gemm_conv.hip NTArgs)
 };
 
 // Wave priority (A/B knob, MI_G256_PRIO): 0 none; 1 static s_setprio 1 for the second-dispatched
@@ -457,7 +458,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
           if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
           if (a.bn_relu) yq[sl][u] = xq[sl][u];
 #else
-          if (a.bn_relu) yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+          if (a.bn_relu) {
+            if (a.mbits)
+              yq[sl][u].x = a.mbits[offs[sl][u] >> 3];  // mask byte (offs is a multiple of 8)
+            else
+              yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+          }
           if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
 #endif
         } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
@@ -484,7 +490,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] += c0[q];
           }
-          if (a.bn_relu) {
+          if (a.bn_relu && a.mbits) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = ((yq[sl][u].x >> q) & 1u) ? f[q] : 0.f;
+          } else if (a.bn_relu) {
             float yv[8];
             unpack8(yq[sl][u], yv);
 #pragma unroll
@@ -926,15 +935,31 @@ MI_API int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, floa
                           N, 0, st);
 }
 
+MI_API int mi_gemm256_conv3(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                            const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
+                            int Q, int R, int S, int stride, int pad, int N, int aux_even, const void* mbits,
+                            hipStream_t st);
+
 // as mi_gemm256_conv; aux_even: see G256Args
 MI_API int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
                             const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
                             int Q, int R, int S, int stride, int pad, int N, int aux_even, hipStream_t st) {
+  return mi_gemm256_conv3(mode, A, B, C, stats, epi, aux, aux2, mean, bn_relu, Nb, H, W, Cs, P, Q, R, S, stride, pad,
+                          N, aux_even, nullptr, st);
+}
+
+// as mi_gemm256_conv2; mbits: the epi 4 / 5 ReLU mask as bytes (see G256Args)
+MI_API int mi_gemm256_conv3(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                            const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
+                            int Q, int R, int S, int stride, int pad, int N, int aux_even, const void* mbits,
+                            hipStream_t st) {
   if ((mode != 1 && mode != 2) || Cs % 64 != 0 || N % 8 != 0 || (mode == 2 && stride != 1) ||
-      !(epi == 0 || epi == 3 || epi == 4 || epi == 5) || (epi == 3 && !aux) || (epi >= 4 && bn_relu && !aux) ||
+      !(epi == 0 || epi == 3 || epi == 4 || epi == 5) || (epi == 3 && !aux) ||
+      (epi >= 4 && bn_relu && !aux && !mbits) || (mbits && (epi < 4 || !bn_relu)) ||
       (epi >= 4 && stats && (!aux2 || !mean)))
     return (int)hipErrorInvalidValue;
   G256Args a{};
+  a.mbits = (const uint8_t*)mbits;
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = nullptr;
   a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu; a.epi = epi;
   a.stats = stats;

@@ -123,6 +123,10 @@ struct NTArgs {
   const float* nol_shift;
   const float* mask_scale;
   const float* mask_shift;
+  // epi 4 / 5 with bn_relu: the ReLU mask as one byte per 8 channels of C's layout (bit j = channel
+  // 8i + j positive; norm_act.hip mi_bn_apply_bits) instead of the bf16 BN output aux -- 1/16 of
+  // the bytes
+  const uint8_t* mbits;
   ConvGeom g;
 };
 
@@ -737,7 +741,12 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
         if (a.bn_relu) yq[sl][u] = xq[sl][u];
 #else
-        if (!MASKC && a.bn_relu) yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+        if (!MASKC && a.bn_relu) {
+          if (a.mbits)
+            yq[sl][u].x = a.mbits[offs[sl][u] >> 3];  // mask byte (offs is a multiple of 8)
+          else
+            yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+        }
         if (a.stats || mask_c) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
 #endif
       } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
@@ -775,6 +784,9 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
             const bool keep = ((mgt >> q) & 1u) ? xv[q] > t : xv[q] < t;
             f[q] = keep ? f[q] : 0.f;
           }
+        } else if (a.bn_relu && a.mbits) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = ((yq[sl][u].x >> q) & 1u) ? f[q] : 0.f;
         } else if (a.bn_relu) {
           float yv[8];
           unpack8(yq[sl][u], yv);
@@ -1884,24 +1896,45 @@ MI_API int mi_conv2d_dgrad_ex2(const void* dy, const void* wt, void* dx, int Nb,
                              flags, nullptr, nullptr, st);
 }
 
-// mi_conv2d_dgrad_ex2 with, for epi 4, the ReLU mask of the producing BN taken from its input c (aux2)
-// as fma(c, mask_scale, mask_shift) > 0 -- aux (the BN output) unused: normalize-on-load schedules
-// never write it.  Only where mi_conv_nol_ok holds (the 128-tile kernels).
+MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                               const float* mean, int bn_relu, float* stats, int flags, const float* mask_scale,
+                               const float* mask_shift, const void* mbits, hipStream_t st);
+
 MI_API int mi_conv2d_dgrad_ex3(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                                int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
                                const float* mean, int bn_relu, float* stats, int flags, const float* mask_scale,
                                const float* mask_shift, hipStream_t st) {
+  return mi_conv2d_dgrad_ex4(dy, wt, dx, Nb, H, W, C, K, R, S, stride, pad, P, Q, epi, aux, aux2, mean, bn_relu, stats,
+                             flags, mask_scale, mask_shift, nullptr, st);
+}
+
+extern "C" int mi_gemm256_conv3(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
+                                const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs,
+                                int P, int Q, int R, int S, int stride, int pad, int N, int aux_even,
+                                const void* mbits, hipStream_t st);
+
+// mi_conv2d_dgrad_ex2 with, for epi 4, the ReLU mask of the producing BN taken from its input c (aux2)
+// as fma(c, mask_scale, mask_shift) > 0 -- aux (the BN output) unused: normalize-on-load schedules
+// never write it.  Only where mi_conv_nol_ok holds (the 128-tile kernels).
+// mbits (epi 4 / 5 with bn_relu): the ReLU mask as bytes of 8 channel bits ([Nb*H*W][C/8], from
+// mi_bn_apply_bits) instead of reading the BN output aux (which may then be null).
+MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                               int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
+                               const float* mean, int bn_relu, float* stats, int flags, const float* mask_scale,
+                               const float* mask_shift, const void* mbits, hipStream_t st) {
   const bool mask_c = mask_scale != nullptr;
   if (mask_c && (epi != 4 || !mask_shift || !aux2 || !bn_relu)) return (int)hipErrorInvalidValue;
+  if (mbits && (epi < 4 || !bn_relu || mask_c)) return (int)hipErrorInvalidValue;
   if (K % 64 != 0 || C % 8 != 0 || stride > 2 || !(epi == 0 || epi == 3 || epi == 4 || epi == 5) ||
-      (epi && !aux && bn_relu && !mask_c) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)) ||
+      (epi && !aux && bn_relu && !mask_c && !mbits) || (epi == 3 && !aux) || (epi >= 4 && stats && (!aux2 || !mean)) ||
       ((flags & 1) && (stride != 2 || epi != 0)) || ((flags & 2) && epi != 3 && epi != 5))
     return (int)hipErrorInvalidValue;
   const int aux_even = (flags >> 1) & 1;
   if (mask_c && stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K)) return (int)hipErrorNotSupported;
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
-    return mi_gemm256_conv2(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
-                            bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, st);
+    return mi_gemm256_conv3(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
+                            bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, mbits, st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
@@ -1910,6 +1943,7 @@ MI_API int mi_conv2d_dgrad_ex3(const void* dy, const void* wt, void* dx, int Nb,
   a.stats = (epi >= 4) ? stats : nullptr;
   a.aux_even = aux_even;
   a.mask_scale = mask_scale; a.mask_shift = mask_shift;
+  a.mbits = (const uint8_t*)mbits;
   a.a_bytes = rsrc_bytes((int64_t)Nb * P * Q * K);
   a.b_bytes = rsrc_bytes((int64_t)C * a.K);
   a.g = make_geom(P, Q, K, H, W, S, stride, pad, R);

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict
                                                         const float* __restrict__ shift,
                                                         const float* __restrict__ rscale,
                                                         const float* __restrict__ rshift, int64_t nvec, int C,
-                                                        int relu) {
+                                                        int relu, uint8_t* __restrict__ bits) {
   EwIter it(nvec, C);
   float a[8], b[8], pr[8], qr[8];
   if (FIXC) {
@@ -291,7 +291,9 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
       }
-      st16(y, v, pack8(f));
+      const uint4 o = pack8(f);
+      st16(y, v, o);
+      if (bits) bits[v] = (uint8_t)nz_bits8(o);  // the consumer's ReLU mask, 1/16 of y's bytes
       if (!FIXC) c = it.chan(c, C);
     }
   }
@@ -836,14 +838,15 @@ inline bool ew_fixc(int grid, int C) { return ((int64_t)grid * NT * 8) % C == 0;
 
 template <bool RES_BN>
 inline void launch_bn_apply(const void* x, const void* res, void* y, const float* scale, const float* shift,
-                            const float* rscale, const float* rshift, int64_t nvec, int C, int relu, hipStream_t st) {
+                            const float* rscale, const float* rshift, int64_t nvec, int C, int relu, hipStream_t st,
+                            void* bits = nullptr) {
   const int grid = ew_grid(nvec);
   if (ew_fixc(grid, C))
     hipLaunchKernelGGL((bn_apply_kernel_t<RES_BN, true>), dim3(grid), dim3(NT), 0, st, (const bf16_t*)x,
-                       (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu);
+                       (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu, (uint8_t*)bits);
   else
     hipLaunchKernelGGL((bn_apply_kernel_t<RES_BN, false>), dim3(grid), dim3(NT), 0, st, (const bf16_t*)x,
-                       (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu);
+                       (const bf16_t*)res, (bf16_t*)y, scale, shift, rscale, rshift, nvec, C, relu, (uint8_t*)bits);
 }
 
 inline void launch_bn_bwd_apply(const void* dy, const void* y, const void* x, const float* coef, void* dx, void* dres,
@@ -1163,6 +1166,20 @@ MI_API int mi_bn_apply_dual(const void* x, const void* res, void* y, int M, int 
   if (C % 8 != 0 || !x || !res || !y) return (int)hipErrorInvalidValue;
   int64_t nvec = (int64_t)M * C / 8;
   launch_bn_apply<true>(x, res, y, scale, shift, rscale, rshift, nvec, C, relu, st);
+  return (int)hipGetLastError();
+}
+
+// y = relu(x*scale + shift + res') with res' = res (rscale null) or res*rscale + rshift, plus the
+// ReLU mask of y as one byte per 8 channels (bits [M][C/8], bit j = channel 8i+j of y is > 0): a
+// block output whose mask the next block's data-gradient epilogue reads instead of y.
+MI_API int mi_bn_apply_bits(const void* x, const void* res, void* y, void* bits, int M, int C, const float* scale,
+                            const float* shift, const float* rscale, const float* rshift, hipStream_t st) {
+  if (C % 8 != 0 || !x || !y || !bits || (rscale && (!res || !rshift))) return (int)hipErrorInvalidValue;
+  int64_t nvec = (int64_t)M * C / 8;
+  if (rscale)
+    launch_bn_apply<true>(x, res, y, scale, shift, rscale, rshift, nvec, C, 1, st, bits);
+  else
+    launch_bn_apply<false>(x, res, y, scale, shift, nullptr, nullptr, nvec, C, 1, st, bits);
   return (int)hipGetLastError();
 }
 

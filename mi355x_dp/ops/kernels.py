@@ -22,6 +22,7 @@ signature("mi_conv_nol_ok", I, I, I, I, I, I, I, I, I, I, I)
 signature("mi_conv2d_fwd_nol", P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_wgrad_nol", P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv2d_dgrad_ex3", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P, P, P)
+signature("mi_conv2d_dgrad_ex4", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P, P, P, P)
 signature("mi_conv_wtrans", P, P, I, I, I, P)
 # stem_conv.hip (ops/stem.py): weight pack and the gradient straight into the parameter's buffer
 signature("mi_stem_wpack", P, P, I, I, I, I, L, L, L, L, P)
@@ -42,6 +43,7 @@ signature("mi_bn_set_small_elems", L)
 signature("mi_bn_init_counters")
 signature("mi_bn_fwd_train", P, P, P, I, I, F, F, P, P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_bn_apply_dual", P, P, P, I, I, P, P, P, P, I, P)
+signature("mi_bn_apply_bits", P, P, P, P, I, I, P, P, P, P, P)
 signature("mi_bn_fwd_eval", P, P, P, I, I, F, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_train", P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P)
 signature("mi_bn_bwd_eval", P, P, P, P, P, I, I, I, P)

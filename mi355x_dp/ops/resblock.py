@@ -165,14 +165,37 @@ def _bn_fwd(c, slab, rows, bn, relu, res=None, apply=True):
 
 def _bn_fwd_dual(c, slab, rows, bn, cd, slabd, rowsd, bnd):
     """A block's last BN + ReLU with the projection shortcut's BN folded into the same pass:
-    y = relu(bn(c) + bn_d(cd)) -- the shortcut's normalised activation is never materialised."""
+    y = relu(bn(c) + bn_d(cd)) -- the shortcut's normalised activation is never materialised.
+    Returns (y, mean, invstd, mean_d, invstd_d, bits) -- see _out_apply."""
     _, md, isd, sd, hd = _bn_fwd(cd, slabd, rowsd, bnd, relu=False, apply=False)
     _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bn, relu=True, apply=False)
+    y, bits = _out_apply(c, cd, sc, sh, sd, hd)
+    return y, m, inv, md, isd, bits
+
+
+# A block output's ReLU mask as one byte per 8 channels (mi_bn_apply_bits): the next block's conv1
+# data-gradient epilogue (epi 5) reads it instead of the bf16 block output -- 1/16 of the bytes in
+# the most memory-bound kernels of the backward.  Tensors below this size keep the single-launch
+# small-BN path (finalize + apply fused) and the bf16 mask source.
+OUT_BITS = os.environ.get("MI355X_DP_OUT_BITS", "1") != "0"
+OUT_BITS_MIN = 1 << 22
+
+
+def _out_apply(c, res, sc, sh, rsc=None, rsh=None):
+    """block output y = relu(c * sc + sh + res') (res' = res, or res * rsc + rsh for a projection
+    shortcut's raw conv output) -> (y, bits); bits is None when the mask is not emitted."""
     N, C, H, W = c.shape
     y = torch.empty_like(c, memory_format=CL)
-    _lib.call("mi_bn_apply_dual", ptr(c), ptr(cd), ptr(y), N * H * W, C, ptr(sc), ptr(sh), ptr(sd), ptr(hd), 1,
-              stream_of(c))
-    return y, m, inv, md, isd
+    if OUT_BITS and N * H * W * C >= OUT_BITS_MIN:
+        bits = torch.empty((N, H, W, C // 8), dtype=torch.uint8, device=c.device)
+        _lib.call("mi_bn_apply_bits", ptr(c), ptr(res), ptr(y), ptr(bits), N * H * W, C, ptr(sc), ptr(sh), ptr(rsc),
+                  ptr(rsh), stream_of(c))
+        return y, bits
+    if rsc is not None:
+        _lib.call("mi_bn_apply_dual", ptr(c), ptr(res), ptr(y), N * H * W, C, ptr(sc), ptr(sh), ptr(rsc), ptr(rsh), 1,
+                  stream_of(c))
+        return y, None
+    return None, None
 
 
 # ---------------------------------------------------------------------- backward pieces
@@ -199,12 +222,17 @@ def _wgrad(x, dy, spec, nol=None):
     return _finish_grad(spec.w, g)
 
 
-def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0, stats=None, flags=0):
+def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0, stats=None, flags=0, mbits=None):
     N, C, H, W = x_shape
     K, _, R, S = spec.w.shape
     P, Q = dy.shape[2], dy.shape[3]
     st = stream_of(dy)
     wt = weight_bf16_t(spec.w)
+    if mbits is not None:  # ReLU mask bytes instead of the bf16 BN output (epi 4 / 5)
+        _lib.call("mi_conv2d_dgrad_ex4", ptr(dy), ptr(wt), ptr(out), N, H, W, C, K, R, S, spec.stride, spec.pad, P,
+                  Q, int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), int(flags), ptr(None),
+                  ptr(None), ptr(mbits), st)
+        return out
     _lib.call("mi_conv2d_dgrad_ex2", ptr(dy), ptr(wt), ptr(out), N, H, W, C, K, R, S, spec.stride, spec.pad, P, Q,
               int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), int(flags), st)
     return out
@@ -273,6 +301,7 @@ class _ResBlock(torch.autograd.Function):
         n_main = len(convs) - (1 if has_ds else 0)
         x = _nhwc(x)
         saved_c, saved_y, saved_m, saved_i = [], [], [], []
+        out_bits = None          # the block output's ReLU mask bytes (_out_apply), for the next block
         aux = _aux_stream(x.device) if has_ds else None
         if aux is not None:
             # shortcut conv + its BN statistics / finalize, concurrently with the main chain
@@ -291,13 +320,13 @@ class _ResBlock(torch.autograd.Function):
                 if has_ds and aux is not None:
                     _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bns[i], relu=True, apply=False)
                     main.wait_stream(aux)
-                    N_, C_, H_, W_ = c.shape
-                    y = torch.empty_like(c, memory_format=CL)
-                    _lib.call("mi_bn_apply_dual", ptr(c), ptr(cd), ptr(y), N_ * H_ * W_, C_, ptr(sc), ptr(sh),
-                              ptr(sd), ptr(hd), 1, stream_of(c))
+                    y, out_bits = _out_apply(c, cd, sc, sh, sd, hd)
                 elif has_ds:
                     cd, slabd, rowsd = _conv_fwd_stats(x, convs[-1])
-                    y, m, inv, md, isd = _bn_fwd_dual(c, slab, rows, bns[i], cd, slabd, rowsd, bns[-1])
+                    y, m, inv, md, isd, out_bits = _bn_fwd_dual(c, slab, rows, bns[i], cd, slabd, rowsd, bns[-1])
+                elif OUT_BITS and c.numel() >= OUT_BITS_MIN:
+                    _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bns[i], relu=True, apply=False)
+                    y, out_bits = _out_apply(c, x, sc, sh)
                 else:
                     y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True, res=x)
             elif _nol_ok(c, convs[i + 1]):
@@ -323,7 +352,8 @@ class _ResBlock(torch.autograd.Function):
         ctx.save_for_backward(*tensors)
         ctx.specs = specs
         ctx.n_main = n_main
-        ctx.out_bnsrc = (saved_c[-1], saved_m[-1])   # read by the next block (input = this output)
+        # read by the next block (input = this output): its last BN's input, mean and ReLU mask bytes
+        ctx.out_bnsrc = (saved_c[-1], saved_m[-1], out_bits)
         ctx.prev_bnsrc = prev_bnsrc
         return h
 
@@ -400,13 +430,14 @@ class _ResBlock(torch.autograd.Function):
             grads[id(bns[-1].w)], grads[id(bns[-1].b)] = _finish_grad(bns[-1].w, gw), _finish_grad(bns[-1].b, gb)
         if ctx.prev_bnsrc is not None:
             # dx = mask_prev * (dx + dgrad_1) + the previous block's last-BN backward statistics
-            c_prev, m_prev = ctx.prev_bnsrc
+            c_prev, m_prev, bits_prev = ctx.prev_bnsrc
             N, C, H, W = x.shape
             lib = _lib.load()
             rows = lib.mi_dgrad_stat_rows(N, H, W, C, dc.shape[2], dc.shape[3], convs[0].stride,
                                           convs[0].w.shape[0], convs[0].w.shape[2] * convs[0].w.shape[3])
             slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dx.device)
-            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab, flags=acc_flags)
+            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab, flags=acc_flags,
+                   mbits=bits_prev)
             _HANDOFF[(dx.data_ptr(), dx.device.index)] = (slab, rows, dx._version, c_prev.data_ptr())
         else:
             _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx, flags=acc_flags)   # dx += dgrad_1

@@ -641,3 +641,68 @@ def test_normalize_on_load_kernels(shape):
     mism = float(((dz1.float() != dz2.float()).float().mean()))
     assert mism < 1e-3, ("dgrad mask", mism)  # only where c * scale + shift rounds to ~0
     assert rel_err(sl2[:rows], sl1[:rows]) < 1e-2, ("dgrad stats", rel_err(sl2[:rows], sl1[:rows]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [
+    # (N, C, H, K): the block-input data gradient (1x1 conv1 of the next block, epi 5) on the 128-tile
+    # kernel and on the 256x256 kernel (wide outputs)
+    (8, 256, 56, 64), (16, 512, 28, 128), (32, 1024, 14, 256),
+])
+def test_block_output_mask_bits(shape):
+    """mi_bn_apply_bits (a block's last BN + residual + ReLU, with the ReLU mask as one byte per 8
+    channels) against the y-only apply, and the data-gradient epilogue (epi 5: accumulate, mask,
+    BN-backward statistics) reading the mask bytes (mi_conv2d_dgrad_ex4) against reading y: both
+    bit-identical."""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops import kernels  # noqa: F401
+    from mi355x_dp.ops._lib import ptr, stream_of
+    N, C, H, K = shape
+    M = N * H * H
+    g = torch.Generator(device="cuda").manual_seed(5)
+    c = torch.randn(N, C, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    res = torch.randn(N, C, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    scale = torch.rand(C, device="cuda", generator=g) + 0.5
+    shift = torch.randn(C, device="cuda", generator=g) * 0.5
+    rsc = torch.rand(C, device="cuda", generator=g) + 0.5
+    rsh = torch.randn(C, device="cuda", generator=g) * 0.5
+    st = stream_of(c)
+    for rs in ((None, None), (rsc, rsh)):
+        y_ref = torch.empty_like(c)
+        if rs[0] is None:
+            _lib.call("mi_bn_apply_dual", ptr(c), ptr(res), ptr(y_ref), M, C, ptr(scale), ptr(shift),
+                      ptr(torch.ones(C, device="cuda")), ptr(torch.zeros(C, device="cuda")), 1, st)
+        else:
+            _lib.call("mi_bn_apply_dual", ptr(c), ptr(res), ptr(y_ref), M, C, ptr(scale), ptr(shift), ptr(rs[0]),
+                      ptr(rs[1]), 1, st)
+        y = torch.empty_like(c)
+        bits = torch.empty((N, H, H, C // 8), dtype=torch.uint8, device="cuda")
+        _lib.call("mi_bn_apply_bits", ptr(c), ptr(res), ptr(y), ptr(bits), M, C, ptr(scale), ptr(shift), ptr(rs[0]),
+                  ptr(rs[1]), st)
+        torch.cuda.synchronize()
+        if rs[0] is not None:
+            assert torch.equal(y, y_ref)
+        else:  # identity residual: relu(c*scale + shift + res)
+            ref = torch.relu(c.float() * scale.view(1, C, 1, 1) + shift.view(1, C, 1, 1) + res.float())
+            assert rel_err(y, ref) < 1e-2
+        pos = (y.permute(0, 2, 3, 1).reshape(M, C // 8, 8).float() > 0).to(torch.int32)
+        want = (pos << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8)
+        assert torch.equal(bits.reshape(M, C // 8), want)
+    # data gradient of a 1x1 conv C <- K with the epi-5 BN-backward epilogue: mask from y vs from bits
+    lib = _lib.load()
+    w = (torch.randn(K, C, 1, 1, device="cuda", generator=g) * (2.0 / C) ** 0.5).to(BF)
+    wt = w.permute(1, 2, 3, 0).contiguous()  # [C][1][1][K]
+    dy = torch.randn(N, K, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    acc0 = torch.randn(N, C, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    mean = c.float().mean((0, 2, 3))
+    rows = lib.mi_dgrad_stat_rows(N, H, H, C, H, H, 1, K, 1)
+    sl1 = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), device="cuda")
+    sl2 = torch.empty_like(sl1)
+    dx1, dx2 = acc0.clone(), acc0.clone()
+    _lib.call("mi_conv2d_dgrad_ex2", ptr(dy), ptr(wt), ptr(dx1), N, H, H, C, K, 1, 1, 1, 0, H, H, 5, ptr(y), ptr(c),
+              ptr(mean), 1, ptr(sl1), 0, st)
+    _lib.call("mi_conv2d_dgrad_ex4", ptr(dy), ptr(wt), ptr(dx2), N, H, H, C, K, 1, 1, 1, 0, H, H, 5, ptr(None), ptr(c),
+              ptr(mean), 1, ptr(sl2), 0, ptr(None), ptr(None), ptr(bits), st)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2)
+    assert torch.equal(sl1[:rows], sl2[:rows])
