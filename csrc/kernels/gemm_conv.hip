@@ -1574,6 +1574,17 @@ static bool tn_slabs_on() {
   return g_tn_slabs != 0;
 }
 
+// TN k-loop depth with direct-to-LDS loads: 1 = load, wait, compute per k-step (default); 2 = the
+// next k-step's loads in flight under the current one's MFMAs (MI355X_DP_TN_STAGES=2, A/B)
+static int g_tn_stages = -1;
+static int tn_stages() {
+  if (g_tn_stages < 0) {
+    const char* e = std::getenv("MI355X_DP_TN_STAGES");
+    g_tn_stages = (e && e[0] == '2') ? 2 : 1;
+  }
+  return g_tn_stages;
+}
+
 template <int BM, int BN>
 hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   int tiles = cdiv(a.M, BM) * cdiv(a.N, BN);
@@ -1591,7 +1602,7 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
     a.ws = splitk_workspace((size_t)tiles * splits * BM * BN, st);
   // fewer than 8 splits: the reduce is one split group (in-order sum), which the last-arriving
   // split runs itself -- no reduce launch; more splits keep the chip-wide reduce kernel
-  const int st_n = glds_on() ? 1 : 2;
+  const int st_n = glds_on() ? tn_stages() : 2;
   if (a.ws && splits < 8 && tiles <= SPLITK_COUNTERS && st_n == 1 && tn_split_fused() && !a.nol_scale)
     a.cnt = splitk_counters(st);
   if (a.nol_scale) {

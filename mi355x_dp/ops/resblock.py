@@ -178,6 +178,7 @@ def _bn_fwd_dual(c, slab, rows, bn, cd, slabd, rowsd, bnd):
 # the most memory-bound kernels of the backward.  Tensors below this size keep the single-launch
 # small-BN path (finalize + apply fused) and the bf16 mask source.
 OUT_BITS = os.environ.get("MI355X_DP_OUT_BITS", "1") != "0"
+INNER_BITS = os.environ.get("MI355X_DP_INNER_BITS", "1") != "0"  # the same for the inner BNs (bn1 / bn2)
 OUT_BITS_MIN = 1 << 22
 
 
@@ -238,10 +239,11 @@ def _dgrad(dy, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0
     return out
 
 
-def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev, mask=None):
+def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev, mask=None, bits=None):
     """conv dgrad fused with the relu mask + backward statistics of the BN that produced the conv's
     input: returns (dz, slab, rows).  ``mask`` = that BN's (scale, shift): the mask comes from
-    ``c_prev`` (normalize-on-load schedules never write ``y_prev``, which is then None)."""
+    ``c_prev`` (normalize-on-load schedules never write ``y_prev``, which is then None).  ``bits``:
+    the mask as bytes of 8 channel bits (_out_apply) instead of reading ``y_prev``."""
     N, C, H, W = c_prev.shape
     lib = _lib.load()
     rows = lib.mi_dgrad_stat_rows(N, H, W, C, dy.shape[2], dy.shape[3], spec.stride, spec.w.shape[0],
@@ -255,7 +257,7 @@ def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev, mask=None):
                   spec.stride, spec.pad, P, Q, EPI_BN_BWD, ptr(None), ptr(c_prev), ptr(mean_prev), 1, ptr(slab), 0,
                   ptr(mask[0]), ptr(mask[1]), stream_of(dy))
         return dz, slab, rows
-    _dgrad(dy, spec, y_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab)
+    _dgrad(dy, spec, c_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab, mbits=bits)
     return dz, slab, rows
 
 
@@ -302,6 +304,7 @@ class _ResBlock(torch.autograd.Function):
         x = _nhwc(x)
         saved_c, saved_y, saved_m, saved_i = [], [], [], []
         out_bits = None          # the block output's ReLU mask bytes (_out_apply), for the next block
+        inner_bits = [None] * n_main  # inner BNs' ReLU mask bytes, for the data gradients
         aux = _aux_stream(x.device) if has_ds else None
         if aux is not None:
             # shortcut conv + its BN statistics / finalize, concurrently with the main chain
@@ -337,7 +340,13 @@ class _ResBlock(torch.autograd.Function):
                 nol = (sc, sh)
                 NOL_USED[0] += 1
             else:
-                y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True)
+                if OUT_BITS and INNER_BITS and c.numel() >= OUT_BITS_MIN:
+                    # inner BN: y for the next conv (forward, weight gradient) plus its ReLU mask bytes
+                    # for that conv's data-gradient epilogue
+                    _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bns[i], relu=True, apply=False)
+                    y, inner_bits[i] = _out_apply(c, None, sc, sh)
+                else:
+                    y, m, inv = _bn_fwd(c, slab, rows, bns[i], relu=True)
                 nol = None
             saved_c.append(c); saved_y.append(y); saved_m.append(m); saved_i.append(inv)
             saved_nol.append(nol if y is None else None)
@@ -354,6 +363,7 @@ class _ResBlock(torch.autograd.Function):
         ctx.n_main = n_main
         # read by the next block (input = this output): its last BN's input, mean and ReLU mask bytes
         ctx.out_bnsrc = (saved_c[-1], saved_m[-1], out_bits)
+        ctx.inner_bits = inner_bits
         ctx.prev_bnsrc = prev_bnsrc
         return h
 
@@ -417,7 +427,8 @@ class _ResBlock(torch.autograd.Function):
             nol = nols[i - 1]
             inp = ys[i - 1] if nol is None else cs[i - 1]
             grads[id(convs[i].w)] = _wgrad(inp, dc, convs[i], nol)
-            dz, slab, rows = _dgrad_bn(dc, convs[i], ys[i - 1], cs[i - 1], ms[i - 1], mask=nol)
+            dz, slab, rows = _dgrad_bn(dc, convs[i], ys[i - 1], cs[i - 1], ms[i - 1], mask=nol,
+                                       bits=ctx.inner_bits[i - 1])
             dc, gw, gb = _bn_bwd_pre(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
             grads[id(bns[i - 1].w)], grads[id(bns[i - 1].b)] = gw, gb
         grads[id(convs[0].w)] = _wgrad(x, dc, convs[0])
@@ -443,6 +454,7 @@ class _ResBlock(torch.autograd.Function):
             _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx, flags=acc_flags)   # dx += dgrad_1
         ctx.prev_bnsrc = None
         ctx.out_bnsrc = None
+        ctx.inner_bits = None
         out = [dx, None, None]
         for p in ctx.params_order:
             out.append(grads.get(id(p)))
