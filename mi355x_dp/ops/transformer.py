@@ -94,12 +94,13 @@ def _wbgrad(weight, bias, dy2, x2):
     return _finish_grad(weight, g), _finish_grad(bias, gb)
 
 
-# Plain data-gradient GEMMs (no fused epilogue: the qkv / proj / fc1 input gradients) through the
-# library GEMM (hipBLASLt): on the ViT-B/16 batch-256 shapes it runs 1.1-1.4x the native 256x256
-# kernel (profiles/vit_r3_gemm_attention.md).  Every GEMM with a fused epilogue stays native.
-# MI355X_DP_BLAS_DGRAD=0 keeps all of them native.
+# Plain data-gradient GEMMs (no fused epilogue: the qkv / proj / fc1 input gradients) run on the
+# native 256x256 kernel like every other GEMM of the step.  MI355X_DP_BLAS_DGRAD=1 routes them to
+# the library GEMM (hipBLASLt) instead: 1.1-1.4x faster on these N = 768 shapes in isolation
+# (profiles/vit_r3_gemm_attention.md) but only +1.8 % on the whole ViT-B/16 step
+# (profiles/raw/r4_vit_{lib,native}.log: 6,307 vs 6,196 img/s), so the all-native step is the default.
 import os as _os
-BLAS_DGRAD = _os.environ.get("MI355X_DP_BLAS_DGRAD", "1") == "1"
+BLAS_DGRAD = _os.environ.get("MI355X_DP_BLAS_DGRAD", "0") == "1"
 
 
 def _dgrad(dy2, weight, epi=EPI_NONE, aux=None):
