@@ -62,8 +62,10 @@ def parse(argv=None):
                         "(comm-stream / overlap traces on one GPU); the headline N=1 run leaves it off")
     p.add_argument("--grad-comm", default=os.environ.get("MI355X_DP_GRAD_COMM", "fp32"), choices=("fp32", "bf16"),
                    help="gradient all-reduce dtype (bf16: half the bytes; fp32 master weights either way)")
-    p.add_argument("--wgrad-stream", type=int, default=int(os.environ.get("MI355X_DP_WGRAD_STREAM", "1")),
-                   choices=(0, 1), help="conv weight gradients on a side HIP stream (overlap with data gradients)")
+    p.add_argument("--wgrad-stream", default=os.environ.get("MI355X_DP_WGRAD_STREAM", "auto"),
+                   choices=("auto", "0", "1"),
+                   help="weight gradients on a side HIP stream (overlap with data gradients); auto: on for "
+                        "conv nets, off for all-GEMM models (mi355x_dp.parallel.ddp.WGRAD_STREAM)")
     p.add_argument("--shard-optimizer", action="store_true",
                    default=os.environ.get("MI355X_DP_SHARD_OPTIMIZER", "0") == "1",
                    help="SMDDP balanced shards: reduce-scatter gradients, shard-local SGD, all-gather parameters")
@@ -242,7 +244,7 @@ def main(argv=None):
     if args.force_comm:
         kw["force_comm"] = True
     kw["grad_comm"] = args.grad_comm
-    kw["wgrad_stream"] = bool(args.wgrad_stream)
+    kw["wgrad_stream"] = "auto" if args.wgrad_stream == "auto" else args.wgrad_stream == "1"
     if args.calibrate_comm:
         kw["calibrate"] = True
     kw["shard_optimizer"] = bool(args.shard_optimizer)
@@ -388,7 +390,7 @@ def main(argv=None):
                 "buckets": len(engine.buckets),
                 "grad_comm": args.grad_comm,
                 "shard_optimizer": bool(args.shard_optimizer),
-                "wgrad_stream": bool(args.wgrad_stream),
+                "wgrad_stream": engine.wgrad_stream is not None,
                 "hip_graph": bool(args.graph),
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             },

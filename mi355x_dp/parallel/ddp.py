@@ -62,9 +62,18 @@ GRAD_COMM = os.environ.get("MI355X_DP_GRAD_COMM", "fp32")
 # measure the all-reduce alpha-beta model on the actual fabric at construction (world > 1, planner
 # cap not given explicitly) instead of assuming 7 x 153 GB/s xGMI rings with a 25 us launch cost
 CALIBRATE = os.environ.get("MI355X_DP_CALIBRATE", "0") == "1"
-# run conv weight gradients on a side HIP stream, overlapping the data-gradient chain
-# (mi355x_dp.ops.functional.WgradStream); CUDA engines only
-WGRAD_STREAM = os.environ.get("MI355X_DP_WGRAD_STREAM", "1") == "1"
+# run weight gradients on a side HIP stream, overlapping the data-gradient chain
+# (mi355x_dp.ops.functional.WgradStream); CUDA engines only.  "auto" (default): on for models with
+# convolutions -- their BatchNorm / elementwise-heavy data-gradient chain leaves CUs the weight
+# gradients fill (ResNet-152 bs256: 5,580 vs 5,132 img/s) -- and off for all-GEMM models, where
+# both streams are MFMA-bound and only contend (ViT-B/16 bs256: 6,780 vs 6,435 img/s;
+# profiles/raw/r4_vws*, r4_r152ws0).  MI355X_DP_WGRAD_STREAM=1 / 0 forces it.
+_WS = os.environ.get("MI355X_DP_WGRAD_STREAM", "auto")
+WGRAD_STREAM = "auto" if _WS == "auto" else _WS == "1"
+
+
+def _wgrad_stream_auto(module: nn.Module) -> bool:
+    return any(isinstance(m, nn.Conv2d) for m in module.modules())
 # balanced-shard mode: reduce-scatter gradients, shard-local optimizer, all-gather parameters
 SHARD_OPTIMIZER = os.environ.get("MI355X_DP_SHARD_OPTIMIZER", "0") == "1"
 
@@ -231,7 +240,7 @@ class DataParallel(nn.Module):
                  bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
                  check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM,
-                 wgrad_stream: bool = WGRAD_STREAM, calibrate: bool = CALIBRATE,
+                 wgrad_stream=WGRAD_STREAM, calibrate: bool = CALIBRATE,
                  shard_optimizer: bool = SHARD_OPTIMIZER, device_ids=None, output_device=None, dim: int = 0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  static_graph: bool = False, foreign_optimizer: bool = False):
@@ -357,6 +366,8 @@ class DataParallel(nn.Module):
                                           bool(force_comm), self._comm_buf, self.sharded)
         self._comm_hook = None
         self.wgrad_stream = None
+        if wgrad_stream == "auto":
+            wgrad_stream = _wgrad_stream_auto(module)
         if wgrad_stream and self.flat.grad.is_cuda:
             from mi355x_dp.ops.functional import WgradStream
             self.wgrad_stream = WgradStream(self.flat.grad.device)
