@@ -65,7 +65,7 @@ def parse(argv=None):
     p.add_argument("--wgrad-stream", default=os.environ.get("MI355X_DP_WGRAD_STREAM", "auto"),
                    choices=("auto", "0", "1"),
                    help="weight gradients on a side HIP stream (overlap with data gradients); auto: on for "
-                        "conv nets, off for all-GEMM models (mi355x_dp.parallel.ddp.WGRAD_STREAM)")
+                        "BatchNorm conv nets, off for GEMM-bound models (mi355x_dp.parallel.ddp.WGRAD_STREAM)")
     p.add_argument("--shard-optimizer", action="store_true",
                    default=os.environ.get("MI355X_DP_SHARD_OPTIMIZER", "0") == "1",
                    help="SMDDP balanced shards: reduce-scatter gradients, shard-local SGD, all-gather parameters")

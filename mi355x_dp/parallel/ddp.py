@@ -64,16 +64,18 @@ GRAD_COMM = os.environ.get("MI355X_DP_GRAD_COMM", "fp32")
 CALIBRATE = os.environ.get("MI355X_DP_CALIBRATE", "0") == "1"
 # run weight gradients on a side HIP stream, overlapping the data-gradient chain
 # (mi355x_dp.ops.functional.WgradStream); CUDA engines only.  "auto" (default): on for models with
-# convolutions -- their BatchNorm / elementwise-heavy data-gradient chain leaves CUs the weight
-# gradients fill (ResNet-152 bs256: 5,580 vs 5,132 img/s) -- and off for all-GEMM models, where
-# both streams are MFMA-bound and only contend (ViT-B/16 bs256: 6,780 vs 6,435 img/s;
-# profiles/raw/r4_vws*, r4_r152ws0).  MI355X_DP_WGRAD_STREAM=1 / 0 forces it.
+# BatchNorm -- their BatchNorm / elementwise-heavy data-gradient chain leaves CUs the weight
+# gradients fill (ResNet-152 bs256: 5,580 vs 5,132 img/s) -- and off for GEMM-bound models without
+# BatchNorm (a transformer's patch-embedding conv aside), where both streams are MFMA-bound and only
+# contend (ViT-B/16 bs256: 6,780 vs 6,435 img/s; profiles/raw/r4_vws*, r4_r152ws0).
+# MI355X_DP_WGRAD_STREAM=1 / 0 forces it.
 _WS = os.environ.get("MI355X_DP_WGRAD_STREAM", "auto")
 WGRAD_STREAM = "auto" if _WS == "auto" else _WS == "1"
 
 
 def _wgrad_stream_auto(module: nn.Module) -> bool:
-    return any(isinstance(m, nn.Conv2d) for m in module.modules())
+    """side stream for conv + BatchNorm networks (the memory-bound BN passes leave CUs to fill)"""
+    return any(isinstance(m, nn.modules.batchnorm._BatchNorm) for m in module.modules())
 # balanced-shard mode: reduce-scatter gradients, shard-local optimizer, all-gather parameters
 SHARD_OPTIMIZER = os.environ.get("MI355X_DP_SHARD_OPTIMIZER", "0") == "1"
 

@@ -938,3 +938,13 @@ def test_comm_path_choice_from_probe_table():
     assert choose_paths([{"bytes": MB, "rccl": 0.1, "ipc_oneshot": -1.0, "ipc_twoshot": None}]) == (0, 0)
     # RCCL not measured: IPC wins wherever it ran
     assert choose_paths([{"bytes": MB, "ipc_oneshot": 0.1, "ipc_twoshot": 0.2}]) == (MB, MB)
+
+
+def test_wgrad_stream_auto_policy():
+    """The weight-gradient side stream defaults on for BatchNorm conv nets and off for GEMM-bound
+    models (ViT: its patch-embedding conv does not count)."""
+    from mi355x_dp.models import get_model
+    from mi355x_dp.parallel.ddp import _wgrad_stream_auto
+    assert _wgrad_stream_auto(get_model("resnet50"))
+    assert _wgrad_stream_auto(get_model("resnet18"))
+    assert not _wgrad_stream_auto(get_model("vit_b_16"))
