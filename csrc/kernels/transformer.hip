@@ -193,6 +193,117 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// The same backward with 16-byte accesses, for D % 256 == 0 (D <= 256 * LN16_MAXV): a row is one
+// HALF-wave -- lane hl = lane & 31 of half hf owns the 8-element chunks hl + 32 i -- so a wave works
+// on 2 rows at a time (RW16 row pairs in flight), every load / store is a 16-byte access (half the
+// memory instructions of the 8-byte, full-wave-row kernel), and the row reductions are 5-step
+// half-wave xor shuffles.  dw / db partials as ln_bwd_kernel, over 8 half-waves per block.
+#ifndef MI_LN16_RW
+#define MI_LN16_RW 2   // row pairs in flight per wave
+#endif
+constexpr int LN16_MAXV = 4;
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void ln_bwd16_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                       const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                       const float* __restrict__ rstd_in,
+                                                       const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                       float* __restrict__ dw, float* __restrict__ db, int M, int D,
+                                                       float* __restrict__ rep, int R) {
+  extern __shared__ float red[];  // [8 half-waves][D]
+  constexpr int RW = MI_LN16_RW;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5, hl = lane & 31;
+  float pw[V][8], pb[V][8], wr[V][8];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = 8 * (hl + 32 * i);
+    const float4 a = *(const float4*)(w + c), b = *(const float4*)(w + c + 4);
+    wr[i][0] = a.x; wr[i][1] = a.y; wr[i][2] = a.z; wr[i][3] = a.w;
+    wr[i][4] = b.x; wr[i][5] = b.y; wr[i][6] = b.z; wr[i][7] = b.w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { pw[i][e] = 0.f; pb[i][e] = 0.f; }
+  }
+  const bf16_t* rsrc = dres ? dres : dy;  // no residual gradient: loaded, then ignored
+  const float invD = 1.f / (float)D;
+  for (int row0 = (blockIdx.x * 4 + wv) * 2 * RW; row0 < M; row0 += gridDim.x * 8 * RW) {
+    // every load of the RW row pairs first (rows past M read row M - 1 and are discarded)
+    uint4 qd[RW][V], qx[RW][V], qr[RW][V];
+    float mean[RW], rstd[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const size_t row = (size_t)min(row0 + 2 * r + hf, M - 1);
+      mean[r] = mean_in[row];
+      rstd[r] = rstd_in[row];
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const size_t off = row * D + 8 * (hl + 32 * i);
+        qd[r][i] = *(const uint4*)(dy + off);
+        qx[r][i] = *(const uint4*)(x + off);
+        qr[r][i] = *(const uint4*)(rsrc + off);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int row = row0 + 2 * r + hf;
+      const bool live = row < M;  // both halves take part in the shuffles; only live rows count
+      float xh[V][8], g[V][8];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        float d[8];
+        unpack8(qd[r][i], d);
+        unpack8(qx[r][i], xh[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[i][e] = (xh[i][e] - mean[r]) * rstd[r];
+          g[i][e] = d[e] * wr[i][e];
+          s1 += g[i][e];
+          s2 += g[i][e] * xh[i][e];
+          if (live) {
+            pw[i][e] += d[e] * xh[i][e];
+            pb[i][e] += d[e];
+          }
+        }
+      }
+      const float m1 = half_sum(s1) * invD, m2 = half_sum(s2) * invD;
+      if (live) {
+        bf16_t* dxr = dx + (size_t)row * D;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          float o[8], rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if (dres) unpack8(qr[r][i], rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = rv[e] + rstd[r] * (g[i][e] - m1 - xh[i][e] * m2);
+          *(uint4*)(dxr + 8 * (hl + 32 * i)) = pack8(o);
+        }
+      }
+    }
+  }
+  const int hw = wv * 2 + hf;  // half-wave index 0..7
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < V; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[hw * D + 8 * (hl + 32 * i) + e] = pass ? pb[i][e] : pw[i][e];
+    __syncthreads();
+    float* dst = rep ? rep + ((size_t)(blockIdx.x % R) * 2 + pass) * D : (pass ? db : dw);
+    for (int col = threadIdx.x; col < D; col += 256) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += red[k * D + col];
+      atomicAdd(dst + col, t);
+    }
+  }
+}
+
 // dw[c] += sum_r rep[r][0][c], db[c] += sum_r rep[r][1][c] (fixed order), replicas zeroed again
 __global__ __launch_bounds__(256) void ln_rep_reduce_kernel(float* __restrict__ rep, int R, int D,
                                                             float* __restrict__ dw, float* __restrict__ db) {
@@ -323,6 +434,40 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
   const int rw = nvec <= 4 ? MI_LN_BWD_RW : 1;
   float* rep = (dw && db) ? ln_rep_workspace(D, st) : nullptr;
   const int R = LN_REPLICAS;
+  static int ln16 = -1;  // MI355X_DP_LN_BWD16=0: always the full-wave-row kernel (A/B)
+  if (ln16 < 0) {
+    const char* e = std::getenv("MI355X_DP_LN_BWD16");
+    ln16 = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (ln16 && D % 256 == 0 && nvec <= LN16_MAXV && dw && db) {
+    const size_t lds16 = (size_t)8 * D * sizeof(float);
+    static std::map<std::pair<int, size_t>, int> resident16;
+    auto cap16 = [&](const void* fn) {
+      if (env_blocks > 0) return env_blocks;
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+      std::lock_guard<std::mutex> lk(res_mu);
+      auto it = resident16.find({dev, lds16});
+      if (it != resident16.end()) return it->second;
+      int cus = 256, per_cu = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds16) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+      resident16[{dev, lds16}] = cus * per_cu;
+      return cus * per_cu;
+    };
+#define MI_LN_BWD16_CASE(V)                                                                              \
+  case V:                                                                                                \
+    hipLaunchKernelGGL(ln_bwd16_kernel<V>,                                                               \
+                       dim3(min(cdiv(M, 8 * MI_LN16_RW), cap16((const void*)ln_bwd16_kernel<V>))), dim3(256), \
+                       lds16, st, (const bf16_t*)dy, (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres,    \
+                       (bf16_t*)dx, dw, db, M, D, rep, R);                                               \
+    break;
+    switch (nvec) { MI_LN_BWD16_CASE(1) MI_LN_BWD16_CASE(2) MI_LN_BWD16_CASE(3) MI_LN_BWD16_CASE(4) }
+#undef MI_LN_BWD16_CASE
+    if (rep) hipLaunchKernelGGL(ln_rep_reduce_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, rep, R, D, dw, db);
+    return (int)hipGetLastError();
+  }
 #define MI_LN_BWD(V)                                                                                    \
   case V:                                                                                               \
     hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(min(cdiv(M, 4 * rw), cap((const void*)ln_bwd_kernel<V>))),  \

@@ -28,7 +28,7 @@ def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(BF)
 
 
-@pytest.mark.parametrize("M,D", [(300, 768), (77, 64), (5, 1024), (130, 200)])
+@pytest.mark.parametrize("M,D", [(300, 768), (77, 64), (5, 1024), (130, 200), (4099, 768), (33, 512)])
 def test_layernorm_fwd_bwd(M, D):
     from mi355x_dp.ops import transformer as T
     x = rnd(M, D, scale=2.0) + 0.5
