@@ -304,6 +304,73 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const bf16_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- ViT token embedding
+// out[n][0][:] = cls + pos[0], out[n][1 + p][:] = patches[n][p][:] + pos[1 + p]: the class-token
+// concatenation and the position-embedding add in one pass (fp32 math, one bf16 rounding).
+// 8 channels per thread; T = tokens (patches + 1), D % 8 == 0.
+__global__ __launch_bounds__(256) void vit_embed_fwd_kernel(const bf16_t* __restrict__ patches,
+                                                            const float* __restrict__ cls,
+                                                            const float* __restrict__ pos, bf16_t* __restrict__ out,
+                                                            int64_t total8, int T, int D) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total8) return;
+  const int64_t e = i * 8;
+  const int64_t per = (int64_t)T * D;
+  const int64_t n = e / per;
+  const int64_t r = e - n * per;  // token * D + channel
+  const int t = (int)(r / D), c = (int)(r - (int64_t)t * D);
+  float f[8];
+  if (t == 0) {
+    *(float4*)&f[0] = *(const float4*)(cls + c);
+    *(float4*)&f[4] = *(const float4*)(cls + c + 4);
+  } else {
+    unpack8(*(const uint4*)(patches + (n * (T - 1) + (t - 1)) * D + c), f);
+  }
+  const float4 p0 = *(const float4*)(pos + r), p1 = *(const float4*)(pos + r + 4);
+  f[0] += p0.x; f[1] += p0.y; f[2] += p0.z; f[3] += p0.w;
+  f[4] += p1.x; f[5] += p1.y; f[6] += p1.z; f[7] += p1.w;
+  *(uint4*)(out + e) = pack8(f);
+}
+
+// backward, pass 1: dpatches[n][p] = dout[n][1 + p] (the patch conv's dense output gradient) and
+// per image-group partial sums part[g][t * D + c] = sum over the group's images of dout[n][t][c]
+// (fixed order).  Block (x, g): 256 threads x 8 channels of the T * D positions, images
+// [g * per_g, (g + 1) * per_g).
+__global__ __launch_bounds__(256) void vit_embed_bwd_kernel(const bf16_t* __restrict__ dout,
+                                                            bf16_t* __restrict__ dpatches, float* __restrict__ part,
+                                                            int N, int T, int D, int per_g) {
+  const int64_t TD = (int64_t)T * D;
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (r >= TD) return;
+  const int t = (int)(r / D);
+  const int n0 = blockIdx.y * per_g, n1 = min(N, n0 + per_g);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int n = n0; n < n1; ++n) {
+    const uint4 v = *(const uint4*)(dout + n * TD + r);
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] += f[q];
+    if (t > 0) *(uint4*)(dpatches + n * (TD - D) + (r - D)) = v;
+  }
+  float* o = part + (size_t)blockIdx.y * TD + r;
+  *(float4*)o = make_float4(s[0], s[1], s[2], s[3]);
+  *(float4*)(o + 4) = make_float4(s[4], s[5], s[6], s[7]);
+}
+
+// pass 2: dpos[r] += sum_g part[g][r]; dcls[c] += the same sum for token 0 (the class token's
+// gradient is the position embedding's row 0)
+__global__ __launch_bounds__(256) void vit_embed_bwd_sum_kernel(const float* __restrict__ part, int G, int64_t TD,
+                                                                int D, float* __restrict__ dpos,
+                                                                float* __restrict__ dcls) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= TD) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(size_t)g * TD + r];
+  if (dpos) dpos[r] += s;
+  if (dcls && r < D) dcls[r] += s;
+}
+
 // dw[c] += sum_r rep[r][0][c], db[c] += sum_r rep[r][1][c] (fixed order), replicas zeroed again
 __global__ __launch_bounds__(256) void ln_rep_reduce_kernel(float* __restrict__ rep, int R, int D,
                                                             float* __restrict__ dw, float* __restrict__ db) {
@@ -373,7 +440,7 @@ static float* ln_rep_workspace(int D, hipStream_t st) {
     const size_t bytes = sizeof(float) * LN_REPLICAS * 2 * (size_t)D;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
     if (hipMemset(p, 0, bytes) != hipSuccess) return nullptr;
-    hipDeviceSynchronize();  // the zeroing is complete before any stream uses the replicas
+    (void)hipDeviceSynchronize();  // the zeroing is complete before any stream uses the replicas
     mi_ws_retire(w.p);       // graphs captured earlier may still replay into it (common.h)
     w.p = p;
     w.D = D;
@@ -480,6 +547,38 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
   }
 #undef MI_LN_BWD
   if (rep) hipLaunchKernelGGL(ln_rep_reduce_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, rep, R, D, dw, db);
+  return (int)hipGetLastError();
+}
+
+// ViT embedding: out [N][T][D] bf16 from patches [N][T-1][D] bf16, cls [D] and pos [T][D] fp32.
+MI_API int mi_vit_embed_fwd(const void* patches, const float* cls, const float* pos, void* out, int N, int T, int D,
+                            hipStream_t st) {
+  if (D % 8 != 0 || N <= 0 || T < 2) return (int)hipErrorInvalidValue;
+  const int64_t total8 = (int64_t)N * T * D / 8;
+  hipLaunchKernelGGL(vit_embed_fwd_kernel, dim3((unsigned)cdiv(total8, 256)), dim3(256), 0, st,
+                     (const bf16_t*)patches, cls, pos, (bf16_t*)out, total8, T, D);
+  return (int)hipGetLastError();
+}
+
+// backward: dpatches [N][T-1][D] bf16 = dout[:, 1:], dpos [T][D] += sum_n dout[n], dcls [D] += sum_n
+// dout[n][0] (fp32, fixed-order sums; dpos / dcls may be null).  part: fp32 workspace of
+// mi_vit_embed_bwd_part_floats(N, T, D) floats.
+MI_API int64_t mi_vit_embed_bwd_part_floats(int N, int T, int D) {
+  const int G = std::min(N, 16);
+  return (int64_t)G * T * D;
+}
+
+MI_API int mi_vit_embed_bwd(const void* dout, void* dpatches, float* dpos, float* dcls, float* part, int N, int T,
+                            int D, hipStream_t st) {
+  if (D % 8 != 0 || N <= 0 || T < 2) return (int)hipErrorInvalidValue;
+  const int G = std::min(N, 16), per_g = cdiv(N, G);
+  const int G_used = cdiv(N, per_g);
+  const int64_t TD = (int64_t)T * D;
+  hipLaunchKernelGGL(vit_embed_bwd_kernel, dim3((unsigned)cdiv(TD / 8, 256), G_used), dim3(256), 0, st,
+                     (const bf16_t*)dout, (bf16_t*)dpatches, part, N, T, D, per_g);
+  if (dpos || dcls)
+    hipLaunchKernelGGL(vit_embed_bwd_sum_kernel, dim3((unsigned)cdiv(TD, 256)), dim3(256), 0, st, part, G_used,
+                       TD, D, dpos, dcls);
   return (int)hipGetLastError();
 }
 

@@ -16,6 +16,7 @@ bf16 column sums.
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -25,6 +26,10 @@ import torch.nn.functional as F
 from mi355x_dp.ops import functional as Fm
 from mi355x_dp.ops import transformer as Tm
 from .layers import Conv2d, Linear
+
+
+# MI355X_DP_VIT_EMBED=0: the stock concatenation / broadcast add / full-sequence final LayerNorm (A/B)
+_NATIVE_EMBED = os.environ.get("MI355X_DP_VIT_EMBED", "1") != "0"
 
 
 class LayerNorm(nn.LayerNorm):
@@ -151,6 +156,14 @@ class VisionTransformer(nn.Module):
                 x = x.to(torch.bfloat16, memory_format=torch.channels_last)
         x = self._process_input(x)
         n = x.shape[0]
+        if x.is_cuda and _NATIVE_EMBED and x.dtype == torch.bfloat16 and self.class_token.dtype == torch.float32 \
+                and self.hidden_dim % 8 == 0:
+            # class token + position embedding in one native pass (ops.transformer.vit_embed); the
+            # head reads only the class token and LayerNorm is per token, so the final LayerNorm
+            # runs on those rows alone -- the same output as encoder(x)[:, 0]
+            enc = self.encoder
+            x = enc.layers(enc.dropout(Tm.vit_embed(x, self.class_token, enc.pos_embedding)))
+            return self.heads(enc.ln(x[:, 0]))
         x = torch.cat([self.class_token.expand(n, -1, -1).to(x.dtype), x], dim=1)
         x = self.encoder(x)
         return self.heads(x[:, 0])

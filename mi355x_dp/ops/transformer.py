@@ -295,6 +295,43 @@ class _LayerNorm(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _VitEmbed(torch.autograd.Function):
+    """[class token ; patch embeddings] + position embedding as one native pass
+    (``mi_vit_embed_fwd``); backward: the patches' dense gradient plus the fixed-order batch sums
+    for the position embedding and the class token (``mi_vit_embed_bwd``) -- no concatenation,
+    broadcast-add, cast or reduction launches."""
+
+    @staticmethod
+    def forward(ctx, patches, cls, pos):
+        N, P, D = patches.shape
+        T = P + 1
+        p = patches.contiguous()
+        out = torch.empty((N, T, D), dtype=BF16, device=p.device)
+        _lib.call("mi_vit_embed_fwd", ptr(p), ptr(cls), ptr(pos), ptr(out), N, T, D, stream_of(p))
+        ctx.params = (cls, pos)
+        ctx.shape = (N, T, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cls, pos = ctx.params
+        N, T, D = ctx.shape
+        d = dout.to(BF16).contiguous()
+        dp = torch.empty((N, T - 1, D), dtype=BF16, device=d.device)
+        gpos = _grad_buffer(pos) if ctx.needs_input_grad[2] else None
+        gcls = _grad_buffer(cls) if ctx.needs_input_grad[1] else None
+        part = torch.empty(int(_lib.load().mi_vit_embed_bwd_part_floats(N, T, D)), dtype=F32, device=d.device)
+        _lib.call("mi_vit_embed_bwd", ptr(d), ptr(dp), ptr(gpos), ptr(gcls), ptr(part), N, T, D, stream_of(d))
+        dcls = _finish_grad(cls, gcls) if gcls is not None else None
+        dpos = _finish_grad(pos, gpos) if gpos is not None else None
+        return dp, dcls, dpos
+
+
+def vit_embed(patches, cls, pos):
+    """bf16 [N][T][D] tokens = cat(cls, patches) + pos for fp32 ``cls`` [1,1,D] / ``pos`` [1,T,D]."""
+    return _VitEmbed.apply(patches, cls, pos)
+
+
 def layer_norm(x, weight, bias, eps):
     """Native LayerNorm over the last dim (bf16 out, fp32 affine parameters)."""
     return _LayerNorm.apply(x, weight, bias, eps)

@@ -152,3 +152,32 @@ def test_attention_fwd_bwd(B, T, H):
             assert float(dq[:, i].float().abs().max()) < 1e-4, name
         else:
             assert rel_err(dq[:, i], dr[:, i]) < 4e-2, name
+
+
+def test_vit_native_matches_cpu_fp32():
+    """The GPU ViT step -- native token embedding (class token + position embedding in one pass,
+    fixed-order batch sums in backward) and the class-token-only final LayerNorm -- against the same
+    module's stock fp32 CPU path (torch.cat, broadcast add, full-sequence LayerNorm)."""
+    import copy
+    from mi355x_dp.models.vit import VisionTransformer
+    torch.manual_seed(0)
+    m = VisionTransformer(image_size=64, patch_size=16, num_layers=2, num_heads=1, hidden_dim=64, mlp_dim=128,
+                          num_classes=10)
+    with torch.no_grad():  # the zero-initialised head / class token would make the check trivial
+        m.heads.head.weight.normal_(std=0.2)
+        m.class_token.normal_(std=0.5)
+    mc = copy.deepcopy(m)
+    mg = m.cuda()
+    x = torch.randn(6, 3, 64, 64)
+    y = torch.arange(6) % 10
+    out_g = mg(x.cuda())
+    out_c = mc(x)
+    assert rel_err(out_g.float().cpu(), out_c) < 5e-2
+    F.cross_entropy(out_g.float(), y.cuda()).backward()
+    F.cross_entropy(out_c, y).backward()
+    for name in ("class_token", "encoder.pos_embedding", "conv_proj.weight", "conv_proj.bias", "encoder.ln.weight",
+                 "encoder.ln.bias", "heads.head.weight"):
+        gg = mg.get_parameter(name).grad
+        gc = mc.get_parameter(name).grad
+        assert gg is not None, name
+        assert rel_err(gg.float().cpu(), gc) < 8e-2, (name, rel_err(gg.float().cpu(), gc))
