@@ -332,6 +332,37 @@ __global__ __launch_bounds__(256) void vit_embed_fwd_kernel(const bf16_t* __rest
   *(uint4*)(out + e) = pack8(f);
 }
 
+// Patchify for a stride = kernel = p patch embedding: x NHWC [N][H][W][Cs] bf16 -> out [N * (H/p) *
+// (W/p)][p * p * C] bf16, row = patch, columns in (r, s, c) order -- the flat engine's conv weight
+// layout [K][R][S][C] -- for the C <= Cs real channels.  The patch embedding is then one plain GEMM
+// with K = p * p * C (768 for ViT-B/16) instead of an 8-channel-padded implicit-GEMM conv (2048).
+// One thread per 16-byte output chunk (8 columns, from up to 4 input pixels).
+__global__ __launch_bounds__(256) void vit_patchify_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
+                                                           int64_t chunks, int H, int W, int Cs, int C, int p,
+                                                           int Qn, int PQ) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= chunks) return;
+  const int row_len = p * p * C;
+  const int64_t e0 = i * 8;
+  const int64_t patch = e0 / row_len;
+  const int col0 = (int)(e0 - patch * row_len);
+  const int n = (int)(patch / PQ), pq = (int)(patch - (int64_t)n * PQ);
+  const int py = pq / Qn, px = pq - (pq / Qn) * Qn;
+  const bf16_t* img = x + (size_t)n * H * W * Cs;
+  bf16_t v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int col = col0 + q;
+    const int pix = col / C, c = col - pix * C;
+    const int r = pix / p, sx = pix - r * p;
+    v[q] = img[((size_t)(py * p + r) * W + (px * p + sx)) * Cs + c];
+  }
+  uint4 o;
+  o.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16); o.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+  o.z = (uint32_t)v[4] | ((uint32_t)v[5] << 16); o.w = (uint32_t)v[6] | ((uint32_t)v[7] << 16);
+  *(uint4*)(out + e0) = o;
+}
+
 // backward, pass 1: dpatches[n][p] = dout[n][1 + p] (the patch conv's dense output gradient) and
 // per image-group partial sums part[g][t * D + c] = sum over the group's images of dout[n][t][c]
 // (fixed order).  Block (x, g): 256 threads x 8 channels of the T * D positions, images
@@ -547,6 +578,15 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
   }
 #undef MI_LN_BWD
   if (rep) hipLaunchKernelGGL(ln_rep_reduce_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, rep, R, D, dw, db);
+  return (int)hipGetLastError();
+}
+
+MI_API int mi_vit_patchify(const void* x, void* out, int N, int H, int W, int Cs, int C, int p, hipStream_t st) {
+  if (p <= 0 || H % p || W % p || C <= 0 || C > Cs || (p * p * C) % 8 != 0) return (int)hipErrorInvalidValue;
+  const int Pn = H / p, Qn = W / p;
+  const int64_t chunks = (int64_t)N * Pn * Qn * p * p * C / 8;
+  hipLaunchKernelGGL(vit_patchify_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, st, (const bf16_t*)x,
+                     (bf16_t*)out, chunks, H, W, Cs, C, p, Qn, Pn * Qn);
   return (int)hipGetLastError();
 }
 

@@ -144,6 +144,8 @@ class VisionTransformer(nn.Module):
 
     def _process_input(self, x):
         n = x.shape[0]
+        if _NATIVE_EMBED and Tm.patch_embed_ok(x, self.conv_proj):
+            return Tm.patch_embed(x, self.conv_proj)  # patchify + one plain GEMM: [N, h*w, D]
         x = self.conv_proj(x)                 # [N, D, h, w]  (channels_last on the GPU path)
         x = x.permute(0, 2, 3, 1).reshape(n, -1, self.hidden_dim)  # NHWC storage: a free view
         return x

@@ -76,6 +76,7 @@ signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)
 signature("mi_layernorm_fwd", P, P, P, P, P, P, I, I, F, P)
 signature("mi_layernorm_bwd", P, P, P, P, P, P, P, P, P, I, I, P)
 signature("mi_colsum_bf16", P, P, I, I, I, P)
+signature("mi_vit_patchify", P, P, I, I, I, I, I, I, P)
 signature("mi_vit_embed_fwd", P, P, P, P, I, I, I, P)
 signature("mi_vit_embed_bwd_part_floats", I, I, I, restype=L)
 signature("mi_vit_embed_bwd", P, P, P, P, P, I, I, I, P)

@@ -295,6 +295,67 @@ class _LayerNorm(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _PatchEmbed(torch.autograd.Function):
+    """Stride = kernel = p patch embedding as patchify + one plain GEMM: the NHWC input's real
+    channels C are gathered into [patches][p * p * C] rows in (r, s, c) order -- the flat engine's
+    [K][R][S][C] conv weight layout, so the weight and its gradient are used as [K][p * p * C]
+    matrices in place -- instead of the 8-channel-padded implicit-GEMM conv (K = 768 instead of 2048
+    for ViT-B/16).  Returns [N][patches][K] bf16; no input gradient (images)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N, Cs, H, W = x.shape
+        K, C, R, S = weight.shape
+        Kd = R * S * C
+        rows = N * (H // R) * (W // S)
+        st = stream_of(x)
+        xp = torch.empty((rows, Kd), dtype=BF16, device=x.device)
+        _lib.call("mi_vit_patchify", ptr(x), ptr(xp), N, H, W, Cs, C, R, st)
+        w2 = weight_bf16(weight).permute(0, 2, 3, 1)
+        w2 = w2.reshape(K, Kd) if w2.is_contiguous() else w2.contiguous().reshape(K, Kd)
+        y = torch.empty((rows, K), dtype=BF16, device=x.device)
+        _lib.call("mi_gemm_nt", ptr(xp), ptr(w2), ptr(y), ptr(bias), ptr(None), rows, K, Kd, Kd, Kd, K, 0, 0, st)
+        ctx.save_for_backward(xp)
+        ctx.params = (weight, bias)
+        return y.view(N, rows // N, K)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xp,) = ctx.saved_tensors
+        weight, bias = ctx.params
+        rows, Kd = xp.shape
+        K = weight.shape[0]
+        dy2 = dy.reshape(rows, K).to(BF16).contiguous()
+        st = stream_of(dy2)
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            g = _grad_buffer(weight)
+            g2 = g.permute(0, 2, 3, 1)  # [K][R][S][C]: contiguous in the kernel layout
+            tmp = None if g2.is_contiguous() else torch.zeros(g2.shape, dtype=F32, device=g.device)
+            _lib.call("mi_gemm_tn", ptr(dy2), ptr(xp), ptr(g2 if tmp is None else tmp), K, Kd, rows, K, Kd, Kd, st)
+            if tmp is not None:
+                g2.add_(tmp)
+            dw = _finish_grad(weight, g)
+        if bias is not None and ctx.needs_input_grad[2]:
+            gb = _grad_buffer(bias)
+            _lib.call("mi_colsum_bf16", ptr(dy2), ptr(gb), rows, K, K, st)
+            db = _finish_grad(bias, gb)
+        return None, dw, db
+
+
+def patch_embed_ok(x, conv) -> bool:
+    K, C, R, S = conv.weight.shape
+    return (x.is_cuda and x.dtype == BF16 and x.is_contiguous(memory_format=torch.channels_last)
+            and tuple(conv.stride) == (R, S) and R == S and tuple(conv.padding) == (0, 0) and conv.groups == 1
+            and C <= x.shape[1] and (R * S * C) % 8 == 0 and K % 8 == 0 and x.shape[2] % R == 0
+            and x.shape[3] % S == 0 and conv.weight.dtype == torch.float32)
+
+
+def patch_embed(x, conv):
+    """[N][patches][K] bf16 embedding of the NHWC bf16 image batch ``x`` by the stride-p conv ``conv``."""
+    return _PatchEmbed.apply(x, conv.weight, conv.bias)
+
+
 class _VitEmbed(torch.autograd.Function):
     """[class token ; patch embeddings] + position embedding as one native pass
     (``mi_vit_embed_fwd``); backward: the patches' dense gradient plus the fixed-order batch sums
