@@ -1282,9 +1282,40 @@ __global__ void wtrans_multi_kernel(const bf16_t* __restrict__ w, bf16_t* __rest
   const int ky = r0 % nkb;
   const int tap = r0 / nkb;
   const int k0 = ky * 64, c0 = cx * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const bf16_t* src = w + d.src;
   bf16_t* dst = wt + d.dst;
+  if ((d.C & 7) == 0 && (d.K & 7) == 0) {
+    // 16-byte accesses both ways (every row of both layouts is a whole number of 8-element
+    // chunks): thread -> (row, chunk) pairs; the transposed chunk is gathered from 8 LDS rows
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
+      const int k = k0 + r, c = c0 + 8 * ch;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (k < d.K && c < d.C) v = *(const uint4*)(src + ((size_t)k * d.RS + tap) * d.C + c);
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[r][8 * ch + 2 * j] = (bf16_t)(u[j] & 0xffffu);
+        t[r][8 * ch + 2 * j + 1] = (bf16_t)(u[j] >> 16);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;  // r: output row (c), ch: k chunk
+      const int c = c0 + r, k = k0 + 8 * ch;
+      if (c < d.C && k < d.K) {
+        uint32_t u[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          u[j] = (uint32_t)t[8 * ch + 2 * j][r] | ((uint32_t)t[8 * ch + 2 * j + 1][r] << 16);
+        *(uint4*)(dst + ((size_t)c * d.RS + tap) * d.K + k) = make_uint4(u[0], u[1], u[2], u[3]);
+      }
+    }
+    return;
+  }
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int k = k0 + r, c = c0 + tx;
     t[r][tx] = (k < d.K && c < d.C) ? src[((size_t)k * d.RS + tap) * d.C + c] : (bf16_t)0;

@@ -706,3 +706,27 @@ def test_block_output_mask_bits(shape):
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx2)
     assert torch.equal(sl1[:rows], sl2[:rows])
+
+
+@pytest.mark.gpu
+def test_flat_engine_transposed_weight_copies():
+    """mi_conv_wtrans_multi (the flat engine's dgrad operands, refreshed once per optimizer step):
+    every conv's [C][R][S][K] copy and every linear's [in][out] copy equal the transpose of the bf16
+    compute copy -- 16-byte path (C, K % 8 == 0) and the scalar path (a 3-channel conv) alike."""
+    import torch.nn as nn
+    from mi355x_dp.models.layers import Conv2d, Linear
+    from mi355x_dp.parallel import DataParallel
+    torch.manual_seed(0)
+    m = nn.Sequential(Conv2d(3, 64, 7, 2, 3, bias=False), Conv2d(64, 200, 1, bias=False),
+                      Conv2d(200, 136, 3, 1, 1, bias=False), nn.Flatten(), Linear(136, 72)).cuda()
+    DataParallel(m)
+    n = 0
+    for p in m.parameters():
+        wt = getattr(p, "_mi_bf16_t", None)
+        if wt is None:
+            continue
+        w16 = p._mi_bf16
+        ref = w16.permute(1, 2, 3, 0) if p.dim() == 4 else w16.t()
+        assert torch.equal(wt.reshape(ref.shape).float(), ref.float()), tuple(p.shape)
+        n += 1
+    assert n >= 3
