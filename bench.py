@@ -348,9 +348,13 @@ def main(argv=None):
         # `smddp` c10d backend (csrc/comm/smddp_backend.cpp, the reference's backend name,
         # gpu.py:17-23 / nb2:781,1223) -- so every multi-GPU run also exercises the product path,
         # while the headline keeps the path most likely to succeed
-        if cuda:
-            torch.cuda.empty_cache()
-        smddp_job = run_child_bench(world, args, "smddp")
+        if cuda and world > torch.cuda.device_count():
+            # ranks sharing a device (one-GPU rehearsals): RCCL refuses two ranks on one GPU
+            smddp_job = "skipped: ranks share a device"
+        else:
+            if cuda:
+                torch.cuda.empty_cache()
+            smddp_job = run_child_bench(world, args, "smddp")
     ipc_probe = None
     if (rank == 0 and world > 1 and cuda and world <= torch.cuda.device_count()
             and os.environ.get("MI355X_DP_BENCH_IPC_PROBE", "1") == "1"):
