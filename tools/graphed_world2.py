@@ -23,6 +23,11 @@ import smdistributed.dataparallel.torch.torch_smddp  # noqa: E402,F401  (install
 dist.init_process_group(backend="smddp")
 r, w = dist.get_rank(), dist.get_world_size()
 STEPS = int(os.environ.get("GRAPHED_STEPS", "8"))
+# per-rank batch / image size (default: the reference's 32 at 32x32).  The gate-overlap check of the
+# test runs a larger shape: at the reference shape the replayed backward (~0.9 ms) can finish before
+# the host has even returned from launching the ~150-node graph, so no gate could open under it.
+BATCH = int(os.environ.get("GRAPHED_BATCH", "32"))
+SIZE = int(os.environ.get("GRAPHED_SIZE", "32"))
 
 
 def run(mode):
@@ -38,8 +43,8 @@ def run(mode):
     g = torch.Generator().manual_seed(11 + r)  # each rank its own shard of data
     losses = []
     for _ in range(STEPS):
-        x = torch.randn(32, 3, 32, 32, generator=g).cuda()
-        y = torch.randint(0, 1000, (32,), generator=g).cuda()
+        x = torch.randn(BATCH, 3, SIZE, SIZE, generator=g).cuda()
+        y = torch.randint(0, 1000, (BATCH,), generator=g).cuda()
         opt.zero_grad()
         loss = crit(ddp(x), y)
         loss.backward()
