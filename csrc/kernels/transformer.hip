@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ rstd_in,
                                                        const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
                                                        float* __restrict__ dw, float* __restrict__ db, int M, int D,
-                                                       float* __restrict__ rep, int R, int* __restrict__ cnt) {
+                                                       float* __restrict__ rep, int R) {
   extern __shared__ float red[];  // [8 half-waves][D]
   constexpr int RW = MI_LN16_RW;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5, hl = lane & 31;
@@ -301,28 +301,6 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const bf16_t* __restrict_
       atomicAdd(dst + col, t);
     }
   }
-  if (!rep || !cnt) return;
-  // the replica reduction in the last-arriving block instead of a second launch: this block's
-  // agent-scope atomics have completed (vmcnt counts them) before it counts its arrival; the last
-  // block reads the replicas with agent-scope loads, sums them in replica order into dw / db
-  // (deterministic, as ln_rep_reduce_kernel) and re-zeroes them and the counter
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(cnt, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  for (int i = threadIdx.x; i < 2 * D; i += 256) {
-    const int pass = i / D, col = i - pass * D;
-    float t = 0.f;
-    for (int r = 0; r < R; ++r) {
-      float* a = rep + ((size_t)r * 2 + pass) * D + col;
-      t += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    (pass ? db : dw)[col] += t;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- ViT token embedding
@@ -489,8 +467,7 @@ static float* ln_rep_workspace(int D, hipStream_t st) {
       return nullptr;  // -> the replica-free parameter-gradient path
     }
     float* p = nullptr;
-    // + one int arrival counter after the replicas (ln_bwd16_kernel's in-kernel replica reduction)
-    const size_t bytes = sizeof(float) * LN_REPLICAS * 2 * (size_t)D + 256;
+    const size_t bytes = sizeof(float) * LN_REPLICAS * 2 * (size_t)D;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
     if (hipMemset(p, 0, bytes) != hipSuccess) return nullptr;
     (void)hipDeviceSynchronize();  // the zeroing is complete before any stream uses the replicas
@@ -582,11 +559,13 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
     hipLaunchKernelGGL(ln_bwd16_kernel<V>,                                                               \
                        dim3(min(cdiv(M, 8 * MI_LN16_RW), cap16((const void*)ln_bwd16_kernel<V>))), dim3(256), \
                        lds16, st, (const bf16_t*)dy, (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres,    \
-                       (bf16_t*)dx, dw, db, M, D, rep, R, cnt);                                          \
+                       (bf16_t*)dx, dw, db, M, D, rep, R);                                               \
     break;
-    int* cnt = rep ? (int*)(rep + (size_t)LN_REPLICAS * 2 * D) : nullptr;
     switch (nvec) { MI_LN_BWD16_CASE(1) MI_LN_BWD16_CASE(3) }
 #undef MI_LN_BWD16_CASE
+    // a separate reduce: in the last-arriving block the same 2 x D x 32 replica reads ran ~10x
+    // longer than this 6-block launch (ViT-B/16 -7 %, profiles/raw/r4_l38_*)
+    if (rep) hipLaunchKernelGGL(ln_rep_reduce_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, rep, R, D, dw, db);
     return (int)hipGetLastError();
   }
 #define MI_LN_BWD(V)                                                                                    \

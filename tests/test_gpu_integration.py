@@ -448,19 +448,23 @@ def test_smddp_ipc_mesh_collectives_multi_rank(world):
 
 def test_graphed_engine_two_ranks_gated_buckets():
     """The graphed engine at world 2: the reference loop (ResNet-18,
-    1000-class head, stock SGD; batch 128 at 128x128, see below) through the engine-backed DDP, graphed
+    1000-class head, stock SGD; batch 256 at 224x224, see below) through the engine-backed DDP, graphed
     vs eager on IPC-only smddp (2 ranks sharing cuda:0).
     Graphed == eager bit for bit on every rank (losses and flat fp32 parameters), replicas
     identical, and every bucket's collective released by its gate before the replayed backward
     ended (the first bucket well before)."""
     import json
-    # batch 128 at 128x128 (graphed up to 8M input elements here): the replayed backward must outlast
-    # the host's graph launch plus the gate launches (~1.5-2 ms of host time) for a gate to open under
-    # it -- at the reference's batch 32 @ 32x32 the whole backward (~0.9 ms) ends first, and at 128 @
-    # 64x64 (~1.3 ms) still did (tools/graphed_world2.py)
+    # batch 256 at 224x224 (graphed here up to 64M input elements): the replayed backward must outlast
+    # the host side of the replay -- hipGraphLaunch of the ~150-node graph returns only after ~2 ms,
+    # and the gates are enqueued behind it -- for a gate to open under it.  At the reference's batch
+    # 32 @ 32x32 (0.9 ms), 128 @ 64x64 (1.3 ms) and 128 @ 128x128 (1.9 ms) the whole backward ended
+    # first (tools/graphed_world2.py)
     env = {**os.environ, "PYTHONPATH": ROOT, "MI355X_DP_SMDDP_IPC_ONLY": "1", "MI355X_DP_SMDDP_DEVICE": "0",
-           "MI355X_DP_SMDDP_IPC_MB": "4", "MI355X_DP_SMDDP_TERMINATE_TRACE": "1", "GRAPHED_BATCH": "128",
-           "GRAPHED_SIZE": "128", "MI355X_DP_ENGINE_GRAPH_MAX_NUMEL": str(1 << 23)}
+           "MI355X_DP_SMDDP_IPC_MB": "4", "MI355X_DP_SMDDP_TERMINATE_TRACE": "1", "GRAPHED_BATCH": "256",
+           "GRAPHED_SIZE": "224", "MI355X_DP_ENGINE_GRAPH_MAX_NUMEL": str(1 << 26),
+           # ranks sharing a GPU otherwise get ONE hardware queue each (utils/hwqueues.py SHARED):
+           # every stream of a rank then runs in order on it and no gate can open under the replay
+           "GPU_MAX_HW_QUEUES": "6"}
     r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2",
                         os.path.join(ROOT, "tools", "graphed_world2.py")], cwd=ROOT, capture_output=True, text=True,
                        timeout=240, env=env)

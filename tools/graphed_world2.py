@@ -66,6 +66,7 @@ print(json.dumps({"rank": r, "world": w, "losses_graphed": loss_g, "losses_eager
                   "replays_eager": replays_e, "gated": gated, "graphed_equals_eager": bool(torch.equal(flat_g,
                                                                                            eng_e.flat.data)),
                   "replicas_identical": bool(same), "buckets": len(eng_g.buckets),
-                  "gate_open_ms": trace[0] if trace else None, "replay_end_ms": trace[1] if trace else None}),
+                  "gate_open_ms": trace[0] if trace else None, "replay_end_ms": trace[1] if trace else None,
+                  "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}),
       flush=True)
 dist.destroy_process_group()
