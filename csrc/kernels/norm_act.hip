@@ -84,17 +84,47 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const bf16_t* __restrict__
 #endif
 constexpr int FIN_T = MI_FIN_T, FIN_G = FIN_T / 64;
 
+// a += sum of p[2 i * C + c], b += sum of p[(2 i + 1) * C + c] over rows i = i0, i0 + step, .. < i1,
+// in row order (bitwise the plain loop's result), with FIN_U rows' loads in flight at once: the
+// one-row-per-iteration loops waited a full memory round trip per row (s_waitcnt vmcnt(0) each
+// iteration) -- 8 L2 trips in a split, 3+ memory trips (agent-scope hand-off loads) in the final
+// stage, ~9 us of the ~10 us a finalize launch took.  ATOMIC: agent-scope loads (hand-off rows).
+constexpr int FIN_U = 8;
+template <bool ATOMIC>
+__device__ __forceinline__ void sum_rows(const float* __restrict__ p, int i0, int i1, int step, int C, int c,
+                                         double& a, double& b) {
+  for (int i = i0; i < i1; i += FIN_U * step) {
+    float va[FIN_U], vb[FIN_U];
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      const int r = i + u * step;
+      va[u] = 0.f;
+      vb[u] = 0.f;
+      if (r < i1) {
+        const float* q = p + (size_t)(2 * r) * C + c;
+        if constexpr (ATOMIC) {
+          va[u] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vb[u] = __hip_atomic_load(q + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          va[u] = q[0];
+          vb[u] = q[C];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {  // + 0.0 past the end: exact, the order is the plain loop's
+      a += va[u];
+      b += vb[u];
+    }
+  }
+}
+
 __device__ __forceinline__ bool slab_reduce64(const float* __restrict__ part, int nblk, int C, double& s, double& q) {
   __shared__ double red[2][FIN_G][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int i = rg; i < nblk; i += FIN_G) {
-      a += part[(size_t)(2 * i) * C + c];
-      b += part[(size_t)(2 * i + 1) * C + c];
-    }
-  }
+  if (c < C) sum_rows<false>(part, rg, nblk, FIN_G, C, c, a, b);
   red[0][rg][cl] = a;
   red[1][rg][cl] = b;
   __syncthreads();
@@ -113,12 +143,7 @@ __global__ __launch_bounds__(FIN_T) void slab_split_kernel(const float* __restri
   const int c = blockIdx.x * 64 + cl;
   const int b0 = blockIdx.y * rows_per, b1 = min(nblk, b0 + rows_per);
   double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int i = b0 + rg; i < b1; i += FIN_G) {
-      a += part[(size_t)(2 * i) * C + c];
-      b += part[(size_t)(2 * i + 1) * C + c];
-    }
-  }
+  if (c < C) sum_rows<false>(part, b0 + rg, b1, FIN_G, C, c, a, b);
   red[0][rg][cl] = a;
   red[1][rg][cl] = b;
   __syncthreads();
@@ -372,12 +397,7 @@ __global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __re
   const int c = blockIdx.x * 64 + cl;
   const int b0 = blockIdx.y * rows_per, b1 = min(nblk, b0 + rows_per);
   double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int i = b0 + rg; i < b1; i += FIN_G) {
-      a += part[(size_t)(2 * i) * C + c];
-      b += part[(size_t)(2 * i + 1) * C + c];
-    }
-  }
+  if (c < C) sum_rows<false>(part, b0 + rg, b1, FIN_G, C, c, a, b);
   red[0][rg][cl] = a;
   red[1][rg][cl] = b;
   __syncthreads();
@@ -419,12 +439,7 @@ __global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __re
   }
   // second stage over the S split rows (other blocks' rows: sc1 loads, see above)
   double s2 = 0.0, q2 = 0.0;
-  if (c < C) {
-    for (int i = rg; i < (int)gridDim.y; i += FIN_G) {
-      s2 += __hip_atomic_load(out + (size_t)(2 * i) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      q2 += __hip_atomic_load(out + (size_t)(2 * i + 1) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (c < C) sum_rows<true>(out, rg, (int)gridDim.y, FIN_G, C, c, s2, q2);
   __syncthreads();
   red[0][rg][cl] = s2;
   red[1][rg][cl] = q2;

@@ -388,9 +388,13 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float4* __
   constexpr int NV = STEM_WELEMS / 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (pos < NV)
-    for (int b = grp; b < rows; b += SWR_G) {
-      const float4 v = ws[(size_t)b * NV + pos];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    for (int b = grp; b < rows; b += 4 * SWR_G) {  // 4 rows' loads in flight, summed in row order
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = b + u * SWR_G < rows ? ws[(size_t)(b + u * SWR_G) * NV + pos] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
   red[grp][pl] = s;
   __syncthreads();
@@ -418,7 +422,13 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_to_kernel(const float* 
   const int o = (k * NTAP + tap) * 8 + c;
   float s = 0.f;
   if (pos < ne)
-    for (int b = grp; b < rows; b += SWR_G) s += ws[(size_t)b * STEM_WELEMS + o];
+    for (int b = grp; b < rows; b += 8 * SWR_G) {  // 8 rows' loads in flight, summed in row order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = b + u * SWR_G < rows ? ws[(size_t)(b + u * SWR_G) * STEM_WELEMS + o] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
   red[grp][pl] = s;
   __syncthreads();
   if (grp != 0 || pos >= ne) return;

@@ -375,13 +375,19 @@ __global__ __launch_bounds__(256) void vit_embed_bwd_kernel(const bf16_t* __rest
   const int t = (int)(r / D);
   const int n0 = blockIdx.y * per_g, n1 = min(N, n0 + per_g);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int n = n0; n < n1; ++n) {
-    const uint4 v = *(const uint4*)(dout + n * TD + r);
-    float f[8];
-    unpack8(v, f);
+  for (int n = n0; n < n1; n += 4) {  // 4 images' loads in flight, summed in image order
+    uint4 v[4];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s[q] += f[q];
-    if (t > 0) *(uint4*)(dpatches + n * (TD - D) + (r - D)) = v;
+    for (int u = 0; u < 4; ++u) v[u] = n + u < n1 ? *(const uint4*)(dout + (n + u) * TD + r) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (n + u >= n1) break;
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += f[q];
+      if (t > 0) *(uint4*)(dpatches + (n + u) * (TD - D) + (r - D)) = v[u];
+    }
   }
   float* o = part + (size_t)blockIdx.y * TD + r;
   *(float4*)o = make_float4(s[0], s[1], s[2], s[3]);
@@ -396,7 +402,13 @@ __global__ __launch_bounds__(256) void vit_embed_bwd_sum_kernel(const float* __r
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= TD) return;
   float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(size_t)g * TD + r];
+  for (int g = 0; g < G; g += 8) {  // 8 partial rows' loads in flight, summed in order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = g + u < G ? part[(size_t)(g + u) * TD + r] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
   if (dpos) dpos[r] += s;
   if (dcls && r < D) dcls[r] += s;
 }
