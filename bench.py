@@ -424,7 +424,7 @@ def _child_env():
     return env
 
 
-def run_child_bench(world: int, args, backend: str, timeout_s: int = 300):
+def run_child_bench(world: int, args, backend: str, timeout_s: int = 150):
     """``bench.py`` again as a fresh N-rank job (native launcher) through ``backend``, a few steps of
     the same configuration, started by rank 0 after the benchmark finished (a failure cannot cost
     the measurement).  Returns its img/s, ranks seen, backend, replica check and step time."""
@@ -465,7 +465,7 @@ def run_child_bench(world: int, args, backend: str, timeout_s: int = 300):
     return f"failed: rc={proc.returncode}: {(err or out)[-400:]}"
 
 
-def run_ipc_probe(world: int, timeout_s: int = 180):
+def run_ipc_probe(world: int, timeout_s: int = 120):
     """The smddp IPC-vs-RCCL path table of this node (tools/ipc_probe.py), as a separate N-rank job
     started by rank 0 after the benchmark finished: a probe failure cannot cost the measurement."""
     from mi355x_dp.launch import NATIVE_LAUNCHER, compat_pythonpath, free_port
