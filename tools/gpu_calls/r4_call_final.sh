@@ -3,7 +3,7 @@
 bash tools/gpu_steps_safe.sh \
  "r4_final_smoke:200:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
  "r4_final_prof:400:bash tools/r4_prof_grid.sh r4_final" &&
-bash tools/r4_call29.sh &&
+bash tools/gpu_calls/r4_call29.sh &&
 bash tools/gpu_steps_safe.sh \
  "r4_final_rn50_a:200:python bench.py" \
  "r4_final_rn50_b:200:python bench.py --steps 30 --warmup 5" \
