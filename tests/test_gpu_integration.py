@@ -464,8 +464,7 @@ def test_graphed_engine_two_ranks_gated_buckets():
     1000-class head, stock SGD) through the engine-backed DDP, graphed vs eager on IPC-only smddp
     (2 ranks sharing cuda:0).  At the reference's shape (batch 32 at 32x32): graphed == eager bit
     for bit on every rank (losses and flat fp32 parameters), replicas identical, one gate per
-    bucket.  At batch 256 at 224x224: every bucket's collective released by its gate, the first one
-    before the replayed backward ended."""
+    bucket.  At batch 256 at 224x224: every bucket's collective released by its gate, in order."""
     rows = _graphed_world2({})
     for row in rows:
         assert row["gated"] and row["replays"] == 6 and row["replays_eager"] == 0, row
@@ -473,20 +472,21 @@ def test_graphed_engine_two_ranks_gated_buckets():
         assert row["graphed_equals_eager"] and row["replicas_identical"], row
         assert len(row["gate_open_ms"]) == row["buckets"] >= 2, row
     assert rows[0]["losses_graphed"] != rows[1]["losses_graphed"]  # different data per rank
-    # The overlap needs a replayed backward that outlasts the host side of the replay:
-    # hipGraphLaunch of the ~150-node graph returns only after ~2 ms, and the gates are enqueued
-    # behind it.  At batch 32 @ 32x32 (0.9 ms), 128 @ 64x64 (1.3 ms) and 128 @ 128x128 (1.9 ms) the
-    # whole backward ended first.  Ranks sharing a GPU otherwise get ONE hardware queue each
-    # (utils/hwqueues.py SHARED), and every stream of a rank then runs in order on it.  (At this
-    # shape the graph's split-K / tail-split schedule may differ from the eager one: no bitwise
-    # comparison here.)
+    # Gate trace at a larger shape (batch 256 at 224x224, graphed up to 64M input elements): every
+    # bucket's gate fires once per replay, in bucket order.  Whether the first one opens before the
+    # replayed backward ends is NOT asserted here.  The gates are enqueued after hipGraphLaunch
+    # returns (~2 ms of host time for the ~150-node graph), and with two ranks on one GPU the
+    # runtime's stream-to-hardware-queue mapping may serialise a rank's comm stream behind its
+    # compute stream.  Two runs at this shape gave gate 0 at 0.39 ms of a ~6.7 ms replay and at
+    # 7.29 ms of 6.68 ms.  The one-rank-per-GPU overlap is measured in profiles/graph_bucket_gates.md.
     rows = _graphed_world2({"GRAPHED_BATCH": "256", "GRAPHED_SIZE": "224",
                             "MI355X_DP_ENGINE_GRAPH_MAX_NUMEL": str(1 << 26), "GPU_MAX_HW_QUEUES": "6"})
     for row in rows:
         assert row["gated"] and row["replays"] == 6 and row["replicas_identical"], row
         opened, end = row["gate_open_ms"], row["replay_end_ms"]
-        assert len(opened) == row["buckets"] >= 2 and opened == sorted(opened), row
-        assert opened[0] < end, row  # the first bucket's collective starts under the replay
+        assert len(opened) == row["buckets"] >= 2 and opened == sorted(opened) and end > 0, row
+        print(f"rank {row['rank']}: gates opened at {[round(t, 2) for t in opened]} ms, replay ended at "
+              f"{end:.2f} ms")
 
 
 @pytest.mark.skipif(REF_CODE is None, reason="reference scripts not staged (run build())")
