@@ -182,12 +182,17 @@ INNER_BITS = os.environ.get("MI355X_DP_INNER_BITS", "1") != "0"  # the same for 
 OUT_BITS_MIN = 1 << 22
 
 
+def _bits_ok(c):
+    """emit the mask bytes for BN output ``c``: large enough, and whole bytes per pixel"""
+    return OUT_BITS and c.numel() >= OUT_BITS_MIN and c.shape[1] % 8 == 0
+
+
 def _out_apply(c, res, sc, sh, rsc=None, rsh=None):
     """block output y = relu(c * sc + sh + res') (res' = res, or res * rsc + rsh for a projection
     shortcut's raw conv output) -> (y, bits); bits is None when the mask is not emitted."""
     N, C, H, W = c.shape
     y = torch.empty_like(c, memory_format=CL)
-    if OUT_BITS and N * H * W * C >= OUT_BITS_MIN:
+    if _bits_ok(c):
         bits = torch.empty((N, H, W, C // 8), dtype=torch.uint8, device=c.device)
         _lib.call("mi_bn_apply_bits", ptr(c), ptr(res), ptr(y), ptr(bits), N * H * W, C, ptr(sc), ptr(sh), ptr(rsc),
                   ptr(rsh), stream_of(c))
@@ -327,7 +332,7 @@ class _ResBlock(torch.autograd.Function):
                 elif has_ds:
                     cd, slabd, rowsd = _conv_fwd_stats(x, convs[-1])
                     y, m, inv, md, isd, out_bits = _bn_fwd_dual(c, slab, rows, bns[i], cd, slabd, rowsd, bns[-1])
-                elif OUT_BITS and c.numel() >= OUT_BITS_MIN:
+                elif _bits_ok(c):
                     _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bns[i], relu=True, apply=False)
                     y, out_bits = _out_apply(c, x, sc, sh)
                 else:
@@ -340,7 +345,7 @@ class _ResBlock(torch.autograd.Function):
                 nol = (sc, sh)
                 NOL_USED[0] += 1
             else:
-                if OUT_BITS and INNER_BITS and c.numel() >= OUT_BITS_MIN:
+                if INNER_BITS and _bits_ok(c):
                     # inner BN: y for the next conv (forward, weight gradient) plus its ReLU mask bytes
                     # for that conv's data-gradient epilogue
                     _, m, inv, sc, sh = _bn_fwd(c, slab, rows, bns[i], relu=True, apply=False)

@@ -49,3 +49,14 @@ def test_package_installs(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=str(tmp_path),
                        env={**os.environ, "PYTHONPATH": str(target)})
     assert r.returncode == 0 and r.stdout.split() == ["True", "True", "True"], r.stdout + r.stderr
+
+
+def test_mask_bytes_gate_needs_whole_bytes():
+    """ReLU mask bytes (one byte per 8 channels) are only emitted for channel counts divisible by 8
+    and tensors above the size threshold; anything else keeps the bf16 mask path."""
+    import torch
+    from mi355x_dp.ops import resblock as rb
+    big = 1 << 22
+    assert rb._bits_ok(torch.empty((big // 64, 64, 1, 1), device="meta")) == rb.OUT_BITS
+    assert not rb._bits_ok(torch.empty((big // 12 + 1, 12, 1, 1), device="meta"))
+    assert not rb._bits_ok(torch.empty((2, 64, 8, 8), device="meta"))
