@@ -357,6 +357,7 @@ class SmddpBackend : public c10d::Backend {
   // sizes) or two-shot (reduce-scatter into the own slot + all-gather: 2/world of the chunk per
   // xGMI link) kernel; chunks pipeline through the two alternating slots on the comm stream
   void ipc_allreduce(at::Tensor& t, bool avg, hipStream_t s) {
+    ipc_capture_check();
     const int64_t n = t.numel(), per = (int64_t)(ipc_cap_ / 4);
     for (int64_t off = 0; off < n || (n == 0 && off == 0); off += per) {
       const int64_t cnt = std::min(per, n - off);
@@ -379,6 +380,7 @@ class SmddpBackend : public c10d::Backend {
   // IPC-only mode: any dtype / op through the generic one-shot kernel (op 3 = copy from root,
   // nbytes 0 = barrier), chunked like ipc_allreduce
   void ipc_generic(void* ptr, int64_t nbytes, int dtype, int op, int root, hipStream_t s) {
+    ipc_capture_check();
     const int64_t per = (int64_t)ipc_cap_;
     for (int64_t off = 0; off < nbytes || (nbytes == 0 && off == 0); off += per) {
       const int64_t cnt = std::min(per, nbytes - off);
@@ -401,6 +403,7 @@ class SmddpBackend : public c10d::Backend {
   // packs `cnt` elements of each rank's piece into its slot with one strided copy and pulls its own
   // piece from every peer's slot; chunked so world * cnt fits a slot
   void ipc_reduce_scatter(at::Tensor& out, at::Tensor& in, bool avg, hipStream_t s) {
+    ipc_capture_check();
     const int64_t S = out.numel();
     const size_t esz = in.element_size();
     const int dt = in.scalar_type() == at::kFloat ? 0 : 4;
@@ -425,6 +428,7 @@ class SmddpBackend : public c10d::Backend {
 
   // all-gather over the mesh (mi_ipc_all_gather): any dtype, chunked by the slot size
   void ipc_all_gather(at::Tensor& out, at::Tensor& in, hipStream_t s) {
+    ipc_capture_check();
     const int64_t nb = in.numel() * (int64_t)in.element_size();
     const int64_t per = (int64_t)ipc_cap_ & ~(int64_t)15;
     for (int64_t off = 0; off < nb || (nb == 0 && off == 0); off += per) {
@@ -471,6 +475,18 @@ class SmddpBackend : public c10d::Backend {
   // single rank in IPC-only mode (no RCCL): every collective is the identity
   bool solo() const { return ipc_only_ && size_ == 1; }
 
+  static bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+  }
+  // every IPC launch: the kernels' flag epochs and slot parity are chosen on the host per call, so
+  // a captured IPC collective would replay with stale epochs -- refuse it (the engine then keeps
+  // the collective outside the graph: parallel/step_graph.py)
+  void ipc_capture_check() const {
+    TORCH_CHECK(!capturing_, "smddp: an IPC collective cannot be captured into a HIP graph (host-side flag "
+                             "epochs); capture with the RCCL path (MI355X_DP_SMDDP_IPC=0)");
+  }
+
  public:
 
   const std::string getBackendName() const override { return "smddp"; }
@@ -485,15 +501,29 @@ class SmddpBackend : public c10d::Backend {
     // a ring of producer events: an event is re-recorded only after kReady later collectives, never
     // while the comm stream's wait on its previous record may still be pending
     hipEvent_t ready = ready_[ready_next_++ % kReady];
+    // Inside a HIP graph capture on the caller's stream (the engine captures its bucket collectives
+    // into the replayed backward, parallel/step_graph.py) the event record / wait below become the
+    // graph's fork edge onto the comm stream and Work::wait() its join; RCCL launches are captured
+    // as graph nodes.  Such work is never handed to the watchdog: its events are graph nodes that are
+    // not recorded until a replay, so polling them would only time out.
+    const bool capturing = stream_capturing(cur.stream());
+    TORCH_CHECK(!(capturing && blocking), "smddp: a blocking collective (barrier) cannot be captured");
     HIPCHECK(hipEventRecord(ready, cur.stream()));
     HIPCHECK(hipStreamWaitEvent(comm_stream_.stream(), ready, 0));
     for (auto& t : touched)
       c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(),
                                                                                        comm_stream_);
-    fn(comm_stream_.stream());
+    capturing_ = capturing;
+    try {
+      fn(comm_stream_.stream());
+    } catch (...) {
+      capturing_ = false;
+      throw;
+    }
+    capturing_ = false;
     TORCH_CHECK(err_->code.load() == 0, "smddp: communicator failed: ", err_->what);
     auto w = c10::make_intrusive<SmddpWork>(rank_, op, device_, comm_stream_, std::move(outputs), blocking, err_);
-    {
+    if (!capturing) {
       std::lock_guard<std::mutex> lk(mu_);
       pending_.push_back(w->done_);
     }
@@ -726,6 +756,9 @@ class SmddpBackend : public c10d::Backend {
     if (oneshot_bytes >= 0) ipc_oneshot_bytes_ = (size_t)oneshot_bytes;
   }
   int64_t comm_stream_handle() const { return (int64_t)(intptr_t)comm_stream_.stream(); }
+  // can every collective the engine issues be captured into a HIP graph?  (RCCL path, or a single
+  // IPC-only rank whose collectives are the identity; not while any size may take an IPC kernel)
+  bool capture_safe() const { return solo() || !(ipc_on_ && (ipc_only_ || ipc_threshold_ > 0)); }
 
  private:
   void watchdog_loop() {
@@ -790,6 +823,7 @@ class SmddpBackend : public c10d::Backend {
   bool abort_on_error_ = true;  // MI355X_DP_SMDDP_ABORT_ON_ERROR=0: record only (tests)
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
+  bool capturing_ = false;  // run() is issuing a collective into a HIP graph capture
 };
 
 static void stop_all_watchdogs() {
@@ -837,6 +871,8 @@ int64_t comm_stream(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smdd
 
 std::map<std::string, int64_t> ipc_info(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->ipc_info(); }
 
+bool capture_safe(const c10::intrusive_ptr<c10d::Backend>& b) { return as_smddp(b)->capture_safe(); }
+
 void set_ipc_paths(const c10::intrusive_ptr<c10d::Backend>& b, int64_t threshold_bytes, int64_t oneshot_bytes) {
   as_smddp(b)->set_ipc_paths(threshold_bytes, oneshot_bytes);
 }
@@ -858,6 +894,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("healthy", &smddp::healthy, pybind11::arg("backend"));
   m.def("comm_stream", &smddp::comm_stream, pybind11::arg("backend"));
   m.def("ipc_info", &smddp::ipc_info, pybind11::arg("backend"));
+  m.def("capture_safe", &smddp::capture_safe, pybind11::arg("backend"));
   m.def("set_ipc_paths", &smddp::set_ipc_paths, pybind11::arg("backend"), pybind11::arg("threshold_bytes"),
         pybind11::arg("oneshot_bytes"));
 }

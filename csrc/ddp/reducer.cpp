@@ -26,6 +26,9 @@
 //    collective per bucket).  The flat layout pads every bucket to a multiple of world x 64
 //    elements so the shards are equal and aligned.
 #include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hip/hip_runtime.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Types.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
@@ -34,7 +37,10 @@
 #include <chrono>
 #include <cmath>
 #include <tuple>
+#include <map>
 #include <mutex>
+#include <optional>
+#include <string>
 #include <vector>
 
 namespace mi_ddp {
@@ -151,8 +157,65 @@ class Reducer {
     reset();
   }
 
+  ~Reducer() {
+    for (auto* v : {&ev_ready_, &ev_end_})
+      for (hipEvent_t e : *v) hipEventDestroy(e);
+    if (ev_t0_) hipEventDestroy(ev_t0_);
+    if (ev_bwd_end_) hipEventDestroy(ev_bwd_end_);
+  }
+
+  // GPU-side timeline of the bucket collectives (host launch times are not
+  // overlap evidence).  Per step, relative to an event recorded on the current stream at reset()
+  // (the forward's start): `ready` = an event on the producing stream just before the bucket's
+  // collective is issued (its gradients -- and a bf16 cast -- are complete there), `end` = an event
+  // on a probe stream made to wait on the collective's Work (the collective's completion), and
+  // `bwd_end` = an event on the current stream when finish() starts (the compute stream has joined
+  // the weight-gradient stream there: the end of the backward's kernels).  Collectives are serial on
+  // the comm stream, so each one starts at max(its ready, the previous end).  Not recorded inside a
+  // graph capture.
+  void set_gpu_timing(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (on && !grad_.is_cuda()) return;
+    timing_ = on;
+    if (!on || !ev_ready_.empty()) return;
+    c10::hip::HIPGuardMasqueradingAsCUDA dg(grad_.device());
+    ev_ready_.assign(buckets_.size(), nullptr);
+    ev_end_.assign(buckets_.size(), nullptr);
+    for (auto* v : {&ev_ready_, &ev_end_})
+      for (auto& e : *v) TORCH_CHECK(hipEventCreate(&e) == hipSuccess, "hipEventCreate");
+    TORCH_CHECK(hipEventCreate(&ev_t0_) == hipSuccess && hipEventCreate(&ev_bwd_end_) == hipSuccess, "hipEventCreate");
+    probe_ = c10::hip::getStreamFromPoolMasqueradingAsCUDA(true, grad_.device().index());
+  }
+  bool gpu_timing() const { return timing_; }
+
+  // {"bwd_end_ms": ..} plus per launched bucket (b, bytes, ready_ms, end_ms) of the last step;
+  // synchronises on the step's last events (call after the step, never inside the timed loop)
+  std::pair<double, std::vector<std::tuple<int64_t, int64_t, double, double>>> gpu_trace() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::tuple<int64_t, int64_t, double, double>> out;
+    if (!timing_ || !t0_ok_) return {-1.0, out};
+    auto ms = [&](hipEvent_t e) {
+      float v = -1.f;
+      if (hipEventSynchronize(e) != hipSuccess || hipEventElapsedTime(&v, ev_t0_, e) != hipSuccess) return -1.0;
+      return (double)v;
+    };
+    for (size_t b = 0; b < timed_.size(); ++b)
+      if (timed_[b]) {
+        const auto& r = ranges_[b];
+        const int64_t esz = comm_.defined() ? comm_.element_size() : grad_.element_size();
+        out.emplace_back((int64_t)b, (r.second - r.first) * esz, ms(ev_ready_[b]), ms(ev_end_[b]));
+      }
+    return {bwd_end_ok_ ? ms(ev_bwd_end_) : -1.0, out};
+  }
+
   void reset() {
     std::lock_guard<std::mutex> g(mu_);
+    timed_.assign(buckets_.size(), false);
+    t0_ok_ = bwd_end_ok_ = false;
+    if (timing_) {
+      auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(grad_.device().index());
+      if (!capturing(cur.stream())) t0_ok_ = hipEventRecord(ev_t0_, cur.stream()) == hipSuccess;
+    }
     pending_.assign(buckets_.size(), 0);
     for (size_t b = 0; b < buckets_.size(); ++b) pending_[b] = (int64_t)buckets_[b].size();
     ready_.assign(buckets_.size(), false);
@@ -193,6 +256,10 @@ class Reducer {
       std::fill(ready_.begin(), ready_.end(), true);
       launch_ready_locked();
       works.swap(works_);
+      if (timing_ && t0_ok_ && !works.empty()) {
+        auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(grad_.device().index());
+        if (!capturing(cur.stream())) bwd_end_ok_ = hipEventRecord(ev_bwd_end_, cur.stream()) == hipSuccess;
+      }
     }
     for (auto& w : works) w->wait();
     std::lock_guard<std::mutex> g(mu_);
@@ -258,6 +325,11 @@ class Reducer {
   }
 
  private:
+  static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+  }
+
   double since_reset_us() const {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0_).count();
   }
@@ -268,6 +340,12 @@ class Reducer {
       const at::Tensor& buf = comm_.defined() ? comm_ : grad_;
       trace_.emplace_back(next_, (r.second - r.first) * buf.element_size(), since_reset_us());
       if (pg_ && (pg_->getSize() > 1 || force_comm_)) {
+        const bool timed = timing_ && t0_ok_;
+        hipStream_t cur_s = nullptr;
+        if (timed) {
+          cur_s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(grad_.device().index()).stream();
+          hipEventRecord(ev_ready_[next_], cur_s);
+        }
         at::Tensor slice = grad_.narrow(0, r.first, r.second - r.first);
         if (comm_.defined()) {
           at::Tensor c = comm_.narrow(0, r.first, r.second - r.first);
@@ -287,6 +365,12 @@ class Reducer {
           c10d::AllreduceOptions opts;
           opts.reduceOp = c10d::ReduceOp::SUM;
           works_.push_back(pg_->allreduce(ts, opts));
+        }
+        if (timed) {
+          // the probe stream waits on the collective (Work::wait is a stream wait), then records
+          c10::hip::HIPStreamGuardMasqueradingAsCUDA pg_guard(*probe_);
+          works_.back()->wait();
+          timed_[next_] = hipEventRecord(ev_end_[next_], probe_->stream()) == hipSuccess;
         }
         ++comm_calls_;
         comm_bytes_ += (r.second - r.first) * slice.element_size();
@@ -309,6 +393,12 @@ class Reducer {
   std::vector<std::tuple<int64_t, int64_t, double>> trace_;
   std::chrono::steady_clock::time_point t0_ = std::chrono::steady_clock::now();
   int64_t next_ = 0, comm_calls_ = 0, comm_bytes_ = 0;
+  // GPU timeline (set_gpu_timing)
+  bool timing_ = false, t0_ok_ = false, bwd_end_ok_ = false;
+  std::vector<hipEvent_t> ev_ready_, ev_end_;
+  std::vector<bool> timed_;
+  hipEvent_t ev_t0_ = nullptr, ev_bwd_end_ = nullptr;
+  std::optional<c10::hip::HIPStreamMasqueradingAsCUDA> probe_;
   std::mutex mu_;
 };
 
@@ -342,5 +432,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("comm_bytes", &mi_ddp::Reducer::comm_bytes)
       .def_property_readonly("ranges", &mi_ddp::Reducer::ranges)
       .def_property_readonly("buckets", &mi_ddp::Reducer::buckets)
-      .def_property_readonly("trace", &mi_ddp::Reducer::trace);
+      .def_property_readonly("trace", &mi_ddp::Reducer::trace)
+      .def_property("gpu_timing", &mi_ddp::Reducer::gpu_timing, &mi_ddp::Reducer::set_gpu_timing)
+      .def("gpu_trace", &mi_ddp::Reducer::gpu_trace, py::call_guard<py::gil_scoped_release>());
 }

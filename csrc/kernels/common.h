@@ -24,7 +24,16 @@ inline void mi_ws_retire(void* p) {
   std::lock_guard<std::mutex> lk(mu);
   retired.push_back(p);
 }
+// Captures are taken with capture_error_mode="thread_local" (the smddp / RCCL watchdog threads poll
+// events during a capture), so a workspace-growth path running on ANOTHER thread or stream than the
+// capturing one would not be rejected by the runtime: its allocation / synchronisation would run
+// silently outside the graph.  The capturing code therefore also announces every capture here
+// (mi_capture_enter / _exit, parallel/step_graph.py, graphs.py), and while any capture is open no
+// workspace grows, on any thread or stream.
+#include <atomic>
+inline std::atomic<int> g_mi_capture_depth{0};
 inline bool mi_stream_capturing(hipStream_t st) {
+  if (g_mi_capture_depth.load(std::memory_order_acquire) > 0) return true;
   hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(st, &s) == hipSuccess && s != hipStreamCaptureStatusNone;
 }

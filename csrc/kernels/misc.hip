@@ -448,7 +448,7 @@ __global__ void flag_bump_kernel(uint32_t* flag) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void flag_gate_kernel(const uint32_t* flag, uint32_t target, int* err, uint32_t timeout_ticks) {
+__global__ void flag_gate_kernel(const uint32_t* flag, uint32_t target, int* err, uint64_t timeout_ticks) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
@@ -478,10 +478,16 @@ MI_API int mi_flag_bump(uint32_t* flag, hipStream_t st) {
 }
 
 MI_API int mi_flag_gate(const uint32_t* flag, uint32_t target, int* err, int timeout_ms, hipStream_t st) {
+  // 64-bit ticks of the 100 MHz s_memrealtime clock: a 32-bit count capped the wait at ~42.9 s
   hipLaunchKernelGGL(flag_gate_kernel, dim3(1), dim3(64), 0, st, flag, target, err,
-                     (uint32_t)std::min<int64_t>((int64_t)timeout_ms * 100000, 0xFFFFFFFFll));
+                     (uint64_t)std::max(timeout_ms, 1) * 100000ull);
   return (int)hipGetLastError();
 }
+
+// a HIP graph capture is open (any thread, any stream): workspaces must not grow (common.h)
+MI_API void mi_capture_enter() { g_mi_capture_depth.fetch_add(1, std::memory_order_acq_rel); }
+MI_API void mi_capture_exit() { g_mi_capture_depth.fetch_sub(1, std::memory_order_acq_rel); }
+MI_API int mi_capture_depth() { return g_mi_capture_depth.load(std::memory_order_acquire); }
 
 // host-mapped, coherent int (the gates' error word): *host reads it without a synchronisation
 MI_API int mi_host_word_alloc(int** host, int** dev) {

@@ -558,11 +558,15 @@ MI_API int mi_stem_wgrad(const void* x, const void* dy, float* dw, int Nb, int H
 // g [64][Cw][7][7] fp32 (element strides sK, sC, sR, sS) += stem weight gradient of the real
 // channels.  hipErrorNotSupported when the shape is not the stem kernel's or the atomic fallback is
 // selected (the caller then uses mi_conv2d_wgrad into a padded buffer).
+// K, R, S, stride: the conv's real geometry -- the persistent kernel only computes the 7x7/2/64
+// gradient, so any other stem (3x3/1, 32 output channels, ...) must take the generic path.
 MI_API int mi_stem_wgrad_to(const void* x, const void* dy, float* g, int Cw, int64_t sK, int64_t sC, int64_t sR,
-                            int64_t sS, int Nb, int H, int W, int P, int Q, int pad, hipStream_t st) {
+                            int64_t sS, int Nb, int H, int W, int K, int R, int S, int stride, int P, int Q, int pad,
+                            hipStream_t st) {
   if (Cw < 1 || Cw > 8) return (int)hipErrorInvalidValue;
   const char* e = std::getenv("MI355X_DP_STEM_KERNEL");  // =0: the generic path (gemm_conv.hip)
-  if ((e && e[0] == '0') || !mi_stem_conv_ok(8, KOUT, SR, SS, SSTR, pad, Q)) return (int)hipErrorNotSupported;
+  if ((e && e[0] == '0') || !mi_stem_conv_ok(8, K, R, S, stride, pad, Q)) return (int)hipErrorNotSupported;
+  if (P != (H + 2 * pad - R) / stride + 1 || Q != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const StemWTo to{g, Cw, sK, sC, sR, sS};
   return stem_wgrad_impl(x, dy, nullptr, &to, Nb, H, W, P, Q, pad, st);
 }

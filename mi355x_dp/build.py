@@ -109,12 +109,13 @@ def build_comm(force=False, verbose=True):
 
 
 def build_reducer(force=False, verbose=True):
-    """csrc/ddp/reducer.cpp -> mi355x_dp/_native/_reducer_ext*.so (libtorch + c10d only)."""
+    """csrc/ddp/reducer.cpp -> mi355x_dp/_native/_reducer_ext*.so (libtorch + c10d, HIP events for the
+    GPU-side collective timeline)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "ddp", "*.cpp")))
     if not srcs:
         return None
     from mi355x_dp.parallel import _smddp_build
-    return _smddp_build.build(srcs, NATIVE, force=force, verbose=verbose, name="_reducer_ext", hip=False)
+    return _smddp_build.build(srcs, NATIVE, force=force, verbose=verbose, name="_reducer_ext", hip=True)
 
 
 REF_NOTEBOOKS = os.environ.get("MI355X_DP_REF_SRC", "/root/reference/notebooks")

@@ -16,7 +16,25 @@ only during capture and the captured all-reduces replay in the recorded order.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
+
+
+@contextlib.contextmanager
+def capture_open():
+    """Announce an open HIP graph capture to the native library: while any capture is open, no
+    lazily grown workspace grows -- on any thread or stream -- so nothing is allocated or
+    synchronised outside the graph behind the runtime's back (captures use
+    ``capture_error_mode="thread_local"``, which only polices the capturing thread; common.h)."""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops import kernels  # noqa: F401
+    lib = _lib.load(True)
+    lib.mi_capture_enter()
+    try:
+        yield
+    finally:
+        lib.mi_capture_exit()
 
 
 class GraphedStep:
@@ -37,7 +55,7 @@ class GraphedStep:
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, stream=side):
+            with capture_open(), torch.cuda.graph(self.graph, stream=side):
                 self.out = fn()
         finally:
             WgradStream.suspended -= 1

@@ -26,7 +26,7 @@ signature("mi_conv2d_dgrad_ex4", P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P,
 signature("mi_conv_wtrans", P, P, I, I, I, P)
 # stem_conv.hip (ops/stem.py): weight pack and the gradient straight into the parameter's buffer
 signature("mi_stem_wpack", P, P, I, I, I, I, L, L, L, L, P)
-signature("mi_stem_wgrad_to", P, P, P, I, L, L, L, L, I, I, I, I, I, I, P)
+signature("mi_stem_wgrad_to", P, P, P, I, L, L, L, L, I, I, I, I, I, I, I, I, I, I, P)
 signature("mi_conv_wtrans_multi", P, P, P, I, I, P)
 signature("mi_gemm_nt", P, P, P, P, P, I, I, I, I, I, I, I, I, P)
 signature("mi_gemm_tn", P, P, P, I, I, I, I, I, I, P)
@@ -68,6 +68,9 @@ signature("mi_flags_alloc", I, P)
 signature("mi_flag_bump", P, P)
 signature("mi_flag_gate", P, U32, P, I, P)
 signature("mi_host_word_alloc", P, P)
+signature("mi_capture_enter", restype=None)
+signature("mi_capture_exit", restype=None)
+signature("mi_capture_depth")
 
 # gemm_conv.hip (epilogue-fused NT GEMM)
 signature("mi_gemm_nt_epi", P, P, P, P, P, I, I, I, I, I, I, I, P)

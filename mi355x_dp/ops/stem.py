@@ -89,7 +89,7 @@ class _Stem(torch.autograd.Function):
         g = _grad_buffer(wconv)
         # the persistent stem kernel's fixed-order partial sums land in g's own layout; otherwise
         # (other geometry, atomic mode) a padded buffer is cropped and permuted into g
-        rc = lib.mi_stem_wgrad_to(ptr(x), ptr(dc), ptr(g), Cw, *g.stride(), N, H, W, P, Q, pad, st)
+        rc = lib.mi_stem_wgrad_to(ptr(x), ptr(dc), ptr(g), Cw, *g.stride(), N, H, W, K, R, S, stride, P, Q, pad, st)
         if rc != 0:
             gp = torch.zeros((K, R, S, 8), dtype=F32, device=dev)
             _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dc), ptr(gp), N, H, W, 8, K, R, S, stride, pad, P, Q, st)

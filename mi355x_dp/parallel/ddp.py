@@ -635,9 +635,21 @@ class DataParallel(nn.Module):
 
     def _final_callback(self):
         self._final_cb_pending = False
+        if self.__dict__.pop("_graph_comm_done", False):
+            return  # a replayed backward graph already ran its collectives, their join and the 1/world
         if self.__dict__.pop("_graph_backward_ran", False) and self.comm_on:
             self._mark_all_ready()
+        gated = self.__dict__.pop("_graph_gated", None)
         self.finish_gradient_sync(average=True)
+        if gated is not None:
+            # a gate that timed out let its collective run on stale gradients: find out (host wait for
+            # the last gate, i.e. until the replayed backward reached its last bucket) and raise
+            # before backward() returns -- before any optimizer step can use the result
+            from .step_graph import BucketGates
+            ev = self.__dict__.pop("_last_gate_event", None)
+            if ev is not None:
+                ev.synchronize()
+            BucketGates.check()
 
     def _arm_final_callback(self, out):
         """torch DDP's end-of-backward contract: the first gradient that reaches this forward's
@@ -666,12 +678,15 @@ class DataParallel(nn.Module):
         self._reset()
         self.wait_param_sync()
         self._wait_buffer_sync()
+        self._graph_bcast = False
         out = self._graphed_forward(args, kwargs) if self.foreign_optimizer else None
         if out is None:
             out = self.module(*args, **kwargs)
         if self.foreign_optimizer and torch.is_grad_enabled():
             self._arm_final_callback(out)
-        if self.broadcast_buffers and self.buffers.buffers and self.module.training:
+        if self._graph_bcast:
+            pass  # captured into this step's backward graph (step_graph comm_mode "capture")
+        elif self.broadcast_buffers and self.buffers.buffers and self.module.training:
             # torch DDP broadcasts rank 0's buffers synchronously BEFORE every training forward
             # (SURVEY.md X4), on the critical path.  Same values, off the critical path: broadcast
             # AFTER this forward's BN kernels (which update the running statistics) are enqueued;
@@ -716,7 +731,16 @@ class DataParallel(nn.Module):
         tok = self.__dict__.get("_graph_token")
         if tok is None:
             tok = self._graph_token = torch.zeros((), device=x.device, requires_grad=True)
+        self._graph_bcast = st.comm_mode == "capture"
         return st(tok, x)
+
+    def _capture_buffer_broadcast(self):
+        """inside the capture of a backward graph (comm_mode "capture"): rank 0's BN buffers, as
+        updated by the replayed forward, broadcast on the comm stream ahead of the bucket
+        collectives (the eager engine issues it after the forward; same values, same order)"""
+        if self.broadcast_buffers and self.buffers.buffers and self.module.training:
+            return dist.broadcast(self.buffers.data, 0, group=self.process_group, async_op=True)
+        return None
 
     # ------------------------------------- graphed backward: per-bucket gates (step_graph)
     def _begin_capture_marks(self, gates, stream):
@@ -741,10 +765,13 @@ class DataParallel(nn.Module):
             cm["gates"].bump(b, cm["stream"])
 
     def _gate_stream(self):
+        # HIGH priority: HIP pools hardware queues per priority, so the gate stream never shares an
+        # in-order queue with the normal-priority stream that replays the graph -- a gate enqueued
+        # before the replay cannot sit in front of the kernels it waits for
         s = getattr(self, "_gate_s", None)
         if s is None:
             s = self._gate_s = torch.cuda.Stream(device=self.flat.grad.device,
-                                                 priority=int(os.environ.get("MI355X_DP_GATE_PRIO", "0")))
+                                                 priority=int(os.environ.get("MI355X_DP_GATE_PRIO", "-1")))
         return s
 
     def _gate_trace_begin(self):
@@ -754,46 +781,28 @@ class DataParallel(nn.Module):
         t0.record()
         return {"t0": t0, "gates": [], "end": None}
 
-    def _smddp_comm_stream(self):
-        """the native smddp backend's comm stream (a torch ExternalStream), or None"""
-        if "_smddp_cs" not in self.__dict__:
-            cs = None
-            try:
-                from . import comm_paths
-                mod = comm_paths._native()
-                pg = self.process_group if self.process_group is not None else dist.distributed_c10d._get_default_group()
-                if mod is not None and str(dist.get_backend(pg)) == "smddp":
-                    h = int(mod.comm_stream(comm_paths.backend_of(pg)))
-                    cs = torch.cuda.ExternalStream(h, device=self.flat.grad.device)
-            except Exception:
-                cs = None
-            self._smddp_cs = cs
-        return self._smddp_cs
-
-    def _gated_launch(self, step, trace=None):
-        """After a replay of a captured backward: bucket b's collective is launched from the gate
-        stream behind a gate kernel that waits for the graph's bump of b (this replay's count) --
-        the reducer's ready-marks see the gate stream as the producing stream."""
+    def _gated_launch(self, step, target, trace=None):
+        """BEFORE a replay of a captured backward (comm_mode "gates"): per bucket b, in order, a gate
+        kernel on the high-priority gate stream that waits until the graph's bump of b reaches
+        ``target`` (this replay), then b's collective issued with the gate stream current -- the
+        reducer's ready-mark, any bf16 cast and the collective's producer event are all ordered
+        behind that gate, i.e. behind exactly b's gradient kernels."""
         from .step_graph import BucketGates
         BucketGates.check()
-        if trace is not None:
-            trace["end"] = torch.cuda.Event(enable_timing=True)
-            trace["end"].record()
         gs = self._gate_stream()
-        # the native smddp backend: each gate kernel goes straight onto the backend's comm stream
-        # and the collective is issued from the (idle) gate stream, so the comm stream waits on
-        # nothing else.  (Gating through a cross-stream event from the gate stream made the smddp
-        # path ~4x slower at world 1 -- host launches stalled; profiles/graph_bucket_gates.md.)
-        comm = self._smddp_comm_stream()
+        gs.wait_stream(torch.cuda.current_stream(gs.device))  # the previous step's users of the buckets
         with torch.cuda.stream(gs):
             for b, idxs in enumerate(self.buckets):
-                step.gates.gate(b, step.replays, gs if comm is None else comm)
+                step.gates.gate(b, target, gs)
                 if trace is not None:
                     ev = torch.cuda.Event(enable_timing=True)
-                    ev.record(gs if comm is None else comm)
+                    ev.record(gs)
                     trace["gates"].append(ev)
                 for i in idxs:
                     self.reducer.mark_ready(i)
+            last = torch.cuda.Event()
+            last.record(gs)
+        self._last_gate_event = last
         if trace is not None:
             self._last_gate_trace = trace
 

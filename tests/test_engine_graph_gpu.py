@@ -85,3 +85,29 @@ def test_graphed_engine_with_side_stream_reference(monkeypatch):
     assert float(loss) == pytest.approx(l_g[-1], rel=2e-2)
     d = (eng.flat.data - p_g).abs().max()
     assert float(d) < 1e-3
+
+
+@pytest.mark.parametrize("backend", ["nccl", "smddp"])
+def test_graphed_comm_modes_match_eager(backend):
+    """a replayed backward's bucket collectives captured INTO the graph (default
+    for RCCL paths), behind gates enqueued before the replay, or launched after it -- every mode
+    equals the eager engine bit for bit at world 1 with every collective issued (force_comm),
+    and the captured mode issues no per-step collective from the host"""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "graphed_capture_check.py"), "--backend", backend],
+                       capture_output=True, text=True, timeout=300, cwd=root,
+                       env={**os.environ, "MASTER_PORT": str(29593 + (backend == "smddp"))})
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    steps = len(out["eager_losses"])
+    for mode in ("capture", "gates", "after"):
+        m = out[mode]
+        assert m["modes"] == [mode], (mode, m)
+        assert m["replays"] == steps - 2 - 1, (mode, m)
+        assert m["losses_equal"] and m["params_equal"] and m["buffers_equal"], (mode, m)
+    # captured: the replays' collectives come from the graph, not from the host reducer
+    assert out["capture"]["comm_calls"] < out["gates"]["comm_calls"] == out["eager_comm_calls"], out

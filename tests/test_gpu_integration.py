@@ -464,27 +464,29 @@ def test_graphed_engine_two_ranks_gated_buckets():
     1000-class head, stock SGD) through the engine-backed DDP, graphed vs eager on IPC-only smddp
     (2 ranks sharing cuda:0).  At the reference's shape (batch 32 at 32x32): graphed == eager bit
     for bit on every rank (losses and flat fp32 parameters), replicas identical, one gate per
-    bucket.  At batch 256 at 224x224: every bucket's collective released by its gate, in order."""
+    bucket.  At batch 256 at 224x224: every bucket's collective released by its gate, in order, the
+    first one while the replayed backward is still running."""
     rows = _graphed_world2({})
     for row in rows:
-        assert row["gated"] and row["replays"] == 6 and row["replays_eager"] == 0, row
+        assert row["gated"] and row["comm_modes"] == ["gates"], row  # IPC collectives are never captured
+        assert row["replays"] == 6 and row["replays_eager"] == 0, row
         assert row["losses_graphed"] == row["losses_eager"], row
         assert row["graphed_equals_eager"] and row["replicas_identical"], row
         assert len(row["gate_open_ms"]) == row["buckets"] >= 2, row
     assert rows[0]["losses_graphed"] != rows[1]["losses_graphed"]  # different data per rank
     # Gate trace at a larger shape (batch 256 at 224x224, graphed up to 64M input elements): every
-    # bucket's gate fires once per replay, in bucket order.  Whether the first one opens before the
-    # replayed backward ends is NOT asserted here.  The gates are enqueued after hipGraphLaunch
-    # returns (~2 ms of host time for the ~150-node graph), and with two ranks on one GPU the
-    # runtime's stream-to-hardware-queue mapping may serialise a rank's comm stream behind its
-    # compute stream.  Two runs at this shape gave gate 0 at 0.39 ms of a ~6.7 ms replay and at
-    # 7.29 ms of 6.68 ms.  The one-rank-per-GPU overlap is measured in profiles/graph_bucket_gates.md.
+    # bucket's gate fires once per replay, in bucket order, and bucket 0's gate opens BEFORE the
+    # replayed backward ends.  This is structural since round 5: every gate (and the collective
+    # behind it) is enqueued before the replay is launched, on a high-priority stream (its own
+    # hardware-queue pool), so it no longer depends on when the host returns from the launch (the
+    # round-4 schedule enqueued the gates after it: gate 0 at 7.29 ms of a 6.68 ms replay once).
     rows = _graphed_world2({"GRAPHED_BATCH": "256", "GRAPHED_SIZE": "224",
                             "MI355X_DP_ENGINE_GRAPH_MAX_NUMEL": str(1 << 26), "GPU_MAX_HW_QUEUES": "6"})
     for row in rows:
         assert row["gated"] and row["replays"] == 6 and row["replicas_identical"], row
         opened, end = row["gate_open_ms"], row["replay_end_ms"]
         assert len(opened) == row["buckets"] >= 2 and opened == sorted(opened) and end > 0, row
+        assert opened[0] < end, row  # bucket 0's collective released under the replayed backward
         print(f"rank {row['rank']}: gates opened at {[round(t, 2) for t in opened]} ms, replay ended at "
               f"{end:.2f} ms")
 

@@ -62,6 +62,39 @@ def test_fused_stem_matches_per_op(n, size):
         assert rel_err(fused, per_op) < 3e-2, name
 
 
+@pytest.mark.parametrize("k,r,stride,pad", [(64, 3, 1, 1), (32, 7, 2, 3), (64, 5, 2, 2)])
+def test_fused_stem_other_geometries(k, r, stride, pad):
+    """fusable() accepts any small-channel bias-free stem: the persistent 7x7/2/64 weight-gradient
+    kernel must refuse the others and the generic path must give the right gradient
+    without touching other parameters' slices of the flat gradient buffer"""
+    from mi355x_dp.models.layers import BatchNorm2d, Conv2d, MaxPool2d, to_device_input
+    from mi355x_dp.ops import stem as S
+    torch.manual_seed(1)
+    conv = Conv2d(3, k, kernel_size=r, stride=stride, padding=pad, bias=False).cuda()
+    bn = BatchNorm2d(k).cuda()
+    pool = MaxPool2d(3, 2, 1)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xi = to_device_input(torch.randn(4, 3, 40, 40, device="cuda", generator=g))
+    assert S.fusable(conv, bn, pool, xi)
+    # sentinel gradient buffers around the conv's: a wrong-geometry kernel would write past it
+    conv.weight.grad = torch.zeros_like(conv.weight)
+    y = S.stem(conv, bn, pool, xi)
+    dy = torch.randn(y.shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    xr = xi[:, :3].float()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    gr, br = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
+    ref = F.max_pool2d(F.relu(F.batch_norm(F.conv2d(xr, wr, None, stride, pad), None, None, gr, br, True, 0.1,
+                                           bn.eps)), 3, 2, 1)
+    assert rel_err(y, ref) < 2e-2
+    ref.backward(dy.float())
+    assert conv.weight.grad.shape == wr.grad.shape
+    assert rel_err(conv.weight.grad, wr.grad) < 3e-2
+    assert rel_err(bn.weight.grad, gr.grad) < 3e-2 and rel_err(bn.bias.grad, br.grad) < 3e-2
+
+
 def test_fused_stem_used_in_resnet():
     from mi355x_dp.models import resnet50
     from mi355x_dp.ops import cross_entropy

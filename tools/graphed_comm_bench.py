@@ -1,10 +1,11 @@
 #!/usr/bin/env python
 """ms/step of the reference loop shape (ResNet-18, 1000 classes, batch 32 at 32x32, stock SGD through
 the engine-backed DDP, graphed steps) at world 1 with every bucket collective issued
-(MI355X_DP_FORCE_COMM=1), for the per-bucket gates on / off and without collectives -- one process,
-so it can run under rocprofv3.
+(MI355X_DP_FORCE_COMM=1) -- collectives captured into the backward graph, behind per-bucket gates
+enqueued before the replay, or all launched after the replay -- and without collectives.  One
+process, so it can run under rocprofv3.
 
-    python tools/graphed_comm_bench.py --mode gated|ungated|nocomm [--backend smddp|nccl] [--steps 300]
+    python tools/graphed_comm_bench.py --mode capture|gated|ungated|nocomm [--backend smddp|nccl] [--steps 300]
 """
 import argparse
 import json
@@ -19,12 +20,13 @@ sys.path.append(os.path.join(ROOT, "compat"))
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", default="gated", choices=("gated", "ungated", "nocomm"))
+    p.add_argument("--mode", default="capture", choices=("capture", "gated", "ungated", "nocomm"))
     p.add_argument("--backend", default="smddp")
     p.add_argument("--steps", type=int, default=300)
     a = p.parse_args()
     os.environ["MI355X_DP_FORCE_COMM"] = "0" if a.mode == "nocomm" else "1"
-    os.environ["MI355X_DP_GRAPH_GATES"] = "0" if a.mode == "ungated" else "1"
+    os.environ["MI355X_DP_GRAPH_COMM"] = {"capture": "capture", "gated": "gates", "ungated": "after",
+                                          "nocomm": "auto"}[a.mode]
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29577")
     os.environ.setdefault("RANK", "0")
@@ -89,8 +91,8 @@ def main():
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / a.steps
     host = {k: round(1000 * v / (a.steps + 10), 4) for k, v in list(host.items()) + list(ph.items())}
-    gated = any(s.gates is not None for s in getattr(ddp, "_graphs", {}).values())
-    print(json.dumps({"mode": a.mode, "backend": a.backend, "ms_per_step": round(ms, 4), "gated": gated,
+    modes = sorted({s.comm_mode for s in getattr(ddp, "_graphs", {}).values()})
+    print(json.dumps({"mode": a.mode, "backend": a.backend, "ms_per_step": round(ms, 4), "comm_modes": modes,
                       "img_s": round(32 / ms * 1000, 1), "loss": float(loss), "host_ms": host}), flush=True)
     dist.destroy_process_group()
 

@@ -1,7 +1,8 @@
 """Graphed engine at world size W > 1: every rank runs the
 reference's loop shape (ResNet-18, 1000-class head, batch 32 at 32x32, stock optim.SGD, through the
 torch_smddp shim's engine-backed DistributedDataParallel) twice -- graphed (MI355X_DP_ENGINE_GRAPH=1:
-forward + backward replayed as HIP graphs, bucket collectives behind per-bucket gates) and eagerly --
+forward + backward replayed as HIP graphs, bucket collectives behind per-bucket gates enqueued
+before each replay -- IPC collectives cannot be captured) and eagerly --
 and prints one JSON line: per-step losses of both runs, whether the final flat fp32 parameters are
 bit-identical between the runs, the replica checksum of every rank, and the gate trace of the last
 graphed step (ms from the replay's start at which each bucket's collective was released, and the ms
@@ -52,18 +53,18 @@ def run(mode):
         losses.append(float(loss))
     torch.cuda.synchronize()
     replays = sum(s.replays for s in getattr(ddp, "_graphs", {}).values())
-    gated = any(s.gates is not None for s in getattr(ddp, "_graphs", {}).values())
-    return ddp, losses, replays, gated
+    modes = sorted({s.comm_mode for s in getattr(ddp, "_graphs", {}).values()})
+    return ddp, losses, replays, modes
 
 
-eng_g, loss_g, replays, gated = run("1")
+eng_g, loss_g, replays, modes = run("1")
 trace = eng_g.gate_trace_ms()
 flat_g = eng_g.flat.data.clone()
 eng_e, loss_e, replays_e, _ = run("0")
 from mi355x_dp.parallel.health import ReplicaChecker  # noqa: E402
 same = ReplicaChecker(eng_g)(force=True)
 print(json.dumps({"rank": r, "world": w, "losses_graphed": loss_g, "losses_eager": loss_e, "replays": replays,
-                  "replays_eager": replays_e, "gated": gated, "graphed_equals_eager": bool(torch.equal(flat_g,
+                  "replays_eager": replays_e, "gated": modes == ["gates"], "comm_modes": modes, "graphed_equals_eager": bool(torch.equal(flat_g,
                                                                                            eng_e.flat.data)),
                   "replicas_identical": bool(same), "buckets": len(eng_g.buckets),
                   "gate_open_ms": trace[0] if trace else None, "replay_end_ms": trace[1] if trace else None,
