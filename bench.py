@@ -321,6 +321,22 @@ def main(argv=None):
             print(f"[bench] {e}", file=sys.stderr)
             replicas_ok = False
 
+    comm_timeline = None
+    if engine.reducer is not None and engine.comm_on and cuda and not args.graph:
+        # after the timed region, one more step with GPU events around every bucket collective
+        # (every rank runs it, so the collectives still match): when each bucket became ready on the
+        # producing stream, when its collective ended on the comm stream, when the backward's
+        # kernels ended -- the overlap record in device time, not host launch time
+        # (two untimed steps first, so the host runs ahead of the GPU as in the timed loop: right
+        # after a synchronize the device would idle on the host's first launches of the step)
+        step(20_000)
+        step(20_001)
+        engine.reducer.gpu_timing = True
+        step(20_002)
+        sync()
+        comm_timeline = _timeline(engine)
+        engine.reducer.gpu_timing = False
+
     comm_probe = None
     if world > 1 and os.environ.get("MI355X_DP_BENCH_COMM_PROBE", "1") == "1":
         # after the timed region: the fabric's measured collective times, recorded with the result
@@ -406,11 +422,36 @@ def main(argv=None):
             "comm_probe": comm_probe,
             "ipc_probe": ipc_probe,
             "smddp_job": smddp_job,
-            "bucket_launch_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
+            # GPU event times (ms from the forward's start) of one step after the timed region
+            "comm_timeline": comm_timeline,
+            "bucket_launch_ms": comm_timeline["buckets"] if comm_timeline else None,
+            "comm_exposed_ms": comm_timeline["comm_exposed_ms"] if comm_timeline else None,
+            # host clock when each bucket's collective was handed to the backend (not overlap evidence)
+            "bucket_issue_host_ms": [[b, round(nb / 2**20, 2), round(t / 1e3, 3)] for b, nb, t in engine.bucket_trace],
         }
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.destroy_process_group()
+
+
+def _timeline(engine):
+    """The reducer's GPU timeline of the last step (csrc/ddp/reducer.cpp ``gpu_trace``): per bucket
+    [bucket, MB, ready_ms, start_ms, end_ms] -- start = max(ready, previous collective's end), as
+    collectives run one after another on the comm stream -- plus the end of the backward's kernels and
+    ``comm_exposed_ms`` = last collective end - backward end (>= 0): the communication the step waited
+    for after its compute."""
+    bwd_end, rows = engine.reducer.gpu_trace()
+    if not rows or bwd_end < 0:
+        return None
+    out, prev_end = [], 0.0
+    for b, nbytes, ready, end in rows:
+        start = max(ready, prev_end)
+        out.append([b, round(nbytes / 2**20, 2), round(ready, 3), round(start, 3), round(end, 3)])
+        prev_end = end
+    last_end = max(r[4] for r in out)
+    return {"ref": "forward start of the step", "bwd_end_ms": round(bwd_end, 3), "buckets": out,
+            "comm_ms": round(sum(r[4] - r[3] for r in out), 3),
+            "comm_exposed_ms": round(max(0.0, last_end - bwd_end), 3)}
 
 
 def _child_env():

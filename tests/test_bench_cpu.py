@@ -64,7 +64,8 @@ def test_world8_rehearsal_on_cpu_ranks():
     d = _check(lines, 8)
     assert d["config"]["buckets"] >= 2
     # bucket launch trace: every bucket went to the comm stream in order during backward
-    ids = [b for b, _, _ in d["bucket_launch_ms"] if b >= 0]
+    ids = [b for b, _, _ in d["bucket_issue_host_ms"] if b >= 0]
+    assert d["comm_timeline"] is None  # GPU event timeline: CUDA engines only
     assert ids == list(range(d["config"]["buckets"]))
 
 

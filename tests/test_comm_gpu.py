@@ -122,10 +122,19 @@ def test_force_comm_world1_bench(backend, wgrad_stream):
     cfg = out["config"]
     assert cfg["backend"] == backend and cfg["comm_forced_at_world1"] is True
     assert cfg["wgrad_stream"] is bool(wgrad_stream)
-    trace = out["bucket_launch_ms"]
+    trace = out["bucket_issue_host_ms"]
     assert [t[0] for t in trace[:-1]] == list(range(cfg["buckets"])) and trace[-1][0] == -1
     launch_ms = [t[2] for t in trace[:-1]]
     assert launch_ms == sorted(launch_ms)
+    # GPU event timeline: every bucket, in order, each collective ending after its
+    # bucket was ready and after the previous collective; the exposed tail is reported, not negative
+    tl = out["comm_timeline"]
+    assert [r[0] for r in tl["buckets"]] == list(range(cfg["buckets"])), tl
+    for i, (b, mb, ready, start, end) in enumerate(tl["buckets"]):
+        assert 0 <= ready <= start <= end, tl
+        assert i == 0 or start >= tl["buckets"][i - 1][4], tl
+    assert tl["bwd_end_ms"] > 0 and out["comm_exposed_ms"] == tl["comm_exposed_ms"] >= 0
+    assert out["bucket_launch_ms"] == tl["buckets"]
 
 
 @pytest.mark.parametrize("backend", ["smddp", "nccl"])
@@ -140,8 +149,9 @@ def test_force_comm_world1_shard_optimizer(backend):
     out = _bench(common + ["--shard-optimizer"], {"MASTER_PORT": str(port + 1)})
     assert out["config"]["shard_optimizer"] is True and ref["config"]["shard_optimizer"] is False
     assert out["config"]["buckets"] == ref["config"]["buckets"]
-    trace = out["bucket_launch_ms"]
+    trace = out["bucket_issue_host_ms"]
     assert [t[0] for t in trace[:-1]] == list(range(out["config"]["buckets"]))
+    assert [r[0] for r in out["comm_timeline"]["buckets"]] == list(range(out["config"]["buckets"]))
     # same start; both train.  (Exact trajectory equality is not asserted here: the stem / fc weight
     # gradients sum with fp32 atomics and at 32 images of 64x64 the BN statistics amplify a flipped
     # bf16 rounding to ~1e-2 in the loss within a few steps, run to run, in either mode.  The

@@ -67,21 +67,24 @@ def test_fused_stem_other_geometries(k, r, stride, pad):
     """fusable() accepts any small-channel bias-free stem: the persistent 7x7/2/64 weight-gradient
     kernel must refuse the others and the generic path must give the right gradient
     without touching other parameters' slices of the flat gradient buffer"""
-    from mi355x_dp.models.layers import BatchNorm2d, Conv2d, MaxPool2d, to_device_input
+    from mi355x_dp.models.layers import BatchNorm2d, Conv2d, MaxPool2d, conv_bn, to_device_input
     from mi355x_dp.ops import stem as S
     torch.manual_seed(1)
     conv = Conv2d(3, k, kernel_size=r, stride=stride, padding=pad, bias=False).cuda()
     bn = BatchNorm2d(k).cuda()
     pool = MaxPool2d(3, 2, 1)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
     g = torch.Generator(device="cuda").manual_seed(5)
     xi = to_device_input(torch.randn(4, 3, 40, 40, device="cuda", generator=g))
     assert S.fusable(conv, bn, pool, xi)
     # sentinel gradient buffers around the conv's: a wrong-geometry kernel would write past it
     conv.weight.grad = torch.zeros_like(conv.weight)
     y = S.stem(conv, bn, pool, xi)
+    y_p = pool(conv_bn(conv2, bn2, xi, relu=True))  # per-op native path: same bf16 rounding points
     dy = torch.randn(y.shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
     y.backward(dy)
+    y_p.backward(dy)
     torch.cuda.synchronize()
     xr = xi[:, :3].float()
     wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
@@ -91,8 +94,14 @@ def test_fused_stem_other_geometries(k, r, stride, pad):
     assert rel_err(y, ref) < 2e-2
     ref.backward(dy.float())
     assert conv.weight.grad.shape == wr.grad.shape
-    assert rel_err(conv.weight.grad, wr.grad) < 3e-2
-    assert rel_err(bn.weight.grad, gr.grad) < 3e-2 and rel_err(bn.bias.grad, br.grad) < 3e-2
+    # against fp32: no worse than the per-op native path (bf16 activations, BN backward at M=6400
+    # amplifies their rounding), and close to that path itself
+    for name, fused, per_op, ref_g in (("conv", conv.weight.grad, conv2.weight.grad, wr.grad),
+                                       ("gamma", bn.weight.grad, bn2.weight.grad, gr.grad),
+                                       ("beta", bn.bias.grad, bn2.bias.grad, br.grad)):
+        e_f, e_p = rel_err(fused, ref_g), rel_err(per_op, ref_g)
+        assert e_f <= 1.25 * e_p + 0.01, (name, e_f, e_p)
+        assert rel_err(fused, per_op) < 3e-2, name
 
 
 def test_fused_stem_used_in_resnet():
