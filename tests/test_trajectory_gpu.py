@@ -20,24 +20,19 @@ def test_training_trajectory_matches_stock_fp32():
 
 
 def test_reference_shape_trajectory_matches_stock_fp32():
-    """the reference's own shape (ResNet-18, 1000-class head, 32x32, batch 32,
-    lr 0.01, momentum 0.9) for 150 steps of fresh learnable batches, through the engine-backed DDP
-    + stock SGD (graphed after two eager steps), against stock PyTorch fp32 on the same GPU: the
-    10-step mean losses track each other and both curves learn."""
+    """the reference's own shape (ResNet-18, 1000-class head, 32x32,
+    batch 32, lr 0.01, momentum 0.9) for 150 steps of fresh learnable batches, through the
+    engine-backed DDP + stock SGD (graphed after two eager steps), against stock PyTorch fp32 on
+    the same GPU, averaged over 3 (init, data) seeds: every 10-step window of the mean loss curves
+    within 12 %, and both learn."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import ref_trajectory
-    ours, ref, graphed = ref_trajectory.run(150)
-    assert graphed == 148
+    ours, ref, graphed = ref_trajectory.run_seeds(150, seeds=(1, 2, 3))
+    assert graphed == [148, 148, 148]
     wo, wr = ref_trajectory.windows(ours), ref_trajectory.windows(ref)
     msg = "ours " + " ".join(f"{v:.3f}" for v in wo) + " | fp32 " + " ".join(f"{v:.3f}" for v in wr)
-    # bf16 and fp32 runs of 150 SGD steps follow chaotically diverging trajectories, and the stock
-    # fp32 reference is itself not run-to-run deterministic on this GPU: our curve is bit-identical
-    # across runs, while the reference's loss-spike window 4 measured 2.88 in one run and 2.64 in
-    # another (ours 3.04).  So: every window within 20 % + 0.05, the curves on average within 6 %,
-    # and the last window within 10 %.
     for i, (o, r) in enumerate(zip(wo, wr)):
-        assert abs(o - r) <= 0.20 * r + 0.05, (i, msg)
+        assert abs(o - r) <= 0.12 * r + 0.01, (i, msg)
     mean_rel = sum(abs(o - r) / r for o, r in zip(wo, wr)) / len(wo)
-    assert mean_rel <= 0.06, (mean_rel, msg)
-    assert abs(wo[-1] - wr[-1]) <= 0.10 * wr[-1], msg
+    assert mean_rel <= 0.05, (mean_rel, msg)
     assert wo[-1] < 0.75 * wo[0] and wr[-1] < 0.75 * wr[0], msg

@@ -38,12 +38,12 @@ def batches(steps, batch, seed=0):
     return [(x[i * batch:(i + 1) * batch], y[i * batch:(i + 1) * batch]) for i in range(steps)]
 
 
-def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1):
+def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1, data_seed=0):
     from mi355x_dp.models import get_model
     from mi355x_dp.models.stock import stock_resnet
     from mi355x_dp.parallel import DataParallel
     dev = torch.device("cuda", 0)
-    data = batches(steps, batch)
+    data = batches(steps, batch, data_seed)
     torch.manual_seed(seed)  # the reference seeds before building the model (gpu.py:120)
     ours = get_model("resnet18", num_classes=1000).to(dev)
     init = {k: v.detach().clone() for k, v in ours.state_dict().items()}
@@ -79,6 +79,20 @@ def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1):
 
 def windows(v, k=10):
     return [float(np.mean(v[i:i + k])) for i in range(0, len(v) - k + 1, k)]
+
+
+def run_seeds(steps=150, seeds=(1, 2, 3)):
+    """``run`` for several (init, data) seeds: the per-step losses averaged over the seeds, for ours
+    and for the stock fp32 reference, plus the graphed step count.  A single bf16-vs-fp32 pair of
+    150-step SGD trajectories diverges chaotically (and the fp32 reference is itself not run-to-run
+    deterministic on the GPU); the mean over independent seeds is what a tolerance can pin."""
+    ours, ref, graphed = [], [], []
+    for sd in seeds:
+        o, r, g = run(steps, seed=sd, data_seed=sd - 1)
+        ours.append(o)
+        ref.append(r)
+        graphed.append(g)
+    return np.mean(ours, axis=0).tolist(), np.mean(ref, axis=0).tolist(), graphed
 
 
 def main():
