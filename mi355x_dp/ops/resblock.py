@@ -480,7 +480,7 @@ def fusable(block, x) -> bool:
     """The fused node covers the native training path: CUDA, grad enabled, BN in training mode
     with running statistics and a fixed momentum, every conv a native MFMA conv (C % 64 == 0)."""
     from mi355x_dp.models.layers import BatchNorm2d, Conv2d
-    if not (x.is_cuda and torch.is_grad_enabled() and block.training):
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled() and block.training):
         return False
     convs, bns, _ = _specs(block)
     for c in convs:

@@ -103,7 +103,7 @@ def fusable(conv, bn, pool, x) -> bool:
     BN with running stats and fixed momentum, a plain max pool, and an input that needs no
     gradient (the stem dgrad is never needed for images)."""
     from mi355x_dp.models.layers import BatchNorm2d, Conv2d, MaxPool2d
-    if not (x.is_cuda and torch.is_grad_enabled() and bn.training and not x.requires_grad):
+    if not (x.is_cuda and x.dtype == BF16 and torch.is_grad_enabled() and bn.training and not x.requires_grad):
         return False
     if not (isinstance(conv, Conv2d) and isinstance(bn, BatchNorm2d) and isinstance(pool, MaxPool2d)):
         return False

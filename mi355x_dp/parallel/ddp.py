@@ -239,7 +239,7 @@ class DataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = DEFAULT_BUCKET_MB,
                  first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB, broadcast_buffers: bool = True,
-                 bf16_copy: bool = True, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
+                 bf16_copy: Optional[bool] = None, last_bucket_mb: float = DEFAULT_LAST_BUCKET_MB,
                  min_bucket_mb: float = DEFAULT_MIN_BUCKET_MB, force_comm: bool = FORCE_COMM,
                  check_stream_order: bool = CHECK_STREAM_ORDER, grad_comm: str = GRAD_COMM,
                  wgrad_stream=WGRAD_STREAM, calibrate: bool = CALIBRATE,
@@ -295,6 +295,9 @@ class DataParallel(nn.Module):
         on_gpu = any(p.is_cuda for p in params)
         kernel_ids = {id(m.weight) for m in module.modules() if isinstance(m, _NativeConv)} if on_gpu else set()
         self.buffers = FlatBuffers(list(module.buffers()))
+        if bf16_copy is None:  # the bf16 compute shadow serves the bf16 kernels only
+            from mi355x_dp.ops.fp32 import COMPUTE_FP32
+            bf16_copy = not COMPUTE_FP32
 
         from . import _reducer_native
         native = _reducer_native.load()

@@ -98,8 +98,10 @@ class DistributedDataParallel(metaclass=_FactoryMeta):
             if eng.rank == 0:
                 # precision honesty: the reference trains in fp32 (TF32-class
                 # convs on A100); the engine's native kernels compute in bf16
-                print("[mi355x_dp] DistributedDataParallel -> native engine: compute dtype bf16 (MFMA, fp32 "
-                      "accumulation), fp32 master weights, fp32 gradients and all-reduce "
+                from mi355x_dp.ops.fp32 import COMPUTE_FP32
+                cd = "fp32 (MFMA f32 operands, exact fp32)" if COMPUTE_FP32 else "bf16 (MFMA, fp32 accumulation)"
+                print(f"[mi355x_dp] DistributedDataParallel -> native engine: compute dtype {cd}, "
+                      "fp32 master weights, fp32 gradients and all-reduce "
                       f"({len(eng.buckets)} buckets, world {eng.world_size})", flush=True)
             return eng
         return stock_ddp()(module, **kwargs)
