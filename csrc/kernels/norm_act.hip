@@ -843,9 +843,22 @@ __global__ __launch_bounds__(NT) void bnpool3_bwd_apply_kernel(const bf16_t* __r
   }
 }
 
+// grid of the elementwise BN passes: one EW_U-vector batch per thread, capped at
+// MI355X_DP_EW_GRID_CAP blocks (default MI_EW_GRID_CAP; a cap near the resident block count turns
+// the launch into a grid-stride sweep without block turnover)
+inline int ew_grid_cap() {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = std::getenv("MI355X_DP_EW_GRID_CAP");
+    cap = (e && std::atoi(e) > 0) ? std::atoi(e) : MI_EW_GRID_CAP;
+  }
+  return cap;
+}
+
 inline int ew_grid(int64_t nvec) {
   int64_t g = (nvec + NT * EW_U - 1) / (NT * EW_U);
-  return (int)(g < MI_EW_GRID_CAP ? g : MI_EW_GRID_CAP);
+  const int cap = ew_grid_cap();
+  return (int)(g < cap ? g : cap);
 }
 
 // channel octet fixed per thread for the whole grid-stride pass (bn_apply_kernel_t FIXC)

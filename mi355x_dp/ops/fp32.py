@@ -48,7 +48,8 @@ def to_input(x: torch.Tensor) -> torch.Tensor:
     Cp = (C + 3) // 4 * 4
     if Cp == C:
         return _nhwc(x)
-    out = torch.zeros((N, Cp, H, W), dtype=F32, device=x.device, memory_format=CL)
+    out = torch.empty((N, Cp, H, W), dtype=F32, device=x.device, memory_format=CL)
+    out[:, C:].zero_()
     out[:, :C].copy_(x)
     return out
 

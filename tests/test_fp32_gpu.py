@@ -93,7 +93,7 @@ def test_f32_pool_and_linear(fp32_mode):
     xc = x.float().cuda().contiguous(memory_format=CL).requires_grad_()
     y = fp32_mode.max_pool2d(xc, 3, 2, 1)
     y.backward(dy.float().cuda().contiguous(memory_format=CL))
-    assert rel(y, yr) == 0.0 and rel(xc.grad, xr.grad) < 1e-6
+    assert rel(y, yr) < 1e-7 and rel(xc.grad, xr.grad) < 1e-6  # the fp32 max of fp32-rounded inputs
     xg = torch.randn(6, 16, 3, 3, generator=g, dtype=torch.float64)
     xgr = xg.clone().requires_grad_()
     ygr = torch.flatten(F.adaptive_avg_pool2d(xgr, 1), 1)
