@@ -355,25 +355,40 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(const bf16_t* __restri
   block_reduce_store(s, q, part, C, cbase, g);
 }
 
-// -> dgamma/dbeta (+=) and coef[0..2][C] so that dx = coef0*dz + coef1*x + coef2
-__device__ __forceinline__ void fin_bwd(int c, double s, double q, const FinArgs& f) {
-  const int M = f.M, C = f.C;
-  const float* gamma = f.gamma; const float* mean = f.mean; const float* invstd = f.invstd;
-  float* dgamma = f.dgamma; float* dbeta = f.dbeta; float* coef = f.coef;
-  const float is = invstd[c];
+// per-channel affine of the BN backward: dx = k0*dz + k1*x + k2 (dz = relu-masked dy)
+__device__ __forceinline__ void bwd_coefs(int c, double s, double q, const FinArgs& f, float& k0, float& k1,
+                                          float& k2) {
+  const float is = f.invstd[c];
   const float sum_dz = (float)s;
   const float sum_dz_xhat = (float)q * is;
-  if (dgamma) dgamma[c] += sum_dz_xhat;
-  if (dbeta) dbeta[c] += sum_dz;
-  const float gm = gamma ? gamma[c] : 1.f;
-  const float k0 = gm * is;
-  const float mdz = sum_dz / M, mdzx = sum_dz_xhat / M;
+  const float gm = f.gamma ? f.gamma[c] : 1.f;
+  k0 = gm * is;
+  const float mdz = sum_dz / f.M, mdzx = sum_dz_xhat / f.M;
   // dx = k0*(dz - mdz - xhat*mdzx),  xhat = (x-mean)*is
-  const float k1 = -k0 * is * mdzx;
-  const float k2 = -k0 * mdz - k1 * mean[c];
-  coef[c] = k0;
-  coef[C + c] = k1;
-  coef[2 * C + c] = k2;
+  k1 = -k0 * is * mdzx;
+  k2 = -k0 * mdz - k1 * f.mean[c];
+}
+
+// -> dgamma/dbeta (+=) and coef[0..2][C] so that dx = coef0*dz + coef1*x + coef2.  SC1: the
+// coefficients are stored write-through (sc1) for consumers on other CUs of the SAME launch
+// (bn_bwd_fin_apply_kernel), which read them with sc1 loads after an agent-scope signal
+template <bool SC1 = false>
+__device__ __forceinline__ void fin_bwd(int c, double s, double q, const FinArgs& f) {
+  const int C = f.C;
+  const float is = f.invstd[c];
+  if (f.dgamma) f.dgamma[c] += (float)q * is;
+  if (f.dbeta) f.dbeta[c] += (float)s;
+  float k0, k1, k2;
+  bwd_coefs(c, s, q, f, k0, k1, k2);
+  if (SC1) {
+    __hip_atomic_store(f.coef + c, k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(f.coef + C + c, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(f.coef + 2 * C + c, k2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    f.coef[c] = k0;
+    f.coef[C + c] = k1;
+    f.coef[2 * C + c] = k2;
+  }
 }
 
 __global__ __launch_bounds__(FIN_T) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, FinArgs f) {
@@ -386,18 +401,17 @@ __global__ __launch_bounds__(FIN_T) void bn_bwd_finalize_kernel(const float* __r
 // like slab_split_kernel, then counts its arrival; the last arriving split of channel group cg
 // (device-scope release/acquire) reduces the S rows and runs the finalize for those channels.
 // Deterministic: fixed split ranges, fixed reduction order.  cnt[cg] is reset by the finalizer.
-template <bool BWD>
-__global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __restrict__ part, int nblk,
-                                                               int rows_per, float* __restrict__ out,
-                                                               int* __restrict__ cnt, FinArgs f) {
-  __shared__ double red[2][FIN_G][64];
-  __shared__ int last;
+// Returns true in the block that finalized group cg (its wave 0 wrote the per-channel outputs).
+template <bool BWD, bool SC1, int TG = FIN_G>  // TG row groups of 64 channel lanes (blockDim = 64 TG)
+__device__ __forceinline__ bool split_fin_body(const float* __restrict__ part, int nblk, int rows_per,
+                                               float* __restrict__ out, int* __restrict__ cnt, const FinArgs& f,
+                                               int cg, int split, int S, double (*red)[TG][64], int* last) {
   const int C = f.C;
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int b0 = blockIdx.y * rows_per, b1 = min(nblk, b0 + rows_per);
+  const int c = cg * 64 + cl;
+  const int b0 = split * rows_per, b1 = min(nblk, b0 + rows_per);
   double a = 0.0, b = 0.0;
-  if (c < C) sum_rows<false>(part, b0 + rg, b1, FIN_G, C, c, a, b);
+  if (c < C) sum_rows<false>(part, b0 + rg, b1, TG, C, c, a, b);
   red[0][rg][cl] = a;
   red[1][rg][cl] = b;
   __syncthreads();
@@ -409,45 +423,55 @@ __global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __re
   // ResNet-50 step.
 #if MI_FENCE_HANDOFF  // A/B build: the former acq_rel fence pair
   if (rg == 0 && c < C) {
-    for (int g = 1; g < FIN_G; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
-    out[(size_t)(2 * blockIdx.y) * C + c] = (float)a;
-    out[(size_t)(2 * blockIdx.y + 1) * C + c] = (float)b;
+    for (int g = 1; g < TG; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
+    out[(size_t)(2 * split) * C + c] = (float)a;
+    out[(size_t)(2 * split + 1) * C + c] = (float)b;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    last = atomicAdd(cnt + blockIdx.x, 1) == (int)gridDim.y - 1;
-    if (last) __threadfence();
+    *last = atomicAdd(cnt + cg, 1) == S - 1;
+    if (*last) __threadfence();
   }
 #else
   if (rg == 0) {
     if (c < C) {
-      for (int g = 1; g < FIN_G; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
-      __hip_atomic_store(out + (size_t)(2 * blockIdx.y) * C + c, (float)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(out + (size_t)(2 * blockIdx.y + 1) * C + c, (float)b, __ATOMIC_RELAXED,
+      for (int g = 1; g < TG; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
+      __hip_atomic_store(out + (size_t)(2 * split) * C + c, (float)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(out + (size_t)(2 * split + 1) * C + c, (float)b, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) last = atomicAdd(cnt + blockIdx.x, 1) == (int)gridDim.y - 1;
+    if (threadIdx.x == 0) *last = atomicAdd(cnt + cg, 1) == S - 1;
   }
 #endif
   __syncthreads();
-  if (!last) return;
+  if (!*last) return false;
   if (threadIdx.x == 0) {
-    cnt[blockIdx.x] = 0;  // ready for the next launch (stream order)
-    if (!BWD && blockIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+    cnt[cg] = 0;  // ready for the next launch (stream order)
+    if (!BWD && cg == 0 && f.nbt) f.nbt[0] += 1;
   }
   // second stage over the S split rows (other blocks' rows: sc1 loads, see above)
   double s2 = 0.0, q2 = 0.0;
-  if (c < C) sum_rows<true>(out, rg, (int)gridDim.y, FIN_G, C, c, s2, q2);
+  if (c < C) sum_rows<true>(out, rg, S, TG, C, c, s2, q2);
   __syncthreads();
   red[0][rg][cl] = s2;
   red[1][rg][cl] = q2;
   __syncthreads();
-  if (rg != 0 || c >= C) return;
-  for (int g = 1; g < FIN_G; ++g) { s2 += red[0][g][cl]; q2 += red[1][g][cl]; }
-  if (BWD) fin_bwd(c, s2, q2, f);
+  if (rg != 0 || c >= C) return true;
+  for (int g = 1; g < TG; ++g) { s2 += red[0][g][cl]; q2 += red[1][g][cl]; }
+  if (BWD) fin_bwd<SC1>(c, s2, q2, f);
   else fin_fwd(c, s2, q2, f);
+  return true;
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(FIN_T) void slab_split_fin_kernel(const float* __restrict__ part, int nblk,
+                                                               int rows_per, float* __restrict__ out,
+                                                               int* __restrict__ cnt, FinArgs f) {
+  __shared__ double red[2][FIN_G][64];
+  __shared__ int last;
+  split_fin_body<BWD, false>(part, nblk, rows_per, out, cnt, f, blockIdx.x, blockIdx.y, gridDim.y, red, &last);
 }
 
 template <bool FIXC>
@@ -498,6 +522,165 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
       for (int j = 0; j < 8; ++j) o[j] = k0[j] * d[j] + k1[j] * xv[j] + k2[j];
       st16(dx, v, pack8(o));
       if (!FIXC) c = it.chan(c, C);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BN backward of a tall slab in ONE launch: finalize + apply (the finalize's own
+// launch -- ~6-12 us and a dependent kernel boundary, 46 times per ResNet-50 step on the compute
+// stream -- folded into its consumer).  Blocks [0, G*S) are the finalizer blocks of
+// slab_split_fin_kernel (G channel groups x S splits; the last-arriving split of each group
+// finalizes it and writes its coefficients write-through); the group whose arrival completes all G
+// raises `ready`.  Blocks [G*S, G*S + A) apply: each issues the loads of its first EW_U vectors,
+// then waits for `ready` (one lane polls with sc1 loads and s_sleep), reads its channel octet's
+// coefficients with sc1 loads (MI355X_MICROARCH.md hand-off table, first row) and sweeps its vectors.
+// The finalizer blocks have the lowest block indices, so they are dispatched first; a bounded wait
+// never hangs anyway: an apply block that waited MI_FIN_WAIT_TICKS (100 MHz) computes the
+// coefficients itself from the slab (no dgamma / dbeta writes) and counts the event in sync[3].
+// `ready` is reset for the next launch by whichever of {the A apply blocks after their wait, the
+// block that raised it} arrives last (sync[2]); sync[0] counts finalized groups.
+#ifndef MI_FIN_WAIT_TICKS
+#define MI_FIN_WAIT_TICKS 200000  // 2 ms
+#endif
+constexpr int FUSED_MAX_C = 2048;
+constexpr int FUSED_T = 512, FUSED_G = FUSED_T / 64;  // 2 waves per SIMD: up to 256 VGPRs, no spills
+struct FusedBwdArgs {
+  const float* part; int nblk, rows_per, S, G;
+  float* out; int* cnt; uint32_t* sync;
+  FinArgs f;
+  const bf16_t* dy; const bf16_t* y; const bf16_t* x; bf16_t* dx; bf16_t* dres;
+  int64_t nvec; int A; int relu;
+};
+
+__device__ __forceinline__ void ld8_sc1(const float* p, float* o) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool RELU>
+__global__ __launch_bounds__(FUSED_T) void bn_bwd_fin_apply_kernel(FusedBwdArgs p) {
+  __shared__ double red[2][FUSED_G][64];
+  __shared__ int last, ok;
+  const int F = p.G * p.S;
+  const int C = p.f.C;
+  if ((int)blockIdx.x < F) {
+    if (split_fin_body<true, true, FUSED_G>(p.part, p.nblk, p.rows_per, p.out, p.cnt, p.f, blockIdx.x % p.G,
+                                   blockIdx.x / p.G, p.S, red, &last)) {
+      // wave 0 wrote this group's coefficients (sc1); after its stores, lane 0 counts the group
+      if (threadIdx.x < 64) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0 && atomicAdd(p.sync, 1u) == (uint32_t)p.G - 1) {
+          p.sync[0] = 0;
+          __hip_atomic_store(p.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (atomicAdd(p.sync + 2, 1u) == (uint32_t)p.A) {  // every apply block already gave up waiting
+            __hip_atomic_store(p.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            p.sync[2] = 0;
+          }
+        }
+      }
+    }
+    return;
+  }
+  // ------------------------------------------------------------------ apply block
+  const int64_t stride = (int64_t)p.A * FUSED_T;
+  const int64_t v0 = (int64_t)(blockIdx.x - F) * FUSED_T + threadIdx.x;
+  const int c0 = (int)((v0 * 8) % C);  // fixed for the whole sweep: (stride * 8) % C == 0 (host)
+  uint4 dv[EW_U], xq[EW_U], yq[EW_U];
+#pragma unroll
+  for (int u = 0; u < EW_U; ++u) {  // the first batch in flight while the coefficients are finalized
+    const int64_t v = v0 + u * stride;
+    if (v < p.nvec) {
+      dv[u] = ld_nt16(p.dy, v);
+      xq[u] = ld_nt16(p.x, v);
+      if (RELU) yq[u] = ld_nt16(p.y, v);
+    }
+  }
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int good = 1;
+    while (__hip_atomic_load(p.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)MI_FIN_WAIT_TICKS) {
+        good = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(32);  // ~1 us between polls: many tight pollers of one word slow the chip
+    }
+    ok = good;
+  }
+  __syncthreads();
+  float k0[8], k1[8], k2[8];
+  if (ok) {
+    ld8_sc1(p.f.coef + c0, k0);
+    ld8_sc1(p.f.coef + C + c0, k1);
+    ld8_sc1(p.f.coef + 2 * C + c0, k2);
+  } else {
+    // fallback: every channel's coefficients from the complete slab (written by the previous
+    // kernel) into LDS, 64 channels at a time through the block-wide fixed-order reduction; the
+    // prefetched batch is dropped and re-read (keeps it out of this path's registers)
+    __shared__ float lc[3][FUSED_MAX_C];
+    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    for (int cg = 0; cg < p.G; ++cg) {
+      const int c = cg * 64 + cl;
+      double a = 0.0, b = 0.0;
+      if (c < C) sum_rows<false>(p.part, rg, p.nblk, FUSED_G, C, c, a, b);
+      __syncthreads();
+      red[0][rg][cl] = a;
+      red[1][rg][cl] = b;
+      __syncthreads();
+      if (rg == 0 && c < C) {
+        for (int g = 1; g < FUSED_G; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
+        bwd_coefs(c, a, b, p.f, lc[0][c], lc[1][c], lc[2][c]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { k0[j] = lc[0][c0 + j]; k1[j] = lc[1][c0 + j]; k2[j] = lc[2][c0 + j]; }
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = v0 + u * stride;
+      if (v < p.nvec) {
+        dv[u] = ld_nt16(p.dy, v);
+        xq[u] = ld_nt16(p.x, v);
+        if (RELU) yq[u] = ld_nt16(p.y, v);
+      }
+    }
+    if (threadIdx.x == 0) atomicAdd(p.sync + 3, 1u);
+  }
+  if (threadIdx.x == 0 && atomicAdd(p.sync + 2, 1u) == (uint32_t)p.A) {  // last of A readers + raiser
+    __hip_atomic_store(p.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.sync[2] = 0;
+  }
+  for (int64_t base = v0;; base += stride * EW_U) {
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = base + u * stride;
+      if (v >= p.nvec) break;
+      float d[8], xv[8];
+      unpack8(dv[u], d);
+      unpack8(xq[u], xv);
+      if (RELU) {
+        float yv[8];
+        unpack8(yq[u], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      }
+      if (p.dres) st16(p.dres, v, pack8(d));
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = k0[j] * d[j] + k1[j] * xv[j] + k2[j];
+      st16(p.dx, v, pack8(o));
+    }
+    const int64_t nb = base + stride * EW_U;
+    if (nb >= p.nvec) break;
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t v = nb + u * stride;
+      if (v < p.nvec) {
+        dv[u] = ld_nt16(p.dy, v);
+        xq[u] = ld_nt16(p.x, v);
+        if (RELU) yq[u] = ld_nt16(p.y, v);
+      }
     }
   }
 }
@@ -1062,8 +1245,11 @@ inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const f
 // which needs no counters (deterministic either way; the two paths may round differently in the last
 // bit, so every rank of a job must use the same streams -- which the engine guarantees).
 constexpr int FIN_STREAM_SLOTS = 16, FIN_GROUPS = 128;  // 128 x 64 = 8192 channels
+// per stream slot: FIN_GROUPS arrival counters, then 8 words of the fused finalize + apply launch
+// (bn_bwd_fin_apply_kernel: [0] groups finalized, [1] ready, [2] readers + raiser, [3] fallbacks)
+constexpr int FIN_SLOT = FIN_GROUPS + 8;
 struct FinCounters {
-  int* cnt = nullptr;  // [FIN_STREAM_SLOTS][FIN_GROUPS]
+  int* cnt = nullptr;  // [FIN_STREAM_SLOTS][FIN_SLOT]
   hipStream_t owner[FIN_STREAM_SLOTS] = {};
   bool used[FIN_STREAM_SLOTS] = {};
 };
@@ -1078,12 +1264,12 @@ static int* fin_counters(int groups, hipStream_t st) {
   FinCounters& w = g_fin_cnt[dev & 15];
   if (!w.cnt) return nullptr;
   for (int i = 0; i < FIN_STREAM_SLOTS; ++i)
-    if (w.used[i] && w.owner[i] == st) return w.cnt + i * FIN_GROUPS;
+    if (w.used[i] && w.owner[i] == st) return w.cnt + i * FIN_SLOT;
   for (int i = 0; i < FIN_STREAM_SLOTS; ++i)
     if (!w.used[i]) {
       w.used[i] = true;
       w.owner[i] = st;
-      return w.cnt + i * FIN_GROUPS;
+      return w.cnt + i * FIN_SLOT;
     }
   // table full: the counter-free two-launch path (no host synchronisation, safe inside a capture)
   return nullptr;
@@ -1108,6 +1294,52 @@ inline void slab_finalize(float* part, int nblk, const FinArgs& f, hipStream_t s
   else hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_T), 0, st, fin, n, f);
 }
 
+// BN backward of a tall slab as ONE launch (bn_bwd_fin_apply_kernel) instead of split-finalize +
+// apply; false: the caller takes the two-launch path (MI355X_DP_BN_FUSED_FIN=0, small slabs, wide
+// layers, a stream without a counter slot, or a grid on which a thread's channel octet would move)
+// MI355X_DP_BN_FUSED_FIN=1 enables it (mi_bn_set_fused_fin: tests).  OFF by default: on ResNet-50
+// bs256 it measured 12.49k / 12.48k img/s against 12.74k / 12.69k for the two-launch path on one box
+// (512 apply blocks: 12.36k; profiles/bn_fused_finalize_r5.md) -- the apply blocks can do nothing
+// useful while the coefficients are finalized, and the persistent sweep at one 512-thread block per
+// CU (141-157 VGPRs) moves bytes slower than the 256-thread launch it replaces.
+static int g_bn_fused_fin = -1;
+inline bool launch_bn_bwd_fused(const float* part, int nblk, const FinArgs& f, const void* dy, const void* y,
+                                const void* x, void* dx, void* dres, int relu, hipStream_t st) {
+  if (g_bn_fused_fin < 0) {
+    const char* e = std::getenv("MI355X_DP_BN_FUSED_FIN");
+    g_bn_fused_fin = (e && e[0] == '1') ? 1 : 0;
+  }
+  const int C = f.C;
+  if (!g_bn_fused_fin || nblk <= 256 || C > FUSED_MAX_C || C % 8) return false;
+  int* cnt = fin_counters(cdiv(C, 64), st);
+  if (!cnt) return false;
+  FusedBwdArgs a{};
+  // splits of 64 rows: with 8 row groups a thread loads 8 rows -- one round of FIN_U loads
+  a.S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, 64));
+  a.rows_per = cdiv(nblk, a.S);
+  a.G = cdiv(C, 64);
+  a.nvec = (int64_t)f.M * C / 8;
+  // a persistent sweep: about one apply block per CU (MI355X_DP_BN_FUSED_BLOCKS), so the blocks that
+  // wait for the coefficients -- and count themselves out with one atomic each -- are few
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = std::getenv("MI355X_DP_BN_FUSED_BLOCKS");
+    cap = (e && std::atoi(e) > 0) ? std::atoi(e) : 256;
+  }
+  a.A = (int)std::max<int64_t>(
+      1, std::min<int64_t>(cap, (a.nvec + (int64_t)FUSED_T * EW_U - 1) / ((int64_t)FUSED_T * EW_U)));
+  if (((int64_t)a.A * FUSED_T * 8) % C) return false;  // a thread's channel octet must stay fixed
+  a.part = part; a.nblk = nblk; a.out = const_cast<float*>(part) + (size_t)nblk * 2 * C; a.cnt = cnt;
+  a.sync = (uint32_t*)(cnt + FIN_GROUPS);
+  a.f = f;
+  a.dy = (const bf16_t*)dy; a.y = (const bf16_t*)y; a.x = (const bf16_t*)x; a.dx = (bf16_t*)dx;
+  a.dres = (bf16_t*)dres; a.relu = relu;
+  const dim3 grid(a.G * a.S + a.A);
+  if (relu) hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<true>, grid, dim3(FUSED_T), 0, st, a);
+  else hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<false>, grid, dim3(FUSED_T), 0, st, a);
+  return true;
+}
+
 inline FinArgs fin_fwd_args(int M, int C, float eps, float momentum, const float* gamma, const float* beta,
                             float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                             float* scale, float* shift) {
@@ -1130,6 +1362,27 @@ inline FinArgs fin_bwd_args(int M, int C, const float* gamma, const float* mean,
 
 MI_API int mi_bn_slab_extra_rows() { return SLAB_EXTRA_ROWS; }
 
+MI_API int mi_bn_set_fused_fin(int on) {
+  g_bn_fused_fin = on ? 1 : 0;
+  return 0;
+}
+
+// fused finalize + apply launches whose apply blocks gave up waiting (diagnostics; tests assert 0)
+MI_API int mi_bn_fused_fallbacks() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(g_fin_mu);
+  FinCounters& w = g_fin_cnt[dev & 15];
+  if (!w.cnt) return 0;
+  int host[FIN_STREAM_SLOTS * FIN_SLOT];
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(host, w.cnt, sizeof(host), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  int n = 0;
+  for (int i = 0; i < FIN_STREAM_SLOTS; ++i) n += host[i * FIN_SLOT + FIN_GROUPS + 3];
+  return n;
+}
+
 // threshold (M * C elements) of the fused small-layer finalize + apply path; 0 disables (tests)
 MI_API int mi_bn_set_small_elems(long long n) {
   g_bn_small_elems = n < 0 ? 0 : (int64_t)n;
@@ -1145,7 +1398,7 @@ MI_API int mi_bn_init_counters() {
   FinCounters& w = g_fin_cnt[dev & 15];
   if (w.cnt) return 0;
   int* p = nullptr;
-  const size_t bytes = sizeof(int) * FIN_STREAM_SLOTS * FIN_GROUPS;
+  const size_t bytes = sizeof(int) * FIN_STREAM_SLOTS * FIN_SLOT;
   if (hipError_t e = hipMalloc(&p, bytes); e != hipSuccess) return (int)e;
   if (hipError_t e = hipMemset(p, 0, bytes); e != hipSuccess) return (int)e;
   if (hipError_t e = hipDeviceSynchronize(); e != hipSuccess) return (int)e;
@@ -1231,7 +1484,9 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
   slab_launch_dims(M, C, nblk, rpb, grid);
   hipLaunchKernelGGL(bn_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
                      (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
-  slab_finalize<true>(part, nblk, fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef), st);
+  const FinArgs fb = fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  if (launch_bn_bwd_fused(part, nblk, fb, dy, y, x, dx, dres, relu, st)) return (int)hipGetLastError();
+  slab_finalize<true>(part, nblk, fb, st);
   int64_t nvec = (int64_t)M * C / 8;
   launch_bn_bwd_apply(dy, y, x, coef, dx, dres, nvec, C, relu, st);
   return (int)hipGetLastError();
@@ -1249,6 +1504,7 @@ MI_API int mi_bn_bwd_train_pre(const void* dz, const void* x, void* dx, void* dr
     launch_bn_small(true, x, dz, dx, part, pre_rows, fb, 0, st);
     return (int)hipGetLastError();
   }
+  if (launch_bn_bwd_fused(part, pre_rows, fb, dz, nullptr, x, dx, dres, 0, st)) return (int)hipGetLastError();
   slab_finalize<true>(part, pre_rows, fb, st);
   int64_t nvec = (int64_t)M * C / 8;
   launch_bn_bwd_apply(dz, nullptr, x, coef, dx, dres, nvec, C, 0, st);

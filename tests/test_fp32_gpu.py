@@ -128,8 +128,8 @@ def _step_grads(model, x, y):
 def test_f32_resnet18_reference_step_matches_stock_fp32(fp32_mode):
     """The reference's training step (ResNet-18 with the 1000-class head, batch 32 at 32x32, the
     engine-backed DDP as the torch_smddp shim returns it): every one of the 62 parameter gradients
-    within 1e-4 relative error (max-abs over max-abs) of fp64 math on the same weights and batch,
-    and no further from it than stock fp32 PyTorch (MIOpen) on the GPU."""
+    within 1e-4 relative error (max-abs over max-abs) of stock fp32 PyTorch (MIOpen / rocBLAS) on the
+    same weights and batch, and no further from fp64 math than stock fp32 is."""
     from mi355x_dp.models import get_model
     from mi355x_dp.models.stock import stock_resnet
     from mi355x_dp.parallel import DataParallel
@@ -159,8 +159,12 @@ def test_f32_resnet18_reference_step_matches_stock_fp32(fp32_mode):
     worst = []
     for n in names:
         go = grads_o["module." + n] if "module." + n in grads_o else grads_o[n]
-        e_o, e_32 = rel(go, grads_64[n]), rel(grads_32[n], grads_64[n])
-        worst.append((e_o, n, e_32))
-        assert e_o < 1e-4, (n, e_o, e_32)
-        assert e_o <= max(2 * e_32, 1e-5), (n, e_o, e_32)
-    print("worst gradient errors (ours, stock fp32):", sorted(worst, reverse=True)[:3])
+        e_s, e_o, e_32 = rel(go, grads_32[n]), rel(go, grads_64[n]), rel(grads_32[n], grads_64[n])
+        worst.append((e_s, n, e_o, e_32))
+        # the verdict's bar: every gradient within 1e-4 of stock fp32 PyTorch
+        assert e_s < 1e-4, (n, e_s, e_o, e_32)
+        # and no further from fp64 math than stock fp32 is (the stem's weight gradient is ill-conditioned:
+        # both fp32 implementations sit ~3e-3 from fp64 there, within 1e-5 of each other)
+        assert e_o <= 1.5 * e_32 + 1e-5, (n, e_o, e_32)
+    print("worst gradient errors vs stock fp32 (ours-stock, ours-fp64, stock-fp64):",
+          sorted(worst, reverse=True)[:3])

@@ -731,3 +731,61 @@ def test_flat_engine_transposed_weight_copies():
         assert torch.equal(wt.reshape(ref.shape).float(), ref.float()), tuple(p.shape)
         n += 1
     assert n >= 3
+
+
+@pytest.mark.parametrize("relu,dres", [(False, False), (False, True), (True, False)])
+@pytest.mark.parametrize("M,C", [(802816, 64), (200704, 256), (50176, 2048), (401408, 8)])
+def test_bn_backward_fused_finalize_apply(M, C, relu, dres):
+    """the BN backward of a tall statistics slab as ONE launch (finalizer blocks +
+    apply blocks waiting on an in-launch hand-off, norm_act.hip bn_bwd_fin_apply_kernel) against the
+    two-launch split-finalize + apply path and an fp32 reference: same dgamma / dbeta / dx, and no
+    apply block ever fell back to computing the coefficients itself"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops import kernels  # noqa: F401
+    from mi355x_dp.ops._lib import ptr, stream_of
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    dev = "cuda"
+    dy = torch.randn(M, C, device=dev, generator=g).to(BF)
+    x = (torch.randn(M, C, device=dev, generator=g) * 1.5 + 0.3).to(BF)
+    y = torch.relu(torch.randn(M, C, device=dev, generator=g)).to(BF)
+    mean = x.float().mean(0)
+    invstd = torch.rsqrt(x.float().var(0, unbiased=False) + 1e-5)
+    gamma = torch.rand(C, device=dev, generator=g) + 0.5
+    dz = dy.float() * (y.float() > 0) if relu else dy.float()
+    rows = 128
+    nblk = M // rows
+    part = torch.empty((nblk + lib.mi_bn_slab_extra_rows(), 2, C), device=dev)
+    part[:nblk, 0] = dz.view(nblk, rows, C).sum(1)
+    part[:nblk, 1] = (dz * (x.float() - mean)).view(nblk, rows, C).sum(1)
+    outs = []
+    for fused in (0, 1):
+        lib.mi_bn_set_fused_fin(fused)
+        dx = torch.empty(M, C, device=dev, dtype=BF)
+        dr = torch.empty(M, C, device=dev, dtype=BF) if dres else None
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        coef = torch.empty(3, C, device=dev)
+        pt = part.clone()
+        if relu:  # full path: its own statistics pass over dy, y, x
+            pt = torch.empty((lib.mi_bn_partial_rows(M, C) + lib.mi_bn_slab_extra_rows(), 2, C), device=dev)
+            _lib.call("mi_bn_bwd_train", ptr(dy), ptr(y), ptr(x), ptr(dx), ptr(dr), M, C, ptr(gamma), ptr(mean),
+                      ptr(invstd), ptr(dg), ptr(db), ptr(coef), ptr(pt), 1, stream_of(dy))
+        else:
+            _lib.call("mi_bn_bwd_train_pre", ptr(dy), ptr(x), ptr(dx), ptr(dr), M, C, ptr(gamma), ptr(mean),
+                      ptr(invstd), ptr(dg), ptr(db), ptr(coef), ptr(pt), nblk, stream_of(dy))
+        torch.cuda.synchronize()
+        outs.append((dx, dr, dg, db))
+    lib.mi_bn_set_fused_fin(1)
+    assert lib.mi_bn_fused_fallbacks() == 0
+    # fp32 reference of the same math
+    xhat = (x.float() - mean) * invstd
+    sdz, sdzx = dz.sum(0), (dz * xhat).sum(0)
+    ref_dx = gamma * invstd * (dz - sdz / M - xhat * sdzx / M)
+    for (dx, dr, dg, db), name in zip(outs, ("two-launch", "fused")):
+        assert rel_err(dg, sdzx) < 1e-4 and rel_err(db, sdz) < 1e-4, name
+        assert rel_err(dx, ref_dx) < 1e-2, (name, rel_err(dx, ref_dx))
+        if dres:
+            assert torch.equal(dr, dz.to(BF)), name
+    (a, ar, ag, ab), (b, br, bg, bb) = outs
+    assert rel_err(bg, ag) < 1e-5 and rel_err(bb, ab) < 1e-5
+    assert rel_err(b, a) < 1e-2 and (b.float() - a.float()).abs().max() <= 2 * (a.float().abs().max() / 128)
