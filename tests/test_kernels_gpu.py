@@ -775,7 +775,7 @@ def test_bn_backward_fused_finalize_apply(M, C, relu, dres):
                       ptr(invstd), ptr(dg), ptr(db), ptr(coef), ptr(pt), nblk, stream_of(dy))
         torch.cuda.synchronize()
         outs.append((dx, dr, dg, db))
-    lib.mi_bn_set_fused_fin(1)
+    lib.mi_bn_set_fused_fin(0)  # the default (opt-in path)
     assert lib.mi_bn_fused_fallbacks() == 0
     # fp32 reference of the same math
     xhat = (x.float() - mean) * invstd
