@@ -76,6 +76,18 @@ __device__ __forceinline__ float att_exp2(float x) {
 #endif
 }
 
+// First 16-row tile of wave wv (it then takes every NW-th).  13 tiles (T = 197) cannot be dealt
+// evenly over a workgroup's 4 SIMDs (waves w and w + 4 share SIMD w % 4): one SIMD carries 4 tiles,
+// the others 3.  Rotating the deal by the (batch, head) index moves that heavy SIMD from workgroup
+// to workgroup, so two workgroups sharing a CU would mostly load different SIMDs (rot = 3,
+// MI355X_DP_ATT_ROTATE=1).  Measured: forward 0.115 ms either way, backward 0.263 vs 0.255 ms per
+// layer, ViT-B/16 6,999 / 6,998 vs 7,014 / 7,002 img/s (profiles/raw/r5/att_rot/) -- the fixed deal
+// (rot = 0) stays the default: the hardware does not place co-resident workgroups' waves as assumed.
+template <int NW>
+__device__ __forceinline__ int tile_start(int wv, int bh, int rot) {
+  return (wv + (bh & rot)) % NW;
+}
+
 template <int TP, int NW>
 __device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, int ld0, bf16_t* dst1,
                                             const bf16_t* src1, int ld1, int T) {
@@ -108,7 +120,8 @@ __device__ __forceinline__ void stage_rows2(bf16_t* dst0, const bf16_t* src0, in
 // per SIMD per workgroup.  Forward: always 4 (~210 VGPRs).
 template <int NK2, int NW>  // keys padded to 32 * NK2 >= T
 __global__ __launch_bounds__(64 * NW, NW / 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
-                                                          float* __restrict__ lse, int T, int H, float sl2) {
+                                                          float* __restrict__ lse, int T, int H, float sl2,
+                                                          int rot) {
   constexpr int TP = 32 * NK2, NKT = 2 * NK2;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * KSTR];
@@ -120,7 +133,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_fwd_kernel(const bf16_t*
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   const int nqt = (T + 15) >> 4;
-  for (int qt = wv; qt < nqt; qt += NW) {
+  for (int qt = tile_start<NW>(wv, bh, rot); qt < nqt; qt += NW) {
     const int q = qt * 16 + li;
     const bool qv = q < T;
     bf16x8 qf[2];
@@ -180,7 +193,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16
                                                              const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ lse,
                                                              float* __restrict__ dvec, bf16_t* __restrict__ dqkv,
-                                                             int T, int H, float sl2, float scale) {
+                                                             int T, int H, float sl2, float scale, int rot) {
   constexpr int TP = 32 * NK2;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * KSTR];
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   const int nqt = (T + 15) >> 4;
-  for (int qt = wv; qt < nqt; qt += NW) {
+  for (int qt = tile_start<NW>(wv, bh, rot); qt < nqt; qt += NW) {
     const int q = qt * 16 + li;
     const bool qv = q < T;
     const size_t orow = ((size_t)b * T + q) * D + h * HD;
@@ -258,7 +271,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dkv_kernel(const bf1
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ dvec,
                                                               bf16_t* __restrict__ dqkv, int T, int H, float sl2,
-                                                              float scale) {
+                                                              float scale, int rot) {
   constexpr int TP = 32 * NK2;
   __shared__ __attribute__((aligned(16))) bf16_t Qs[TP * KSTR];
   __shared__ __attribute__((aligned(16))) bf16_t Ds[TP * KSTR];
@@ -275,7 +288,7 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dkv_kernel(const bf1
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   const int nkt = (T + 15) >> 4;
-  for (int kt = wv; kt < nkt; kt += NW) {
+  for (int kt = tile_start<NW>(wv, bh, rot); kt < nkt; kt += NW) {
     const int key = kt * 16 + li;
     const bool kv = key < T;
     bf16x8 kf[2], vf[2];
@@ -353,6 +366,20 @@ static int att_waves() {
   return g_att_waves;
 }
 
+static int g_att_rot = -1;
+static int att_rot() {
+  if (g_att_rot < 0) {
+    const char* e = std::getenv("MI355X_DP_ATT_ROTATE");
+    g_att_rot = (e && e[0] == '1') ? 3 : 0;
+  }
+  return g_att_rot;
+}
+
+MI_API int mi_set_att_rotate(int on) {
+  g_att_rot = on ? 3 : 0;
+  return 0;
+}
+
 // backward workgroup size in waves (4 or 8): A/B runs in one process
 MI_API int mi_set_att_waves(int w) {
   g_att_waves = w == 4 ? 4 : 8;
@@ -366,7 +393,7 @@ MI_API int mi_attn_fwd(const void* qkv, void* o, float* lse, int B, int T, int H
   // forward: 4 waves (its 14 score tiles per q tile need ~210 VGPRs: 2 waves per SIMD)
 #define L(N)                                                                                             \
   hipLaunchKernelGGL((attn_fwd_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)o, \
-                     lse, T, H, sl2)
+                     lse, T, H, sl2, att_rot())
   MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
   return (int)hipGetLastError();
@@ -380,19 +407,20 @@ MI_API int mi_attn_bwd(const void* qkv, const void* o, const void* dout, const f
 #define L(N)                                                                                             \
   if (att_waves() == 8)                                                                                  \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<N, 8>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv,    \
-                       (const bf16_t*)o, (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale); \
+                       (const bf16_t*)o, (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale, att_rot()); \
   else                                                                                                   \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv,    \
-                       (const bf16_t*)o, (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
+                       (const bf16_t*)o, (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale,  \
+                       att_rot())
   MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
 #define L(N)                                                                                             \
   if (att_waves() == 8)                                                                                  \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<N, 8>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv,   \
-                       (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale);                  \
+                       (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale, att_rot());       \
   else                                                                                                   \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv,   \
-                       (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale)
+                       (const bf16_t*)dout, lse, dvec, (bf16_t*)dqkv, T, H, sl2, scale, att_rot())
   MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
   return (int)hipGetLastError();
