@@ -371,6 +371,15 @@ def main(argv=None):
             if cuda:
                 torch.cuda.empty_cache()
             smddp_job = run_child_bench(world, args, "smddp")
+    secondary = None
+    if (rank == 0 and world == 1 and cuda and args.model == "resnet50" and not args.force_comm
+            and os.environ.get("MI355X_DP_BENCH_SECONDARY", "1") == "1"):
+        # after the timed region, each as its own process: the other BASELINE.json configs' models
+        # (ResNet-152, ViT-B/16, same per-GPU batch) on this same box, so every driver run records
+        # them too -- a failure or timeout there cannot cost the headline measurement
+        torch.cuda.empty_cache()
+        secondary = {m: run_child_bench(1, args, args.backend, model=m, timeout_s=180)
+                     for m in ("resnet152", "vit_b_16")}
     ipc_probe = None
     if (rank == 0 and world > 1 and cuda and world <= torch.cuda.device_count()
             and os.environ.get("MI355X_DP_BENCH_IPC_PROBE", "1") == "1"):
@@ -422,6 +431,7 @@ def main(argv=None):
             "comm_probe": comm_probe,
             "ipc_probe": ipc_probe,
             "smddp_job": smddp_job,
+            "secondary_models": secondary,
             # GPU event times (ms from the forward's start) of one step after the timed region
             "comm_timeline": comm_timeline,
             "bucket_launch_ms": comm_timeline["buckets"] if comm_timeline else None,
@@ -465,10 +475,11 @@ def _child_env():
     return env
 
 
-def run_child_bench(world: int, args, backend: str, timeout_s: int = 150):
+def run_child_bench(world: int, args, backend: str, timeout_s: int = 150, model: str = None):
     """``bench.py`` again as a fresh N-rank job (native launcher) through ``backend``, a few steps of
-    the same configuration, started by rank 0 after the benchmark finished (a failure cannot cost
-    the measurement).  Returns its img/s, ranks seen, backend, replica check and step time."""
+    the same configuration (or of ``model``), started by rank 0 after the benchmark finished (a
+    failure cannot cost the measurement).  Returns its img/s, ranks seen, backend, replica check and
+    step time."""
     from mi355x_dp.launch import NATIVE_LAUNCHER, free_port
     if not os.path.exists(NATIVE_LAUNCHER):
         return "skipped: native launcher not built"
@@ -476,13 +487,16 @@ def run_child_bench(world: int, args, backend: str, timeout_s: int = 150):
     env["MI355X_DP_BENCH_SMDDP_JOB"] = "0"   # no nested child jobs
     env["MI355X_DP_BENCH_IPC_PROBE"] = "0"
     env["MI355X_DP_BENCH_COMM_PROBE"] = "0"
+    env["MI355X_DP_BENCH_SECONDARY"] = "0"
     env["MI355X_DP_BENCH_SPAWNED"] = "native"
     steps = max(1, min(args.steps, int(os.environ.get("MI355X_DP_BENCH_SMDDP_STEPS", "10"))))
+    # a secondary model keeps its own wgrad-stream policy (auto: off for the GEMM-bound ViT)
+    wgs = "auto" if model else str(args.wgrad_stream)
     cmd = [NATIVE_LAUNCHER, "--nproc", str(world), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            "--", sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--steps", str(steps),
-           "--warmup", str(min(max(args.warmup, 1), 3)), "--model", args.model, "--batch", str(args.batch),
+           "--warmup", str(min(max(args.warmup, 1), 3)), "--model", model or args.model, "--batch", str(args.batch),
            "--image-size", str(args.image_size), "--num-classes", str(args.num_classes), "--backend", backend,
-           "--device", args.device, "--grad-comm", args.grad_comm, "--wgrad-stream", str(args.wgrad_stream)]
+           "--device", args.device, "--grad-comm", args.grad_comm, "--wgrad-stream", wgs]
     if args.shard_optimizer:
         cmd.append("--shard-optimizer")
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -499,10 +513,11 @@ def run_child_bench(world: int, args, backend: str, timeout_s: int = 150):
     for line in out.splitlines():
         if _is_result(line):
             d = json.loads(line)
-            return {"backend": d["config"]["backend"], "comm_library": d["config"]["comm_library"],
-                    "img_s": d["value"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
-                    "ranks_seen": d["ranks_seen"], "replicas_identical": d["replicas_identical"],
-                    "buckets": d["config"]["buckets"]}
+            return {"model": d["config"]["model"], "backend": d["config"]["backend"],
+                    "comm_library": d["config"]["comm_library"], "img_s": d["value"],
+                    "ms_per_step": d["ms_per_step"], "steps": d["steps"], "warmup": d["warmup"],
+                    "per_gpu_batch": d["config"]["per_gpu_batch"], "ranks_seen": d["ranks_seen"],
+                    "replicas_identical": d["replicas_identical"], "buckets": d["config"]["buckets"]}
     return f"failed: rc={proc.returncode}: {(err or out)[-400:]}"
 
 

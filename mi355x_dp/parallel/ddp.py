@@ -784,6 +784,22 @@ class DataParallel(nn.Module):
         t0.record()
         return {"t0": t0, "gates": [], "end": None}
 
+    def _smddp_comm_stream(self):
+        """the native smddp backend's comm stream (a torch ExternalStream), or None"""
+        if "_smddp_cs" not in self.__dict__:
+            cs = None
+            try:
+                from . import comm_paths
+                mod = comm_paths._native()
+                pg = self.process_group if self.process_group is not None else dist.distributed_c10d._get_default_group()
+                if mod is not None and str(dist.get_backend(pg)) == "smddp":
+                    h = int(mod.comm_stream(comm_paths.backend_of(pg)))
+                    cs = torch.cuda.ExternalStream(h, device=self.flat.grad.device)
+            except Exception:
+                cs = None
+            self._smddp_cs = cs
+        return self._smddp_cs
+
     def _gated_launch(self, step, target, trace=None):
         """BEFORE a replay of a captured backward (comm_mode "gates"): per bucket b, in order, a gate
         kernel on the high-priority gate stream that waits until the graph's bump of b reaches
@@ -792,7 +808,11 @@ class DataParallel(nn.Module):
         behind that gate, i.e. behind exactly b's gradient kernels."""
         from .step_graph import BucketGates
         BucketGates.check()
-        gs = self._gate_stream()
+        # the native smddp backend (the IPC collectives that take this path): gates straight on its
+        # comm stream, each collective issued from that stream too -- its producer event, any bf16
+        # cast and the collective all follow the gate in one in-order stream, and no second stream
+        # can share a hardware queue with it; otherwise the high-priority gate stream
+        gs = self._smddp_comm_stream() or self._gate_stream()
         gs.wait_stream(torch.cuda.current_stream(gs.device))  # the previous step's users of the buckets
         with torch.cuda.stream(gs):
             for b, idxs in enumerate(self.buckets):

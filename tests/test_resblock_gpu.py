@@ -108,7 +108,7 @@ def test_fused_block_used_in_training():
     from mi355x_dp.ops import resblock
     m = get_model("resnet50").cuda()
     x = torch.randn(2, 3, 64, 64, device="cuda")
-    assert R.FUSED_BLOCKS and resblock.fusable(m.layer1[0], torch.empty(1, device="cuda"))
+    assert R.FUSED_BLOCKS and resblock.fusable(m.layer1[0], torch.empty(1, device="cuda", dtype=torch.bfloat16))
     out = m.layer1[0](m.maxpool(R.conv_bn(m.conv1, m.bn1, R.to_device_input(x), relu=True)))
     assert type(out.grad_fn).__name__.startswith("_ResBlock")
 

@@ -37,7 +37,11 @@ def run(mode):
     step_graph.MODE = mode
     torch.manual_seed(0)
     model = get_model("resnet18", num_classes=1000).cuda()
-    ddp = torch.nn.parallel.DistributedDataParallel(model)
+    # GRAPHED_BCAST=0: no BN-buffer broadcast (its IPC kernel waits for the peer rank, which -- two
+    # ranks time-slicing one GPU -- can lag by milliseconds and holds the comm stream in front of the
+    # first gate; the gate-timing run measures the gates, not the peer's skew)
+    ddp = torch.nn.parallel.DistributedDataParallel(
+        model, broadcast_buffers=os.environ.get("GRAPHED_BCAST", "1") != "0")
     assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
     opt = torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
     crit = torch.nn.CrossEntropyLoss().cuda()
