@@ -38,12 +38,16 @@ def batches(steps, batch, seed=0):
     return [(x[i * batch:(i + 1) * batch], y[i * batch:(i + 1) * batch]) for i in range(steps)]
 
 
-def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1, data_seed=0):
+def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1, data_seed=0, fp32=False):
+    """``fp32``: the engine in its fp32 compute mode (MI355X_DP_COMPUTE_DTYPE=fp32, ops/fp32.py)"""
     from mi355x_dp.models import get_model
     from mi355x_dp.models.stock import stock_resnet
+    from mi355x_dp.ops import fp32 as f32mode
     from mi355x_dp.parallel import DataParallel
     dev = torch.device("cuda", 0)
     data = batches(steps, batch, data_seed)
+    prev_mode = f32mode.COMPUTE_FP32
+    f32mode.COMPUTE_FP32 = bool(fp32) or prev_mode
     torch.manual_seed(seed)  # the reference seeds before building the model (gpu.py:120)
     ours = get_model("resnet18", num_classes=1000).to(dev)
     init = {k: v.detach().clone() for k, v in ours.state_dict().items()}
@@ -59,6 +63,7 @@ def run(steps=150, batch=32, lr=0.01, momentum=0.9, seed=1, data_seed=0):
         opt.step()
         ours_loss.append(float(loss))
     graphed = sum(s.replays for s in getattr(eng, "_graphs", {}).values())
+    f32mode.COMPUTE_FP32 = prev_mode
 
     ref = stock_resnet("resnet18", 1000).to(dev)
     ref.load_state_dict(init)
@@ -81,14 +86,14 @@ def windows(v, k=10):
     return [float(np.mean(v[i:i + k])) for i in range(0, len(v) - k + 1, k)]
 
 
-def run_seeds(steps=150, seeds=(1, 2, 3)):
+def run_seeds(steps=150, seeds=(1, 2, 3), fp32=False):
     """``run`` for several (init, data) seeds: the per-step losses averaged over the seeds, for ours
     and for the stock fp32 reference, plus the graphed step count.  A single bf16-vs-fp32 pair of
     150-step SGD trajectories diverges chaotically (and the fp32 reference is itself not run-to-run
     deterministic on the GPU); the mean over independent seeds is what a tolerance can pin."""
     ours, ref, graphed = [], [], []
     for sd in seeds:
-        o, r, g = run(steps, seed=sd, data_seed=sd - 1)
+        o, r, g = run(steps, seed=sd, data_seed=sd - 1, fp32=fp32)
         ours.append(o)
         ref.append(r)
         graphed.append(g)
