@@ -340,6 +340,159 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dkv_kernel(const bf1
   }
 }
 
+// Backward in ONE kernel per (batch, head): the dQ pass and the dK/dV pass of the two kernels above
+// share a workgroup, so every operand is read from HBM once instead of twice.
+//   stage K, V (LDS X0, X1) and the LSE
+//   pass 1 (per q tile, as attn_bwd_dq_kernel): Q / dO / O fragments from global, D = rowsum(dO*O)
+//          into LDS (never to global), dQ
+//   each wave copies the K / V fragments of its (<= 2) key tiles from LDS into registers, then
+//   X0, X1 are restaged with Q, dO (the rows pass 1 just read: L2 / MALL hits)
+//   pass 2 (per key tile, as attn_bwd_dkv_kernel): dK, dV
+// 8 waves, 66 KB of LDS at T <= 224, <= 128 VGPRs (launch bound: 4 waves per SIMD): two workgroups
+// per CU, one's staging under the other's MFMAs.
+template <int NK2>
+__global__ __launch_bounds__(512, 4) void attn_bwd_fused_kernel(const bf16_t* __restrict__ qkv,
+                                                              const bf16_t* __restrict__ o,
+                                                              const bf16_t* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              bf16_t* __restrict__ dqkv, int T, int H, float sl2,
+                                                              float scale) {
+  constexpr int NW = 8;
+  constexpr int TP = 32 * NK2;
+  __shared__ __attribute__((aligned(16))) bf16_t X0[TP * KSTR];
+  __shared__ __attribute__((aligned(16))) bf16_t X1[TP * KSTR];
+  __shared__ float Ls[TP], Dv[TP];
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
+  const bf16_t* dbase = dout + (size_t)b * T * D + h * HD;
+  stage_rows2<TP, NW>(X0, base + D, ld, X1, base + 2 * D, ld, T);
+  for (int i = threadIdx.x; i < TP; i += 64 * NW) {
+    Ls[i] = i < T ? lse[(size_t)bh * T + i] * LOG2E : INFINITY;  // padded queries: P = 0
+    Dv[i] = 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  const int nt = (T + 15) >> 4;
+
+  // ---- pass 1: dQ (K = X0, V = X1)
+  for (int qt = wv; qt < nt; qt += NW) {
+    const int q = qt * 16 + li;
+    const bool qv = q < T;
+    const size_t orow = ((size_t)b * T + q) * D + h * HD;
+    bf16x8 qf[2], df[2];
+    float dd = 0.f;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      qf[h2] = qv ? g16(base + (size_t)q * ld + 32 * h2 + 8 * g) : zero8();
+      df[h2] = qv ? g16(dout + orow + 32 * h2 + 8 * g) : zero8();
+      const bf16x8 of = qv ? g16(o + orow + 32 * h2 + 8 * g) : zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dd += (float)df[h2][j] * (float)of[j];
+    }
+    dd += __shfl_xor(dd, 16, 64);
+    dd += __shfl_xor(dd, 32, 64);
+    const float l2 = Ls[q];  // q < nt * 16 <= TP
+    if (qv && g == 0) Dv[q] = dd;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int ks = 0; ks < NK2; ++ks) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int kt = 2 * ks + t;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          s = mfma(*(const bf16x8*)&X0[(kt * 16 + li) * KSTR + 32 * h2 + 8 * g], qf[h2], s);
+          dp = mfma(*(const bf16x8*)&X1[(kt * 16 + li) * KSTR + 32 * h2 + 8 * g], df[h2], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool valid = qv && (kt * 16 + 4 * g + r < T);
+          const float e = att_exp2(s[r] * sl2 - l2);
+          ds[t][r] = (valid ? e : 0.f) * (dp[r] - dd);
+        }
+      }
+      const bf16x8 sb = pack_perm(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = mfma(tr8(X0, ks * 32 + 4 * g + q4, ks * 32 + 16 + 4 * g + q4, (dt * 4 + p4) * 4), sb, dq[dt]);
+    }
+    if (qv) {
+      bf16_t* drow = dqkv + ((size_t)b * T + q) * ld + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4bf(drow + dt * 16 + 4 * g, dq[dt], scale);
+    }
+  }
+
+  // ---- hand-over: this wave's key tiles (wv, wv + NW; nt <= 16) to registers, then Q / dO staged
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int row = min(wv + NW * j, nt - 1) * 16 + li;  // rows >= T are zero in the staged tiles
+      kf[j][h2] = *(const bf16x8*)&X0[row * KSTR + 32 * h2 + 8 * g];
+      vf[j][h2] = *(const bf16x8*)&X1[row * KSTR + 32 * h2 + 8 * g];
+    }
+  __syncthreads();
+  stage_rows2<TP, NW>(X0, base, ld, X1, dbase, D, T);
+  __syncthreads();
+
+  // ---- pass 2: dK, dV (Q = X0, dO = X1)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kt = wv + NW * j;
+    if (kt >= nt) break;
+    const int key = kt * 16 + li;
+    const bool kv = key < T;
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
+#pragma unroll 1
+    for (int qs = 0; qs < NK2; ++qs) {
+      f32x4 P[2], S[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int row = (2 * qs + t) * 16 + li;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          s = mfma(*(const bf16x8*)&X0[row * KSTR + 32 * h2 + 8 * g], kf[j][h2], s);
+          dp = mfma(*(const bf16x8*)&X1[row * KSTR + 32 * h2 + 8 * g], vf[j][h2], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = (2 * qs + t) * 16 + 4 * g + r;
+          const float e = att_exp2(s[r] * sl2 - Ls[qq]);
+          const float p = kv ? e : 0.f;
+          P[t][r] = p;
+          S[t][r] = p * (dp[r] - Dv[qq]);
+        }
+      }
+      const bf16x8 pb = pack_perm(P[0], P[1]), sb = pack_perm(S[0], S[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int r0 = qs * 32 + 4 * g + q4, r1 = r0 + 16, col = (dt * 4 + p4) * 4;
+        dv[dt] = mfma(tr8(X1, r0, r1, col), pb, dv[dt]);
+        dk[dt] = mfma(tr8(X0, r0, r1, col), sb, dk[dt]);
+      }
+    }
+    if (kv) {
+      bf16_t* drow = dqkv + ((size_t)b * T + key) * ld + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store4bf(drow + D + dt * 16 + 4 * g, dk[dt], scale);
+        store4bf(drow + 2 * D + dt * 16 + 4 * g, dv[dt], 1.f);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 #define MI_ATT_SWITCH(NK2, LAUNCH)                                                                       \
@@ -399,11 +552,34 @@ MI_API int mi_attn_fwd(const void* qkv, void* o, float* lse, int B, int T, int H
   return (int)hipGetLastError();
 }
 
-// dout [B*T][H*64]; dqkv [B*T][3*H*64] fully written; dvec [B*H][T] fp32 scratch
+static int g_att_fused = -1;
+static int att_fused() {
+  if (g_att_fused < 0) {
+    const char* e = std::getenv("MI355X_DP_ATT_FUSED_BWD");
+    g_att_fused = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_att_fused;
+}
+
+// backward schedule: 1 = one fused kernel (default), 0 = the dQ and dK/dV kernels (A/B runs)
+MI_API int mi_set_att_fused_bwd(int on) {
+  g_att_fused = on ? 1 : 0;
+  return 0;
+}
+
+// dout [B*T][H*64]; dqkv [B*T][3*H*64] fully written; dvec [B*H][T] fp32 scratch (two-kernel path)
 MI_API int mi_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse, float* dvec, void* dqkv,
                        int B, int T, int H, float scale, hipStream_t st) {
   if (T <= 0 || T > 256 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
   const float sl2 = scale * LOG2E;
+  if (att_fused() && T <= 224) {  // 2 x 66 KB of LDS per CU at T <= 224
+#define L(N)                                                                                             \
+  hipLaunchKernelGGL((attn_bwd_fused_kernel<N>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv,        \
+                     (const bf16_t*)o, (const bf16_t*)dout, lse, (bf16_t*)dqkv, T, H, sl2, scale)
+    MI_ATT_SWITCH((T + 31) / 32, L)
+#undef L
+    return (int)hipGetLastError();
+  }
 #define L(N)                                                                                             \
   if (att_waves() == 8)                                                                                  \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<N, 8>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv,    \

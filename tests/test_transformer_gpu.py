@@ -154,6 +154,28 @@ def test_attention_fwd_bwd(B, T, H):
             assert rel_err(dq[:, i], dr[:, i]) < 4e-2, name
 
 
+@pytest.mark.parametrize("B,T,H", [(2, 197, 12), (3, 17, 2), (2, 224, 3), (4, 1, 1)])
+def test_attention_fused_bwd_matches_two_kernels(B, T, H):
+    """The single-kernel backward (dQ pass, then dK/dV pass in the same workgroup) against the dQ +
+    dK/dV kernel pair: the same MFMA / exp sequence per element, so bit-identical."""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops import transformer as Tm
+    D = H * 64
+    qkv = rnd(B * T, 3 * D, scale=1.5)
+    do = rnd(B * T, D)
+    grads = []
+    try:
+        for fused in (1, 0):
+            _lib.call("mi_set_att_fused_bwd", fused)
+            x = qkv.clone().requires_grad_()
+            Tm.attention(x, B, T, H).backward(do)
+            torch.cuda.synchronize()
+            grads.append(x.grad.clone())
+    finally:
+        _lib.call("mi_set_att_fused_bwd", 1)
+    assert torch.equal(grads[0], grads[1])
+
+
 def test_vit_native_matches_cpu_fp32():
     """The GPU ViT step -- native token embedding (class token + position embedding in one pass,
     fixed-order batch sums in backward) and the class-token-only final LayerNorm -- against the same

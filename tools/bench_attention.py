@@ -54,17 +54,19 @@ def main():
     def bwd():
         _lib.call("mi_attn_bwd", ptr(qkv), ptr(o), ptr(do), ptr(lse), ptr(dvec), ptr(dqkv), B, T, H, scale, st)
     fwd()
-    res = {"fwd": [], "bwd4": [], "bwd8": [], "fwd_fixed": [], "bwd8_fixed": []}
+    res = {"fwd": [], "bwd_fused": [], "bwd4": [], "bwd8": [], "fwd_rot": []}
     for _ in range(a.rounds):
         res["fwd"].append(timeit(fwd))
+        res["bwd_fused"].append(timeit(bwd))       # default: the single-kernel backward
+        _lib.call("mi_set_att_fused_bwd", 0)      # the dQ + dK/dV kernel pair (A/B)
         _lib.call("mi_set_att_waves", 4)
         res["bwd4"].append(timeit(bwd))
         _lib.call("mi_set_att_waves", 8)
         res["bwd8"].append(timeit(bwd))
-        _lib.call("mi_set_att_rotate", 0)  # the fixed tile deal (A/B)
-        res["fwd_fixed"].append(timeit(fwd))
-        res["bwd8_fixed"].append(timeit(bwd))
-        _lib.call("mi_set_att_rotate", 1)
+        _lib.call("mi_set_att_fused_bwd", 1)
+        _lib.call("mi_set_att_rotate", 1)         # the rotated tile deal (A/B)
+        res["fwd_rot"].append(timeit(fwd))
+        _lib.call("mi_set_att_rotate", 0)
     # reference: the same layout through SDPA (time only)
     q, k, v = qkv.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
     q, k, v = (t.contiguous().requires_grad_() for t in (q, k, v))
@@ -77,14 +79,13 @@ def main():
     t = {k: statistics.median(v) for k, v in res.items()}
     print(f"| op | ms per layer | TF/s |\n|---|---:|---:|")
     print(f"| forward | {t['fwd']:.3f} | {fl_f / t['fwd'] / 1e9:.0f} |")
-    print(f"| backward, 4 waves | {t['bwd4']:.3f} | {2.5 * fl_f / t['bwd4'] / 1e9:.0f} |")
-    print(f"| backward, 8 waves | {t['bwd8']:.3f} | {2.5 * fl_f / t['bwd8'] / 1e9:.0f} |")
+    print(f"| backward, one fused kernel (default) | {t['bwd_fused']:.3f} | {2.5 * fl_f / t['bwd_fused'] / 1e9:.0f} |")
+    print(f"| backward, dQ + dK/dV kernels, 4 waves | {t['bwd4']:.3f} | {2.5 * fl_f / t['bwd4'] / 1e9:.0f} |")
+    print(f"| backward, dQ + dK/dV kernels, 8 waves | {t['bwd8']:.3f} | {2.5 * fl_f / t['bwd8'] / 1e9:.0f} |")
     print(f"| torch SDPA fwd+bwd | {t_sdpa:.3f} | {3.5 * fl_f / t_sdpa / 1e9:.0f} |")
-    print(f"| forward, fixed tile deal | {t['fwd_fixed']:.3f} | {fl_f / t['fwd_fixed'] / 1e9:.0f} |")
-    print(f"| backward 8 waves, fixed tile deal | {t['bwd8_fixed']:.3f} | {2.5 * fl_f / t['bwd8_fixed'] / 1e9:.0f} |")
-    print(f"12 layers: fwd + bwd(8 waves) = {12 * (t['fwd'] + t['bwd8']):.2f} ms/step "
-          f"(4 waves: {12 * (t['fwd'] + t['bwd4']):.2f})")
-
+    print(f"| forward, rotated tile deal | {t['fwd_rot']:.3f} | {fl_f / t['fwd_rot'] / 1e9:.0f} |")
+    print(f"12 layers: fwd + bwd(fused) = {12 * (t['fwd'] + t['bwd_fused']):.2f} ms/step "
+          f"(two kernels, 8 waves: {12 * (t['fwd'] + t['bwd8']):.2f})")
 
 if __name__ == "__main__":
     main()

@@ -2,7 +2,8 @@
 """A/B of the ViT-B/16 weight-gradient GEMMs (batch 256: K = 50,432 tokens), fp32 gradient
 accumulated into an existing buffer plus the bias gradient, in one process with interleaved
 rounds: the native split-K TN kernel with the fused column sums (mi_gemm_tn_bias) vs the library
-GEMM (torch.addmm with out_dtype=float32 -> hipBLASLt, accumulating in place) + mi_colsum_bf16.
+GEMM (torch.addmm with out_dtype=float32 -> hipBLASLt, accumulating in place) + mi_colsum_bf16,
+and the native 256x256 TN kernel (mi_gemm256_tn, fp32 atomics across its K splits) + mi_colsum_bf16.
 
     python tools/bench_vit_wgrad.py [--batch 256] [--rounds 5]
 """
@@ -41,8 +42,9 @@ def main():
     T = a.batch * 197
     # (name, out features N, in features K): dW[N][K] = dY[T][N]^T X[T][K]
     shapes = [("qkv", 2304, 768), ("proj", 768, 768), ("fc1", 3072, 768), ("fc2", 768, 3072)]
-    print(f"| shape | T N K | native TN+colsum ms (TF/s) | hipBLASLt addmm + colsum ms (TF/s) | max rel diff |")
-    print("|---|---|---:|---:|---:|")
+    print("| shape | T N K | native TN+colsum ms (TF/s) | hipBLASLt addmm + colsum ms (TF/s) | "
+          "gemm256_tn + colsum ms (TF/s) | max rel diff (TN, 256) |")
+    print("|---|---|---:|---:|---:|---:|")
     for name, N, K in shapes:
         g = torch.Generator(device="cuda").manual_seed(0)
         dy = (torch.rand(T, N, device="cuda", generator=g) * 2 - 1).to(BF)
@@ -51,6 +53,8 @@ def main():
         gb1 = torch.zeros(N, device="cuda")
         gw2 = torch.zeros(N, K, device="cuda")
         gb2 = torch.zeros(N, device="cuda")
+        gw3 = torch.zeros(N, K, device="cuda")
+        gb3 = torch.zeros(N, device="cuda")
 
         def native():
             _lib.call("mi_gemm_tn_bias", ptr(dy), ptr(x), ptr(gw1), ptr(gb1), N, K, T, N, K, K, stream_of(dy))
@@ -59,17 +63,23 @@ def main():
             torch.addmm(gw2, dy.t(), x, out_dtype=torch.float32, out=gw2)
             _lib.call("mi_colsum_bf16", ptr(dy), ptr(gb2), T, N, N, stream_of(dy))
 
-        native(); library()
+        def g256():
+            _lib.call("mi_gemm256_tn", ptr(dy), ptr(x), ptr(gw3), N, K, T, N, K, K, stream_of(dy))
+            _lib.call("mi_colsum_bf16", ptr(dy), ptr(gb3), T, N, N, stream_of(dy))
+
+        native(); library(); g256()
         torch.cuda.synchronize()
         diff = float((gw1 - gw2).abs().max() / gw2.abs().max())
-        tn, tl = [], []
+        diff3 = float((gw3 - gw2).abs().max() / gw2.abs().max())
+        tn, tl, t3 = [], [], []
         for _ in range(a.rounds):
             tn.append(timeit(native))
             tl.append(timeit(library))
-        mn, ml = statistics.median(tn), statistics.median(tl)
+            t3.append(timeit(g256))
+        mn, ml, m3 = statistics.median(tn), statistics.median(tl), statistics.median(t3)
         fl = 2.0 * T * N * K
-        print(f"| {name} | {T} {N} {K} | {mn:.3f} ({fl / mn / 1e9:.0f}) | {ml:.3f} ({fl / ml / 1e9:.0f}) | {diff:.1e} |",
-              flush=True)
+        print(f"| {name} | {T} {N} {K} | {mn:.3f} ({fl / mn / 1e9:.0f}) | {ml:.3f} ({fl / ml / 1e9:.0f}) | "
+              f"{m3:.3f} ({fl / m3 / 1e9:.0f}) | {diff:.1e} / {diff3:.1e} |", flush=True)
 
 
 if __name__ == "__main__":
