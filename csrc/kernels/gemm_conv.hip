@@ -1076,13 +1076,25 @@ void tn_kernel(TNArgs a) {
     }
   }
 
+  // bias gradient first (the split-K epilogues below may return early): every column of the
+  // ones-product holds the column sum; lane li == 0 adds it
+  if constexpr (CS) if (do_cs && li == 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + 16 * i + 4 * g + r;
+        if (m < a.M) atomicAdd(a.colsum + m, acc_cs[i][r]);
+      }
+  }
+
   // epilogue: lane holds D[m = 16i + 4g + r][n = 16j + li]
   const bool single = (nsplit == 1);
   if (!single && a.ws) {
     // split-K: this block's partial tile goes to its own slab in fragment order -- every store is one
     // fully coalesced 1 KB wave-instruction (64 lanes x float4) -- and tn_splitk_reduce_kernel sums
     // the splits into C: deterministic, and no fp32 atomics (~1.3 TB/s chip-wide) on the hot path
-    if (STAGES == 1 && !CS && a.cnt) {  // GLDS (default) slab variants only (no colsum: no slabs there)
+    if (STAGES == 1 && a.cnt) {  // GLDS (default) slab variants only
       // one launch: fence-free hand-off to the last-arriving split of the tile (as nt_kernel's
       // SPLIT 3): sc1 partial stores, wait, barrier, one arrival count; the last arriver sums the
       // partials in split order from 0 -- what tn_splitk_reduce_kernel does for fewer than 8
@@ -1168,15 +1180,6 @@ void tn_kernel(TNArgs a) {
         }
       }
     }
-  }
-  if constexpr (CS) if (do_cs && li == 0) {  // every column of the ones-product holds the sum; lane li == 0 adds it
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + 16 * i + 4 * g + r;
-        if (m < a.M) atomicAdd(a.colsum + m, acc_cs[i][r]);
-      }
   }
 }
 
@@ -1629,7 +1632,10 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   if (a.a_bytes <= 0 || a.b_bytes <= 0) return hipErrorInvalidValue;  // operand > 2 GiB: split the batch
   a.ws = nullptr;
   a.cnt = nullptr;
-  if (splits > 1 && a.colsum == nullptr && tn_slabs_on())
+  // split-K partials through slabs (deterministic), the Linear weight gradients with their fused
+  // bias column sums included: fp32 atomics there cost ~37 us per ViT-B/16 weight gradient, all of
+  // it after the last k-step (every split block finishes in the same wave)
+  if (splits > 1 && tn_slabs_on())
     a.ws = splitk_workspace((size_t)tiles * splits * BM * BN, st);
   // fewer than 8 splits: the reduce is one split group (in-order sum), which the last-arriving
   // split runs itself -- no reduce launch; more splits keep the chip-wide reduce kernel

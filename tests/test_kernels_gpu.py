@@ -789,3 +789,36 @@ def test_bn_backward_fused_finalize_apply(M, C, relu, dres):
     (a, ar, ag, ab), (b, br, bg, bb) = outs
     assert rel_err(bg, ag) < 1e-5 and rel_err(bb, ab) < 1e-5
     assert rel_err(b, a) < 1e-2 and (b.float() - a.float()).abs().max() <= 2 * (a.float().abs().max() / 128)
+
+
+@pytest.mark.parametrize("T,N,K", [(2048, 2304, 768), (3000, 768, 768)])
+def test_tn_bias_splitk_slabs(T, N, K):
+    """Linear weight + bias gradient (mi_gemm_tn_bias) with K splits through partial slabs -- the
+    last-arriving split's in-launch sum (7 splits) or the reduce launch (21 splits) -- instead of fp32
+    atomics: fused and unfused reductions bit-identical, and all three paths match fp32."""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    lib = _lib.load(True)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dy = (torch.rand(T, N, device="cuda", generator=g) * 2 - 1).to(BF)
+    x = (torch.rand(T, K, device="cuda", generator=g) * 2 - 1).to(BF)
+    gw0 = torch.randn(N, K, device="cuda", generator=g)
+    gb0 = torch.randn(N, device="cuda", generator=g)
+    ref_w = gw0 + dy.float().t() @ x.float()
+    ref_b = gb0 + dy.float().sum(0)
+    out = {}
+    try:
+        for name, slabs, fused in (("slab", 1, 0), ("slab_fused", 1, 1), ("atomic", 0, 0)):
+            lib.mi_set_tn_slabs(slabs)
+            lib.mi_set_tn_split_fused(fused)
+            gw, gb = gw0.clone(), gb0.clone()
+            _lib.call("mi_gemm_tn_bias", ptr(dy), ptr(x), ptr(gw), ptr(gb), N, K, T, N, K, K, stream_of(dy))
+            torch.cuda.synchronize()
+            out[name] = (gw, gb)
+    finally:
+        lib.mi_set_tn_slabs(1)
+        lib.mi_set_tn_split_fused(0)
+    assert torch.equal(out["slab"][0], out["slab_fused"][0])
+    for name, (gw, gb) in out.items():
+        assert rel_err(gw, ref_w) < 1e-4, name
+        assert rel_err(gb, ref_b) < 1e-4, name
