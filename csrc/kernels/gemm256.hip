@@ -577,6 +577,7 @@ struct G256TNArgs {
   int M, N, K, lda, ldb, ldc;
   int tiles_m, tiles_n, splits, kt_per_split;
   int a_bytes, b_bytes;
+  float* ws;  // split-K partial slabs [tiles][splits][256][256] fp32 (nullptr: fp32 atomics into C)
 };
 
 __device__ __forceinline__ int tr_swz32(int k) { return (4 * (k & 3) + 16 * ((k >> 3) & 1)) & 31; }
@@ -713,6 +714,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
 
   // lane holds D[n = 16j + 4g + r][m = 16i + li]: C[m][n..n+3]
   // B part nq holds, for wave column wn, cols (wn>>1)*128 + nq*64 + (wn&1)*32 + j*16 of the tile
+  if (a.splits > 1 && a.ws) {
+    // this split's partial tile, row-major inside the tile; g256_tn_reduce_kernel sums the splits
+    // into C in split order (deterministic, no fp32 atomics)
+    float* slab = a.ws + ((size_t)(tm * a.tiles_n + tn) * a.splits + split) * (G_BM * G_BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = wm * 128 + i * 16 + li;
+        const int nl = (wn >> 1) * 128 + (j >> 1) * 64 + (wn & 1) * 32 + (j & 1) * 16 + 4 * g;
+        *(f32x4*)(slab + ml * G_BN + nl) = acc[i][j];
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wm * 128 + i * 16 + li;
@@ -737,7 +752,33 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
 }
 
 
+// C[M][N] += sum over splits of the gemm256_tn partial slabs: one thread per 4 columns of a tile
+// row, the splits summed in order (4 loads in flight)
+__global__ __launch_bounds__(256) void g256_tn_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C,
+                                                             int M, int N, int ldc, int tiles_n, int splits) {
+  const int tile = blockIdx.y;
+  const int pos = blockIdx.x * 256 + threadIdx.x;  // f32x4 index inside the 256 x 256 tile
+  const int ml = pos >> 6, nl = (pos & 63) * 4;
+  const int m = (tile / tiles_n) * G_BM + ml, n = (tile % tiles_n) * G_BN + nl;
+  if (m >= M || n >= N) return;
+  const f32x4* src = (const f32x4*)(ws + (size_t)tile * splits * (G_BM * G_BN)) + pos;
+  constexpr int TS = G_BM * G_BN / 4;
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  int z = 0;
+  for (; z + 4 <= splits; z += 4) {
+    const f32x4 a0 = src[(size_t)z * TS], a1 = src[(size_t)(z + 1) * TS];
+    const f32x4 a2 = src[(size_t)(z + 2) * TS], a3 = src[(size_t)(z + 3) * TS];
+    s += a0; s += a1; s += a2; s += a3;
+  }
+  for (; z < splits; ++z) s += src[(size_t)z * TS];
+  float* dst = C + (size_t)m * ldc + n;  // N % 8 == 0: the 4 columns are all in range
+  const float4 o = *(const float4*)dst;
+  *(float4*)dst = make_float4(o.x + s[0], o.y + s[1], o.z + s[2], o.w + s[3]);
+}
+
 }  // namespace
+
+extern "C" float* mi_partials_workspace(size_t floats, hipStream_t st);  // gemm_conv.hip
 
 // Tail split-K planning: with 1 block per CU, a grid of `tiles` runs in ceil(tiles / CUs) waves;
 // when the last wave is at most 3/4 full its tiles are split along K so it fills the chip.
@@ -908,14 +949,21 @@ MI_API int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, i
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.tiles_m = cdiv(M, G_BM); a.tiles_n = cdiv(N, G_BN);
   const int tiles = a.tiles_m * a.tiles_n, nkt = cdiv(K, G_BK);
-  // about one wave of blocks (1 block per CU), >= 8 k-tiles per split
-  int splits = max(1, min((256 + tiles / 2) / tiles, nkt / 8));
+  // at most one wave of blocks (1 block per CU), >= 8 k-tiles per split
+  if (g_num_cus == 0) plan_defaults();
+  int splits = max(1, min(g_num_cus / tiles, nkt / 8));
   a.kt_per_split = cdiv(nkt, splits);
   a.splits = cdiv(nkt, a.kt_per_split);
   a.a_bytes = rsrc_bytes256((int64_t)K * lda);
   a.b_bytes = rsrc_bytes256((int64_t)K * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  // split-K partials through slabs + one reduce launch (fp32 atomics, the fallback when no workspace
+  // can be had -- e.g. growth inside a graph capture -- cost ~37 us per ViT-B/16 weight gradient)
+  a.ws = a.splits > 1 ? mi_partials_workspace((size_t)tiles * a.splits * G_BM * G_BN, st) : nullptr;
   hipLaunchKernelGGL(gemm256_tn_kernel, dim3(tiles * a.splits), dim3(512), 0, st, a);
+  if (a.ws)
+    hipLaunchKernelGGL(g256_tn_reduce_kernel, dim3(G_BM * G_BN / 4 / 256, tiles), dim3(256), 0, st, (const float*)a.ws,
+                       C, M, N, ldc, a.tiles_n, a.splits);
   return (int)hipGetLastError();
 }
 
