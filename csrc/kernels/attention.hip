@@ -187,6 +187,96 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_fwd_kernel(const bf16_t*
   }
 }
 
+// Forward at 8 waves per (batch, head) workgroup: the scores of a 16-query tile are taken in
+// chunks of CP key-tile pairs with an online softmax (running max / sum, O rescaled when the max
+// grows), so a wave holds 4 score tiles instead of all 2 * NK2 -- <= 128 VGPRs, 4 waves per SIMD at
+// two workgroups per CU -- and one wave's Q-load and exp latencies hide behind the others' MFMAs
+// (the backward's 4 -> 8 wave step).  Every chunk holds a valid key (chunk c starts at key
+// 32 * CP * c < T), so the running max is finite after the first chunk.
+template <int NK2, int CP>
+__global__ __launch_bounds__(512, 4) void attn_fwd8_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                          float* __restrict__ lse, int T, int H, float sl2) {
+  constexpr int NW = 8, TP = 32 * NK2, NKT = 2 * NK2;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * KSTR];
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * T * ld + h * HD;
+  stage_rows2<TP, NW>(Ks, base + D, ld, Vs, base + 2 * D, ld, T);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  const int nqt = (T + 15) >> 4;
+  for (int qt = wv; qt < nqt; qt += NW) {
+    const int q = qt * 16 + li;
+    const bool qv = q < T;
+    bf16x8 qf[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) qf[h2] = qv ? g16(base + (size_t)q * ld + 32 * h2 + 8 * g) : zero8();
+    float m = -INFINITY, l = 0.f;
+    f32x4 oa[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oa[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int c0 = 0; c0 < NK2; c0 += CP) {
+      f32x4 sc[2 * CP];
+      float cm = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2 * CP; ++t) {
+        const int kt = 2 * c0 + t;
+        if (kt >= NKT) break;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          acc = mfma(*(const bf16x8*)&Ks[(kt * 16 + li) * KSTR + 32 * h2 + 8 * g], qf[h2], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (kt * 16 + 4 * g + r >= T) acc[r] = -INFINITY;
+          cm = fmaxf(cm, acc[r]);
+        }
+        sc[t] = acc;
+      }
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float mn = fmaxf(m, cm);
+      const float alpha = att_exp2((m - mn) * sl2);  // first chunk: exp2(-inf) = 0 (oa, l are 0)
+      m = mn;
+      const float ms = mn * sl2;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) oa[dt] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2 * CP; ++t) {
+        if (2 * c0 + t >= NKT) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = att_exp2(sc[t][r] * sl2 - ms);
+          sc[t][r] = p;
+          l += p;
+        }
+      }
+#pragma unroll
+      for (int kp = 0; kp < CP; ++kp) {
+        const int ks = c0 + kp;
+        if (ks >= NK2) break;
+        const bf16x8 pb = pack_perm(sc[2 * kp], sc[2 * kp + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          oa[dt] = mfma(tr8(Vs, ks * 32 + 4 * g + q4, ks * 32 + 16 + 4 * g + q4, (dt * 4 + p4) * 4), pb, oa[dt]);
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qv) {
+      const float inv = 1.f / l;
+      bf16_t* orow = o + ((size_t)b * T + q) * D + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4bf(orow + dt * 16 + 4 * g, oa[dt], inv);
+      if (g == 0) lse[(size_t)bh * T + q] = (m * sl2 + log2f(l)) * LN2;
+    }
+  }
+}
+
 template <int NK2, int NW>
 __global__ __launch_bounds__(64 * NW, NW / 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                              const bf16_t* __restrict__ o,
@@ -539,10 +629,52 @@ MI_API int mi_set_att_waves(int w) {
   return 0;
 }
 
+static int g_att_fwd_waves = 0;
+static int att_fwd_waves() {
+  if (!g_att_fwd_waves) {
+    const char* e = std::getenv("MI355X_DP_ATT_FWD_WAVES");
+    g_att_fwd_waves = (e && e[0] == '4') ? 4 : 8;
+  }
+  return g_att_fwd_waves;
+}
+
+// key-tile pairs per online-softmax chunk of the 8-wave forward (MI355X_DP_ATT_FWD_CP: 2 or 4)
+static int g_att_fwd_cp = 0;
+static int att_fwd_cp() {
+  if (!g_att_fwd_cp) {
+    const char* e = std::getenv("MI355X_DP_ATT_FWD_CP");
+    g_att_fwd_cp = (e && e[0] == '4') ? 4 : 2;
+  }
+  return g_att_fwd_cp;
+}
+
+MI_API int mi_set_att_fwd_cp(int cp) {
+  g_att_fwd_cp = cp == 4 ? 4 : 2;
+  return 0;
+}
+
+// forward workgroup size in waves: 8 (online softmax over key chunks, default) or 4 (A/B)
+MI_API int mi_set_att_fwd_waves(int w) {
+  g_att_fwd_waves = w == 4 ? 4 : 8;
+  return 0;
+}
+
 // qkv [B*T][3*H*64] bf16 (q | k | v, heads contiguous), o [B*T][H*64] bf16, lse [B*H][T] fp32
 MI_API int mi_attn_fwd(const void* qkv, void* o, float* lse, int B, int T, int H, float scale, hipStream_t st) {
   if (T <= 0 || T > 256 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
   const float sl2 = scale * LOG2E;
+  if (att_fwd_waves() == 8) {
+#define L(N)                                                                                             \
+  if (att_fwd_cp() == 4)                                                                                 \
+    hipLaunchKernelGGL((attn_fwd8_kernel<N, 4>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, \
+                       T, H, sl2);                                                                       \
+  else                                                                                                   \
+    hipLaunchKernelGGL((attn_fwd8_kernel<N, 2>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, \
+                       T, H, sl2)
+    MI_ATT_SWITCH((T + 31) / 32, L)
+#undef L
+    return (int)hipGetLastError();
+  }
   // forward: 4 waves (its 14 score tiles per q tile need ~210 VGPRs: 2 waves per SIMD)
 #define L(N)                                                                                             \
   hipLaunchKernelGGL((attn_fwd_kernel<N, 4>), dim3(B * H), dim3(256), 0, st, (const bf16_t*)qkv, (bf16_t*)o, \

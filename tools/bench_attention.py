@@ -54,9 +54,15 @@ def main():
     def bwd():
         _lib.call("mi_attn_bwd", ptr(qkv), ptr(o), ptr(do), ptr(lse), ptr(dvec), ptr(dqkv), B, T, H, scale, st)
     fwd()
-    res = {"fwd": [], "bwd_fused": [], "bwd4": [], "bwd8": [], "fwd_rot": []}
+    res = {"fwd": [], "fwd_cp4": [], "fwd4": [], "bwd_fused": [], "bwd4": [], "bwd8": [], "fwd_rot": []}
     for _ in range(a.rounds):
-        res["fwd"].append(timeit(fwd))
+        res["fwd"].append(timeit(fwd))                # default: 8 waves, online softmax, 2 key-tile pairs per chunk
+        _lib.call("mi_set_att_fwd_cp", 4)
+        res["fwd_cp4"].append(timeit(fwd))
+        _lib.call("mi_set_att_fwd_cp", 2)
+        _lib.call("mi_set_att_fwd_waves", 4)          # the 4-wave single-pass forward (A/B)
+        res["fwd4"].append(timeit(fwd))
+        _lib.call("mi_set_att_fwd_waves", 8)
         res["bwd_fused"].append(timeit(bwd))       # default: the single-kernel backward
         _lib.call("mi_set_att_fused_bwd", 0)      # the dQ + dK/dV kernel pair (A/B)
         _lib.call("mi_set_att_waves", 4)
@@ -64,8 +70,10 @@ def main():
         _lib.call("mi_set_att_waves", 8)
         res["bwd8"].append(timeit(bwd))
         _lib.call("mi_set_att_fused_bwd", 1)
-        _lib.call("mi_set_att_rotate", 1)         # the rotated tile deal (A/B)
+        _lib.call("mi_set_att_rotate", 1)         # the rotated tile deal (A/B; 4-wave forward only)
+        _lib.call("mi_set_att_fwd_waves", 4)
         res["fwd_rot"].append(timeit(fwd))
+        _lib.call("mi_set_att_fwd_waves", 8)
         _lib.call("mi_set_att_rotate", 0)
     # reference: the same layout through SDPA (time only)
     q, k, v = qkv.view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4).unbind(0)
@@ -78,12 +86,14 @@ def main():
     fl_f = 4.0 * B * H * T * T * Dh
     t = {k: statistics.median(v) for k, v in res.items()}
     print(f"| op | ms per layer | TF/s |\n|---|---:|---:|")
-    print(f"| forward | {t['fwd']:.3f} | {fl_f / t['fwd'] / 1e9:.0f} |")
+    print(f"| forward, 8 waves, online softmax (default) | {t['fwd']:.3f} | {fl_f / t['fwd'] / 1e9:.0f} |")
+    print(f"| forward, 8 waves, 4-pair chunks | {t['fwd_cp4']:.3f} | {fl_f / t['fwd_cp4'] / 1e9:.0f} |")
+    print(f"| forward, 4 waves, single pass | {t['fwd4']:.3f} | {fl_f / t['fwd4'] / 1e9:.0f} |")
     print(f"| backward, one fused kernel (default) | {t['bwd_fused']:.3f} | {2.5 * fl_f / t['bwd_fused'] / 1e9:.0f} |")
     print(f"| backward, dQ + dK/dV kernels, 4 waves | {t['bwd4']:.3f} | {2.5 * fl_f / t['bwd4'] / 1e9:.0f} |")
     print(f"| backward, dQ + dK/dV kernels, 8 waves | {t['bwd8']:.3f} | {2.5 * fl_f / t['bwd8'] / 1e9:.0f} |")
     print(f"| torch SDPA fwd+bwd | {t_sdpa:.3f} | {3.5 * fl_f / t_sdpa / 1e9:.0f} |")
-    print(f"| forward, rotated tile deal | {t['fwd_rot']:.3f} | {fl_f / t['fwd_rot'] / 1e9:.0f} |")
+    print(f"| forward 4 waves, rotated tile deal | {t['fwd_rot']:.3f} | {fl_f / t['fwd_rot'] / 1e9:.0f} |")
     print(f"12 layers: fwd + bwd(fused) = {12 * (t['fwd'] + t['bwd_fused']):.2f} ms/step "
           f"(two kernels, 8 waves: {12 * (t['fwd'] + t['bwd8']):.2f})")
 
