@@ -102,6 +102,7 @@ struct NTArgs {
   // halo_pb = row blocks per image; fPB / fHW2 divide by halo_pb / (Q + 2)
   int halo_rp, halo_pb;
   FastDiv fPB, fHW2;
+  int halo_breg;  // 64-channel halo tiles: weight fragments of all taps in registers (see nt_kernel)
   // mode 3: blockIdx.y -> parity class (empty classes -- no tap reaches them -- can be skipped when
   // their zero output is not needed); epi 3 / 5 with aux_even: the gradient accumulated into is
   // defined only at even (h, w) of the row grid (a stride-2 1x1 data gradient written by class
@@ -156,6 +157,7 @@ constexpr int BK = 64;
 // decomposed by output parity class (stride 2: only the taps that hit real dY pixels).
 // halo tile capacity (pixels of one 64-channel chunk, 128 B each): (rp + 2) x (Q + 2) <= HALO_PX
 constexpr int HALO_PX = 256;
+
 
 // normalize-on-load: per-channel (scale, shift) table of the gathered tensor, right after the
 // staging ring (the epilogue, which never needs it, may overwrite it); channels <= NOL_MAX_C
@@ -482,7 +484,54 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     };
-    for (int kc = 0; kc < Cs; kc += 64) {
+    // 64x64-channel 3x3 (ResNet layer 1, BN = 64, one channel chunk), opt-in (MI355X_DP_HALO_BREG=1):
+    // the wave's weight fragments of all nine taps (32 columns x 576 k = 144 VGPRs) go to registers
+    // with the halo load, so the nine taps run back to back -- one memory wait per tile instead of a
+    // weight-tile load, vmcnt(0) and barrier per tap.  Measured slower: ResNet-50 12,624 / 12,611 vs
+    // 12,845 / 12,861 img/s (the kernel's 198 VGPRs cost the third resident block per CU that hid
+    // the per-tap waits; profiles/raw/r5/halo_breg/)
+    bool breg_done = false;
+    if constexpr (BN == 64 && NOL == 0) {
+      if (Cs == 64 && a.halo_breg) {
+        breg_done = true;
+        load_halo(0);
+        bf16x8 breg[9][2][NJ];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int n = n0 + wn * WN + 16 * j + fr;  // n < N: BN == 64 == N on this path
+              breg[t][kk][j] = __builtin_bit_cast(
+                  bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, (uint32_t)((n * a.ldb + t * 64 + (kk * 4 + fq) * 8) * 2),
+                                                                0, 0));
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int r = t / 3, sx = t - 3 * r;
+          const int hoff = (a.mode == 1) ? r * HW2 + sx : (2 - r) * HW2 + (2 - sx);
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 af[MI];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+              const int hx = hb[i] + hoff;
+              af[i] = __builtin_bit_cast(bf16x8, Hs[hx * 8 + ((kk * 4 + fq) ^ (hx & 7))]);
+            }
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[t][kk][j], af[i], acc[i][j], 0, 0, 0);
+          }
+        }
+        __syncthreads();  // the epilogue's C tile overwrites the halo
+      }
+    }
+    for (int kc = 0; kc < Cs && !breg_done; kc += 64) {
       load_halo(kc);
       load_b(0, kc, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1514,11 +1563,24 @@ static void trace_gemm(const char* what, int mode, int M, int N, int K, int Cs, 
           mode, M, N, K, Cs, R, stride, epi, stats, blocks, splits);
 }
 
+// 64-channel halo convs: per-tap LDS weight tiles (default) or weight fragments in registers
+// (A/B: MI355X_DP_HALO_BREG=1, mi_set_halo_breg)
+static int g_halo_breg = -1;
+MI_API int mi_set_halo_breg(int on) {
+  g_halo_breg = on ? 1 : 0;
+  return 0;
+}
+
 hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
   if (a.mode == 1 || a.mode == 2) {
     const ConvGeom& g = a.g;
     const int rp = halo_rp(a.M, a.N, g.R, g.S, g.stride, g.pad, g.Cs, g.H, g.W, g.P, g.Q);
     if (rp > 0) {
+      if (g_halo_breg < 0) {
+        const char* e = std::getenv("MI355X_DP_HALO_BREG");
+        g_halo_breg = (e && e[0] == '1') ? 1 : 0;
+      }
+      a.halo_breg = g_halo_breg;
       a.halo_rp = rp;
       a.halo_pb = cdiv(g.P, rp);
       a.fPB = make_fastdiv((uint32_t)a.halo_pb);
