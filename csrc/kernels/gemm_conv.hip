@@ -157,6 +157,9 @@ constexpr int BK = 64;
 // decomposed by output parity class (stride 2: only the taps that hit real dY pixels).
 // halo tile capacity (pixels of one 64-channel chunk, 128 B each): (rp + 2) x (Q + 2) <= HALO_PX
 constexpr int HALO_PX = 256;
+#ifndef MI_HALO_BREG
+#define MI_HALO_BREG 0  // 1: A/B build with the register-weight 64-channel halo path (nt_kernel)
+#endif
 
 
 // normalize-on-load: per-channel (scale, shift) table of the gathered tensor, right after the
@@ -484,13 +487,15 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     };
-    // 64x64-channel 3x3 (ResNet layer 1, BN = 64, one channel chunk), opt-in (MI355X_DP_HALO_BREG=1):
+    // 64x64-channel 3x3 (ResNet layer 1, BN = 64, one channel chunk), A/B build only (MI_HALO_BREG=1,
+    // then MI355X_DP_HALO_BREG=1 at run time):
     // the wave's weight fragments of all nine taps (32 columns x 576 k = 144 VGPRs) go to registers
     // with the halo load, so the nine taps run back to back -- one memory wait per tile instead of a
     // weight-tile load, vmcnt(0) and barrier per tap.  Measured slower: ResNet-50 12,624 / 12,611 vs
     // 12,845 / 12,861 img/s (the kernel's 198 VGPRs cost the third resident block per CU that hid
     // the per-tap waits; profiles/raw/r5/halo_breg/)
     bool breg_done = false;
+#if MI_HALO_BREG  // compiled only into the A/B build: its registers would lower every BN = 64 halo launch's occupancy
     if constexpr (BN == 64 && NOL == 0) {
       if (Cs == 64 && a.halo_breg) {
         breg_done = true;
@@ -531,6 +536,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         __syncthreads();  // the epilogue's C tile overwrites the halo
       }
     }
+#endif
     for (int kc = 0; kc < Cs && !breg_done; kc += 64) {
       load_halo(kc);
       load_b(0, kc, 0);

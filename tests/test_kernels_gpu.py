@@ -823,34 +823,3 @@ def test_tn_bias_splitk_slabs(T, N, K):
         assert rel_err(gw, ref_w) < 1e-4, name
         assert rel_err(gb, ref_b) < 1e-4, name
 
-
-@pytest.mark.parametrize("shape", [(8, 64, 56, 64), (3, 64, 17, 64), (2, 64, 30, 64)])
-def test_halo_register_weights_bit_identical(shape):
-    """64-channel 3x3 halo tiles with every tap's weight fragments in registers (opt-in) against the
-    per-tap LDS weight tiles (default): the same MFMA sequence per output, so forward (with its BN
-    statistics partials) and data gradient are bit-identical."""
-    from mi355x_dp.ops import _lib, conv2d
-    from mi355x_dp.ops.functional import conv2d_with_stats
-    N, C, H, K = shape
-    torch.manual_seed(3)
-    x0 = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
-    w0 = (torch.randn(K, C, 3, 3, device="cuda") * (2.0 / (C * 9)) ** 0.5).to(BF).float().contiguous(memory_format=CL)
-    gy = torch.randn(N, K, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
-    lib = _lib.load(True)
-    out = []
-    try:
-        for on in (1, 0):
-            lib.mi_set_halo_breg(on)
-            x = x0.clone().requires_grad_(True)
-            w = w0.clone().requires_grad_(True)
-            y = conv2d(x, w, None, 1, 1)
-            y.backward(gy)
-            ys, (slab, rows) = conv2d_with_stats(x0, w0, 1, 1)
-            torch.cuda.synchronize()
-            out.append((y.detach().clone(), x.grad.clone(), ys.clone(), slab[:rows].clone()))
-    finally:
-        lib.mi_set_halo_breg(0)
-    for a, b in zip(out[0], out[1]):
-        assert torch.equal(a, b)
-    yr = F.conv2d(x0.float(), w0, None, 1, 1)
-    assert rel_err(out[0][0], yr) < 1e-2
