@@ -1,6 +1,6 @@
 #!/usr/bin/env python
-"""Isolated timings of the ResNet-50 layer-1 1x1 convolutions (batch 256, 56x56) with the fused
-epilogues the training step uses, as achieved HBM bandwidth over the bytes each one must move:
+"""Isolated timings of the ResNet-50 layer-1 convolutions (batch 256, 56x56: the 1x1s and the 3x3
+halo tiles) with the fused epilogues the training step uses, as achieved HBM bandwidth over the bytes each one must move:
 is a kernel at its memory roofline in isolation (then its in-model time is contention), or not?
 
     python tools/bench_l1.py [--iters 20] [--rounds 5]
@@ -69,6 +69,12 @@ def main():
 
     sf256, sf64 = slab_f(64, 256), slab_f(256, 64)
     sd256, sd64 = slab_d(256, 64), slab_d(64, 256)
+    w3 = (torch.randn(64, 9 * 64, device=dev) * 0.05).to(BF16).contiguous()     # 3x3 64 -> 64: [K][R][S][C]
+    sf3 = torch.empty((lib.mi_conv_stat_rows_g(Nb, H, H, 64, 64, 3, 3, 1, 1, H, H) + lib.mi_bn_slab_extra_rows(), 2,
+                       64), dtype=F32, device=dev)
+    sd3 = torch.empty((lib.mi_dgrad_stat_rows(Nb, H, H, 64, H, H, 1, 64, 9) + lib.mi_bn_slab_extra_rows(), 2, 64),
+                      dtype=F32, device=dev)
+    y64b = torch.empty_like(y64)
     MB = M * 2 / 1e6  # MB per channel-plane... bytes of one bf16 channel over all pixels
 
     cases = [
@@ -89,6 +95,19 @@ def main():
             "mi_conv2d_dgrad_ex4", ptr(x256), ptr(w_256_64), ptr(y64), Nb, H, H, 64, 256, 1, 1, 1, 0, H, H, 4,
             ptr(None), ptr(c64), ptr(mean64), 1, ptr(sd64), 0, ptr(None), ptr(None), ptr(bits64), st),
          (256 + 64 + 64 + 64 / 16) * MB),
+        # 3x3 / stride 1 halo tiles (conv2 of each layer-1 block): forward + stats, data gradient
+        # with epi 4 (mask bits, BN-backward statistics) and plain (the epilogue's share)
+        ("fwd 3x3 64->64 + stats (halo)", lambda: _lib.call(
+            "mi_conv2d_fwd", ptr(x64), ptr(w3), ptr(y64b), ptr(None), ptr(sf3), Nb, H, H, 64, 64, 3, 3, 1, 1,
+            H, H, 0, st), (64 + 64) * MB),
+        ("dgrad 3x3 64->64 epi4 bits (halo)", lambda: _lib.call(
+            "mi_conv2d_dgrad_ex4", ptr(c64), ptr(w3), ptr(y64b), Nb, H, H, 64, 64, 3, 3, 1, 1, H, H, 4,
+            ptr(None), ptr(x64), ptr(mean64), 1, ptr(sd3), 0, ptr(None), ptr(None), ptr(bits64), st),
+         (64 + 64 + 64 + 64 / 16) * MB),
+        ("dgrad 3x3 64->64 plain (halo)", lambda: _lib.call(
+            "mi_conv2d_dgrad_ex4", ptr(c64), ptr(w3), ptr(y64b), Nb, H, H, 64, 64, 3, 3, 1, 1, H, H, 0,
+            ptr(None), ptr(None), ptr(None), 0, ptr(None), 0, ptr(None), ptr(None), ptr(None), st),
+         (64 + 64) * MB),
     ]
     res = {n: [] for n, _, _ in cases}
     for _ in range(a.rounds):
