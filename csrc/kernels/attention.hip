@@ -193,10 +193,11 @@ __global__ __launch_bounds__(64 * NW, NW / 2) void attn_fwd_kernel(const bf16_t*
 // two workgroups per CU -- and one wave's Q-load and exp latencies hide behind the others' MFMAs
 // (the backward's 4 -> 8 wave step).  Every chunk holds a valid key (chunk c starts at key
 // 32 * CP * c < T), so the running max is finite after the first chunk.
-template <int NK2, int CP>
+template <int NK2>
 __global__ __launch_bounds__(512, 4) void attn_fwd8_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int T, int H, float sl2) {
   constexpr int NW = 8, TP = 32 * NK2, NKT = 2 * NK2;
+  constexpr int CP = 2;  // key-tile pairs per chunk (4 pairs: 0.097 vs 0.095 ms per ViT layer, and spills at NK2 = 4)
   __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * KSTR];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * KSTR];
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
@@ -638,21 +639,6 @@ static int att_fwd_waves() {
   return g_att_fwd_waves;
 }
 
-// key-tile pairs per online-softmax chunk of the 8-wave forward (MI355X_DP_ATT_FWD_CP: 2 or 4)
-static int g_att_fwd_cp = 0;
-static int att_fwd_cp() {
-  if (!g_att_fwd_cp) {
-    const char* e = std::getenv("MI355X_DP_ATT_FWD_CP");
-    g_att_fwd_cp = (e && e[0] == '4') ? 4 : 2;
-  }
-  return g_att_fwd_cp;
-}
-
-MI_API int mi_set_att_fwd_cp(int cp) {
-  g_att_fwd_cp = cp == 4 ? 4 : 2;
-  return 0;
-}
-
 // forward workgroup size in waves: 8 (online softmax over key chunks, default) or 4 (A/B)
 MI_API int mi_set_att_fwd_waves(int w) {
   g_att_fwd_waves = w == 4 ? 4 : 8;
@@ -665,12 +651,8 @@ MI_API int mi_attn_fwd(const void* qkv, void* o, float* lse, int B, int T, int H
   const float sl2 = scale * LOG2E;
   if (att_fwd_waves() == 8) {
 #define L(N)                                                                                             \
-  if (att_fwd_cp() == 4)                                                                                 \
-    hipLaunchKernelGGL((attn_fwd8_kernel<N, 4>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, \
-                       T, H, sl2);                                                                       \
-  else                                                                                                   \
-    hipLaunchKernelGGL((attn_fwd8_kernel<N, 2>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, \
-                       T, H, sl2)
+  hipLaunchKernelGGL((attn_fwd8_kernel<N>), dim3(B * H), dim3(512), 0, st, (const bf16_t*)qkv, (bf16_t*)o, lse, T, \
+                     H, sl2)
     MI_ATT_SWITCH((T + 31) / 32, L)
 #undef L
     return (int)hipGetLastError();

@@ -178,17 +178,16 @@ def test_attention_fused_bwd_matches_two_kernels(B, T, H):
 
 @pytest.mark.parametrize("B,T,H", [(2, 197, 12), (3, 17, 2), (2, 256, 3), (4, 1, 1), (1, 100, 2)])
 def test_attention_fwd_variants_agree(B, T, H):
-    """The 8-wave online-softmax forward (2- and 4-pair key chunks) against the 4-wave single-pass
-    forward: O and the saved log-sum-exp agree to rounding."""
+    """The 8-wave online-softmax forward against the 4-wave single-pass forward: O and the saved
+    log-sum-exp agree to rounding."""
     from mi355x_dp.ops import _lib
     from mi355x_dp.ops._lib import ptr, stream_of
     D = H * 64
     qkv = rnd(B * T, 3 * D, scale=2.0)
     outs = []
     try:
-        for waves, cp in ((4, 2), (8, 2), (8, 4)):
+        for waves in (4, 8):
             _lib.call("mi_set_att_fwd_waves", waves)
-            _lib.call("mi_set_att_fwd_cp", cp)
             o = torch.empty(B * T, D, dtype=BF, device="cuda")
             lse = torch.empty(B * H * T, device="cuda")
             _lib.call("mi_attn_fwd", ptr(qkv), ptr(o), ptr(lse), B, T, H, 0.125, stream_of(qkv))
@@ -196,7 +195,6 @@ def test_attention_fwd_variants_agree(B, T, H):
             outs.append((o.float(), lse))
     finally:
         _lib.call("mi_set_att_fwd_waves", 8)
-        _lib.call("mi_set_att_fwd_cp", 2)
     for o, lse in outs[1:]:
         assert rel_err(o, outs[0][0]) < 1e-2
         assert float((lse - outs[0][1]).abs().max()) < 1e-4

@@ -54,12 +54,9 @@ def main():
     def bwd():
         _lib.call("mi_attn_bwd", ptr(qkv), ptr(o), ptr(do), ptr(lse), ptr(dvec), ptr(dqkv), B, T, H, scale, st)
     fwd()
-    res = {"fwd": [], "fwd_cp4": [], "fwd4": [], "bwd_fused": [], "bwd4": [], "bwd8": [], "fwd_rot": []}
+    res = {"fwd": [], "fwd4": [], "bwd_fused": [], "bwd4": [], "bwd8": [], "fwd_rot": []}
     for _ in range(a.rounds):
         res["fwd"].append(timeit(fwd))                # default: 8 waves, online softmax, 2 key-tile pairs per chunk
-        _lib.call("mi_set_att_fwd_cp", 4)
-        res["fwd_cp4"].append(timeit(fwd))
-        _lib.call("mi_set_att_fwd_cp", 2)
         _lib.call("mi_set_att_fwd_waves", 4)          # the 4-wave single-pass forward (A/B)
         res["fwd4"].append(timeit(fwd))
         _lib.call("mi_set_att_fwd_waves", 8)
@@ -87,7 +84,6 @@ def main():
     t = {k: statistics.median(v) for k, v in res.items()}
     print(f"| op | ms per layer | TF/s |\n|---|---:|---:|")
     print(f"| forward, 8 waves, online softmax (default) | {t['fwd']:.3f} | {fl_f / t['fwd'] / 1e9:.0f} |")
-    print(f"| forward, 8 waves, 4-pair chunks | {t['fwd_cp4']:.3f} | {fl_f / t['fwd_cp4'] / 1e9:.0f} |")
     print(f"| forward, 4 waves, single pass | {t['fwd4']:.3f} | {fl_f / t['fwd4'] / 1e9:.0f} |")
     print(f"| backward, one fused kernel (default) | {t['bwd_fused']:.3f} | {2.5 * fl_f / t['bwd_fused'] / 1e9:.0f} |")
     print(f"| backward, dQ + dK/dV kernels, 4 waves | {t['bwd4']:.3f} | {2.5 * fl_f / t['bwd4'] / 1e9:.0f} |")
