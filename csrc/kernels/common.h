@@ -109,10 +109,15 @@ __device__ __forceinline__ uint32_t nz_bits8(const uint4& v) {
   return b;
 }
 
-// streaming 16-byte load (nontemporal: read once, do not keep in the caches)
+// streaming 16-byte load (nontemporal: read once, do not keep in the caches; MI_NTLOAD=0 A/B
+// builds: plain loads)
+#ifndef MI_NTLOAD
+#define MI_NTLOAD 1
+#endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_nt16(const void* base, int64_t v) {
-  return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)base + v));
+  if (MI_NTLOAD) return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)base + v));
+  return ((const uint4*)base)[v];
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
