@@ -120,6 +120,21 @@ __device__ __forceinline__ uint4 ld_nt16(const void* base, int64_t v) {
   return ((const uint4*)base)[v];
 }
 
+// GEMM-epilogue operand loads (A/B builds): MI_EPI_NT_CY = 1 reads the accumulated-into C and the
+// aux operand (residual / GELU derivative / ReLU source) non-temporally, MI_EPI_NT_X = 1 the BN
+// input read for the BN-backward statistics
+#ifndef MI_EPI_NT_CY
+#define MI_EPI_NT_CY 1
+#endif
+#ifndef MI_EPI_NT_X
+#define MI_EPI_NT_X 0
+#endif
+template <bool NTL>
+__device__ __forceinline__ uint4 epi_ld16(const void* p) {
+  if (NTL) return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)p));
+  return *(const uint4*)p;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -453,21 +453,21 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         }
         if (BN_EPI && ok[sl][u] && a.epi >= 4) {
           if (a.epi == 5)
-            cv[sl][u] = acc_ok ? *(const uint4*)((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
+            cv[sl][u] = acc_ok ? epi_ld16<MI_EPI_NT_CY>((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
 #if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
-          if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
+          if (a.stats) xq[sl][u] = epi_ld16<MI_EPI_NT_X>(a.aux2 + offs[sl][u]);
           if (a.bn_relu) yq[sl][u] = xq[sl][u];
 #else
           if (a.bn_relu) {
             if (a.mbits)
               yq[sl][u].x = a.mbits[offs[sl][u] >> 3];  // mask byte (offs is a multiple of 8)
             else
-              yq[sl][u] = *(const uint4*)(a.aux + offs[sl][u]);
+              yq[sl][u] = epi_ld16<MI_EPI_NT_CY>(a.aux + offs[sl][u]);
           }
-          if (a.stats) xq[sl][u] = *(const uint4*)(a.aux2 + offs[sl][u]);
+          if (a.stats) xq[sl][u] = epi_ld16<MI_EPI_NT_X>(a.aux2 + offs[sl][u]);
 #endif
         } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
-          yq[sl][u] = acc_ok ? *(const uint4*)(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
+          yq[sl][u] = acc_ok ? epi_ld16<MI_EPI_NT_CY>(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
         }
       }
     };
