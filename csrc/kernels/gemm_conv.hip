@@ -38,6 +38,12 @@
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
 #endif
+#ifndef MI_TN_CPOL_A
+#define MI_TN_CPOL_A 0  // cache-policy bits of the TN (weight-gradient) operand loads (A/B builds: 2 = nt)
+#endif
+#ifndef MI_TN_CPOL_B
+#define MI_TN_CPOL_B 0
+#endif
 #ifndef MI_NT_EPI_PIPE
 #define MI_NT_EPI_PIPE 0  // NT epilogue operand loads software-pipelined one group ahead (A/B)
 #endif
@@ -1022,7 +1028,7 @@ void tn_kernel(TNArgs a) {
       const bool ok = k < kend && a_m < a.M;
       const uint32_t vo = ok ? (uint32_t)(k * a.lda + a_m) * 2u : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsA, LDS_PTR(void, &As[(buf * BK + A_RSTEP * i + wid * A_RPI) * AU]), 16, vo, 0, 0, 0);
+          rsA, LDS_PTR(void, &As[(buf * BK + A_RSTEP * i + wid * A_RPI) * AU]), 16, vo, 0, 0, MI_TN_CPOL_A);
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -1042,7 +1048,7 @@ void tn_kernel(TNArgs a) {
         b_q[i] = q; b_p[i] = p; b_img[i] = img;
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsB, LDS_PTR(void, &Bs[(buf * BK + B_RSTEP * i + wid * B_RPI) * BU]), 16, vo, 0, 0, 0);
+          rsB, LDS_PTR(void, &Bs[(buf * BK + B_RSTEP * i + wid * B_RPI) * BU]), 16, vo, 0, 0, MI_TN_CPOL_B);
     }
   };
 
