@@ -43,6 +43,9 @@
 #include <mutex>
 #include <cstdlib>
 
+#ifndef MI_G256_CPOL_A
+#define MI_G256_CPOL_A 0  // cache-policy bits of the conv modes' gathered A operand loads (A/B builds)
+#endif
 #ifndef MI_G256_EPI_U0
 #define MI_G256_EPI_U0 8  // plain-GEMM epilogue: row steps per group of batched operand loads (A/B)
 #endif
@@ -216,7 +219,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const bool ok = ta < kt1 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
         const uint32_t vo = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
         MI_ASSERT(vo == OOB || vo + 16u <= (uint32_t)a.a_bytes, vo);  // valid taps never rely on zero fill
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0,
+                                                 MI_G256_CPOL_A);
       }
     }
   };

@@ -38,6 +38,9 @@
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
 #endif
+#ifndef MI_NT_CPOL_A
+#define MI_NT_CPOL_A 0  // cache-policy bits of the NT kernel's A (activation) operand loads (A/B builds)
+#endif
 #ifndef MI_TN_CPOL_A
 #define MI_TN_CPOL_A 0  // cache-policy bits of the TN (weight-gradient) operand loads (A/B builds: 2 = nt)
 #endif
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       const uint32_t vo = ok ? (uint32_t)(a_base[i] + koffA) * 2u : OOB;
       a_okm |= (ok ? 1u : 0u) << i;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &As[(buf * BM + 32 * i + 8 * wid) * 8]), 16, vo,
-                                               0, 0, 0);
+                                               0, 0, MI_NT_CPOL_A);
     }
     const bool kok = (!SMALLC && a.mode != 0) || (kt * BK + lc * 8 < a.K);
 #pragma unroll
@@ -457,7 +460,8 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         const int ih = hp0 - 1 + (int)hr, iw = hc - 1;
         const bool ok = px < HP && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
         const uint32_t vo = ok ? (uint32_t)((((hi * H + ih) * W + iw) * Cs + kc + ((chp ^ (px & 7)) * 8)) * 2) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &Hs[it * 256 + wid * 64]), 16, vo, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &Hs[it * 256 + wid * 64]), 16, vo, 0, 0,
+                                                 MI_NT_CPOL_A);
       }
     };
     auto load_b = [&](int t, int kc, int buf) {
