@@ -17,6 +17,9 @@
 namespace {
 
 constexpr int NT = 256;
+#ifndef MI_BNX_NT
+#define MI_BNX_NT 0  // BN-backward statistics and stem BN+pool passes: non-temporal input loads (A/B builds)
+#endif
 
 struct SlabGeom {
   int tpr;   // threads per row (each covers 8 channels)
@@ -341,11 +344,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(const bf16_t* __restri
   for (int r = rb + r0; r < re; r += g.rp) {
     const size_t off = (size_t)r * C + cc;
     float d[8], xv[8];
-    unpack8(*(const uint4*)(dy + off), d);
-    unpack8(*(const uint4*)(x + off), xv);
+    unpack8(epi_ld16<MI_BNX_NT>(dy + off), d);
+    unpack8(epi_ld16<MI_BNX_NT>(x + off), xv);
     if (relu) {
       float yv[8];
-      unpack8(*(const uint4*)(y + off), yv);
+      unpack8(epi_ld16<MI_BNX_NT>(y + off), yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
     }
@@ -882,7 +885,7 @@ __global__ __launch_bounds__(NT) void bnpool3_fwd_kernel(const bf16_t* __restric
         const int ih = h0 - 1 + r, iw = w0 - 1 + u;
         const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
         ok[r * 3 + u] = in;
-        v[r * 3 + u] = *(const uint4*)(base + ((size_t)(in ? ih : h0) * W + (in ? iw : w0)) * C);
+        v[r * 3 + u] = epi_ld16<MI_BNX_NT>(base + ((size_t)(in ? ih : h0) * W + (in ? iw : w0)) * C);
       }
     }
     float a[8], b[8], best[8];
@@ -925,8 +928,8 @@ __device__ __forceinline__ void bnpool3_quad(const bf16_t* __restrict__ dy, cons
   const size_t o00 = (((size_t)n * P + p) * Q + q) * C + cc;
   const size_t o01 = qn ? o00 + C : o00, o10 = pn ? o00 + (size_t)Q * C : o00;
   const size_t o11 = (pn && qn) ? o00 + (size_t)Q * C + C : o00;
-  const uint4 g00 = *(const uint4*)(dy + o00), g01 = *(const uint4*)(dy + o01);
-  const uint4 g10 = *(const uint4*)(dy + o10), g11 = *(const uint4*)(dy + o11);
+  const uint4 g00 = epi_ld16<MI_BNX_NT>(dy + o00), g01 = epi_ld16<MI_BNX_NT>(dy + o01);
+  const uint4 g10 = epi_ld16<MI_BNX_NT>(dy + o10), g11 = epi_ld16<MI_BNX_NT>(dy + o11);
   const uint2 i00 = *(const uint2*)(idx + o00), i01 = *(const uint2*)(idx + o01);
   const uint2 i10 = *(const uint2*)(idx + o10), i11 = *(const uint2*)(idx + o11);
   const int h0 = 2 * p, w0 = 2 * q;
@@ -935,7 +938,7 @@ __device__ __forceinline__ void bnpool3_quad(const bf16_t* __restrict__ dy, cons
   for (int i = 0; i < 4; ++i) {
     const int h = h0 + (i >> 1), w = w0 + (i & 1);
     valid[i] = h < H && w < W;
-    xv[i] = *(const uint4*)(c + (((size_t)n * H + (valid[i] ? h : h0)) * W + (valid[i] ? w : w0)) * C + cc);
+    xv[i] = epi_ld16<MI_BNX_NT>(c + (((size_t)n * H + (valid[i] ? h : h0)) * W + (valid[i] ? w : w0)) * C + cc);
   }
   float f00[8], f01[8], f10[8], f11[8];
   unpack8(g00, f00); unpack8(g01, f01); unpack8(g10, f10); unpack8(g11, f11);
