@@ -38,6 +38,9 @@
 #ifndef MI_CONV_NTSTORE
 #define MI_CONV_NTSTORE 0
 #endif
+#ifndef MI_SLAB_NT
+#define MI_SLAB_NT 0  // split-K weight-gradient slabs written / reduced non-temporally (A/B builds)
+#endif
 #ifndef MI_NT_CPOL_A
 #define MI_NT_CPOL_A 0  // cache-policy bits of the NT kernel's A (activation) operand loads (A/B builds)
 #endif
@@ -1226,7 +1229,10 @@ void tn_kernel(TNArgs a) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) slab[((i * NJ + j) * 4 + wid) * 64 + lane] = acc[i][j];
+      for (int j = 0; j < NJ; ++j) {
+        f32x4* q = slab + ((i * NJ + j) * 4 + wid) * 64 + lane;
+        if (MI_SLAB_NT) __builtin_nontemporal_store(acc[i][j], q); else *q = acc[i][j];
+      }
   } else {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -1280,7 +1286,10 @@ __global__ __launch_bounds__(256) void tn_splitk_reduce_kernel(const f32x4* __re
     for (int s0 = grp; s0 < splits; s0 += 8 * G) {
       f32x4 r[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) r[i] = src[(size_t)min(s0 + i * G, splits - 1) * PER];
+      for (int i = 0; i < 8; ++i) {
+        const f32x4* q = src + (size_t)min(s0 + i * G, splits - 1) * PER;
+        r[i] = MI_SLAB_NT ? __builtin_nontemporal_load(q) : *q;
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (s0 + i * G < splits) v += r[i];
