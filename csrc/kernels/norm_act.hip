@@ -231,6 +231,16 @@ __device__ __forceinline__ void st16(void* base, int64_t v, uint4 val) {
   else
     ((uint4*)base)[v] = val;
 }
+// the forward apply's output (the next conv's input): MI_EW_NTSTORE_FWD A/B builds
+#ifndef MI_EW_NTSTORE_FWD
+#define MI_EW_NTSTORE_FWD MI_EW_NTSTORE
+#endif
+__device__ __forceinline__ void st16f(void* base, int64_t v, uint4 val) {
+  if (MI_EW_NTSTORE_FWD)
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, val), (u32x4*)base + v);
+  else
+    ((uint4*)base)[v] = val;
+}
 
 struct EwIter {
   int64_t v0, stride;
@@ -320,7 +330,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel_t(const bf16_t* __restrict
         for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
       }
       const uint4 o = pack8(f);
-      st16(y, v, o);
+      st16f(y, v, o);
       if (bits) bits[v] = (uint8_t)nz_bits8(o);  // the consumer's ReLU mask, 1/16 of y's bytes
       if (!FIXC) c = it.chan(c, C);
     }
