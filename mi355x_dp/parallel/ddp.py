@@ -640,8 +640,14 @@ class DataParallel(nn.Module):
         self._final_cb_pending = False
         if self.__dict__.pop("_graph_comm_done", False):
             return  # a replayed backward graph already ran its collectives, their join and the 1/world
-        if self.__dict__.pop("_graph_backward_ran", False) and self.comm_on:
+        graph_ran = self.__dict__.pop("_graph_backward_ran", False)
+        if graph_ran and self.comm_on:
             self._mark_all_ready()
+        if not graph_ran and "_graph_gated" not in self.__dict__:
+            # an eager backward completed: the script moved past any graphed output it never
+            # back-propagated, so the graphs may replay again (same program order on every rank)
+            for g in self.__dict__.get("_graphs", {}).values():
+                g.pending = False
         gated = self.__dict__.pop("_graph_gated", None)
         self.finish_gradient_sync(average=True)
         if gated is not None:
@@ -721,21 +727,40 @@ class DataParallel(nn.Module):
             seen[key] = seen.get(key, 0) + 1
             if seen[key] <= step_graph.AFTER:
                 return None
+            err = None
             try:
-                st = graphs[key] = step_graph.CapturedStep(self, x)
+                st = step_graph.CapturedStep(self, x)
             except Exception as e:  # never fail a training step over the optimisation: run eagerly
+                err, st = e, None
+            # rank-symmetric: every rank reaches this capture on the same step (the seen counts and
+            # eligibility are SPMD-symmetric), so one MIN all-reduce of the success flag decides for
+            # all of them -- a rank whose capture failed must not run eagerly while its peers replay
+            # graphs with captured collectives (cifar10-distributed-smddp-gpu.py:148,160-168)
+            if not self._all_ranks_agree(err is None):
                 import warnings
                 self._graph_disabled = True
-                warnings.warn(f"mi355x_dp: graph capture of the forward/backward failed ({e!r}); "
-                              "running this engine eagerly", stacklevel=3)
+                why = f"failed here ({err!r})" if err is not None else "failed on another rank"
+                warnings.warn(f"mi355x_dp: graph capture of the forward/backward {why}; "
+                              "every rank runs this engine eagerly", stacklevel=3)
                 return None
+            graphs[key] = st
         elif any(g.busy() for g in graphs.values()):
+            # deterministic (backward-not-yet-run, not object liveness): the same on every rank
             return None
         tok = self.__dict__.get("_graph_token")
         if tok is None:
             tok = self._graph_token = torch.zeros((), device=x.device, requires_grad=True)
         self._graph_bcast = st.comm_mode == "capture"
         return st(tok, x)
+
+    def _all_ranks_agree(self, ok: bool) -> bool:
+        """True iff ``ok`` holds on every rank of the engine's process group (MIN all-reduce of a
+        flag, on the engine's device); world 1: ``ok``."""
+        if self.world_size <= 1 or not dist.is_initialized():
+            return ok
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.flat.grad.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.process_group)
+        return bool(int(flag.item()))
 
     def _capture_buffer_broadcast(self):
         """inside the capture of a backward graph (comm_mode "capture"): rank 0's BN buffers, as

@@ -47,13 +47,15 @@ Eligibility (else the eager path, unchanged): training mode, grad enabled, one C
 argument, gradient sync on (not inside ``no_sync``), no comm hook / stream-order checker / shard
 mode, and -- in the default ``auto`` mode -- a small input (``MAX_NUMEL``), since a large step is
 not launch-bound and would lose the side-stream overlap.  ``MI355X_DP_ENGINE_GRAPH=1`` forces,
-``0`` disables.  A forward whose previous graphed output has not been back-propagated yet (and is
-still alive) runs eagerly, so the static buffers are never overwritten under a pending backward.
+``0`` disables.  A forward whose previous graphed forward has not been back-propagated yet runs
+eagerly, so the static buffers are never overwritten under a pending backward; the rule follows
+program order only (not object liveness), so every rank decides alike.  The capture itself is
+agreed on by all ranks (``DataParallel._all_ranks_agree``): if it fails on any rank, every rank
+runs eagerly.
 """
 from __future__ import annotations
 
 import os
-import weakref
 
 import torch
 
@@ -113,7 +115,9 @@ class _Replay(torch.autograd.Function):
         if x.data_ptr() != step.static_x.data_ptr():
             step.static_x.copy_(x)
         step.fwd.replay()
+        step.gen += 1
         ctx.step = step
+        ctx.gen = step.gen
         # a copy, not a view of the static buffer: outputs a script keeps past backward (logits
         # saved for an accuracy count) must not change under the next replay -- stock DDP returns
         # fresh tensors too; the copy is one small kernel next to the ~150 launches saved
@@ -123,9 +127,15 @@ class _Replay(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         st = ctx.step
+        if ctx.gen != st.gen:
+            # a later replay of the forward reused the graph's activations: this output's backward
+            # would read another step's tensors -- refuse rather than compute wrong gradients
+            raise RuntimeError("mi355x_dp: backward of a graphed forward whose buffers a later replay reused "
+                               "(back-propagate each graphed output before the next forward, or set "
+                               "MI355X_DP_ENGINE_GRAPH=0)")
         st.static_gout.copy_(g)
         eng = st.engine
-        st.pending = None
+        st.pending = False
         if st.comm_mode == "gates":
             # every bucket's gate + collective is enqueued BEFORE the replay: structural ordering
             trace = eng._gate_trace_begin()
@@ -198,7 +208,10 @@ class CapturedStep:
         from mi355x_dp.ops.functional import WgradStream
         self.engine = engine
         self.replays = 0
-        self.pending = None  # weakref to the last graphed output until its backward ran
+        self.gen = 0  # forward replays: a backward must belong to the latest one
+        # True from a forward replay until its backward ran.  Deterministic (program order, not
+        # object liveness), so every rank of an SPMD job takes the same eager / replay decision
+        self.pending = False
         self.comm_mode = comm_mode(engine)
         self.gates = BucketGates(len(engine.buckets)) if self.comm_mode == "gates" else None
         mod = engine.module
@@ -275,12 +288,14 @@ class CapturedStep:
 
     def __call__(self, token, x):
         out = _Replay.apply(token, x, self)
-        self.pending = weakref.ref(out)
+        self.pending = True
         return out
 
     def busy(self) -> bool:
-        """a graphed output is alive whose backward has not run: its static buffers are in use"""
-        return self.pending is not None and self.pending() is not None
+        """the last replayed forward's backward has not run: its static buffers may still be needed.
+        Cleared by that backward, or by a completed eager backward of the same engine (the script
+        moved on: a late backward of the old output then raises via the generation check)."""
+        return self.pending
 
 
 def signature(x: torch.Tensor):

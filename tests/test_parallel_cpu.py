@@ -948,3 +948,73 @@ def test_wgrad_stream_auto_policy():
     assert _wgrad_stream_auto(get_model("resnet50"))
     assert _wgrad_stream_auto(get_model("resnet18"))
     assert not _wgrad_stream_auto(get_model("vit_b_16"))
+
+
+def _worker_capture_agree(rank, world, port, q, fail_rank):
+    """rank ``fail_rank``'s graph capture raises; the others' would succeed (a fake that never gets
+    to replay: the MIN agreement must disable graphs on every rank at the same step)."""
+    try:
+        _init(rank, world, port)
+        from mi355x_dp.parallel import DataParallel, step_graph
+        calls = {"capture": 0, "replay": 0}
+
+        class FakeStep:
+            comm_mode = "none"
+
+            def __init__(self, engine, x):
+                calls["capture"] += 1
+                if rank == fail_rank:
+                    raise RuntimeError("injected capture failure")
+
+            def __call__(self, token, x):  # pragma: no cover - must never run
+                calls["replay"] += 1
+                raise AssertionError("replayed after a failed agreement")
+
+            def busy(self):
+                return False
+
+        step_graph.eligible = lambda engine, args, kwargs: True
+        step_graph.CapturedStep = FakeStep
+        torch.manual_seed(0)
+        ddp = DataParallel(_model(), foreign_optimizer=True)
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.05, momentum=0.9)
+        x, y = _data()
+        part = slice(rank * 8, (rank + 1) * 8)
+        import warnings
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            for _ in range(step_graph.AFTER + 3):
+                opt.zero_grad()
+                torch.nn.functional.cross_entropy(ddp(x[part]), y[part]).backward()
+                opt.step()
+        msgs = [str(m.message) for m in w if "graph capture" in str(m.message)]
+        q.put((rank, ddp.flat.data.clone().numpy(), calls, bool(ddp.__dict__.get("_graph_disabled")), msgs))
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, e, None, None, None))
+
+
+def test_graph_capture_agreement_is_rank_symmetric():
+    """a capture that fails on rank 1 only must leave BOTH ranks eager (MIN
+    all-reduce of the capture flag before any replay) -- no rank replays graphs while a peer runs
+    eagerly, no hang, and the replicas stay bit-identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_capture_agree, args=(r, 2, port, q, 1)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {r: rest for r, *rest in [q.get(timeout=120) for _ in ps]}
+    for p in ps:
+        p.join(60)
+    for r, (d, *_rest) in out.items():
+        assert not isinstance(d, Exception), f"rank {r}: {d!r}"
+    for r in (0, 1):
+        _d, calls, disabled, msgs = out[r]
+        assert disabled, f"rank {r} kept graphs enabled"
+        assert calls == {"capture": 1, "replay": 0}, (r, calls)
+        assert msgs, f"rank {r} did not warn"
+    assert "another rank" in out[0][3][0] and "injected" in out[1][3][0]
+    assert torch.equal(torch.from_numpy(out[0][0]), torch.from_numpy(out[1][0])), "replicas diverged"
