@@ -340,11 +340,14 @@ class Reducer {
       const at::Tensor& buf = comm_.defined() ? comm_ : grad_;
       trace_.emplace_back(next_, (r.second - r.first) * buf.element_size(), since_reset_us());
       if (pg_ && (pg_->getSize() > 1 || force_comm_)) {
-        const bool timed = timing_ && t0_ok_;
+        // GPU timeline only outside a capture: inside one the event would be a captured node and
+        // the probe stream (never captured) would wait on a captured Work
         hipStream_t cur_s = nullptr;
+        bool timed = timing_ && t0_ok_;
         if (timed) {
           cur_s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(grad_.device().index()).stream();
-          hipEventRecord(ev_ready_[next_], cur_s);
+          timed = !capturing(cur_s);
+          if (timed) hipEventRecord(ev_ready_[next_], cur_s);
         }
         at::Tensor slice = grad_.narrow(0, r.first, r.second - r.first);
         if (comm_.defined()) {

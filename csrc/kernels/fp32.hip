@@ -211,7 +211,11 @@ __device__ __forceinline__ void slab_geom4(int C, int& tpr, int& rp) {
   rp = FT / tpr;
 }
 
-__device__ __forceinline__ void block_reduce4(float4 s, float4 q, float* part, int C, int cb) {
+// mv (forward statistics): the sums are of x - k with k = x[rb] (the block's first row, per channel)
+// and the block writes its (mean, M2) instead -- shifted sums keep E[x^2] - mean^2 from cancelling
+// when |mean| >> std; the finalize merges the blocks with Chan's formula
+__device__ __forceinline__ void block_reduce4(float4 s, float4 q, float* part, int C, int cb,
+                                              const float* mv_x = nullptr, int mv_rb = 0, int mv_n = 0) {
   __shared__ float red[2][FT * 4];
   int tpr, rp;
   slab_geom4(C, tpr, rp);
@@ -222,6 +226,13 @@ __device__ __forceinline__ void block_reduce4(float4 s, float4 q, float* part, i
   for (int c = t; c < cw; c += FT) {
     float x = 0.f, y = 0.f;
     for (int r = 0; r < rp; ++r) { x += red[0][r * cw + c]; y += red[1][r * cw + c]; }
+    if (mv_x && cb + c < C) {
+      const float k = mv_x[(int64_t)mv_rb * C + cb + c], n = (float)mv_n;
+      const float d = x / n;                 // mean of x - k
+      const float m2 = fmaxf(y - x * d, 0.f);  // sum (x - k)^2 - n d^2 = sum (x - mean)^2
+      x = k + d;
+      y = m2;
+    }
     part[(int64_t)(blockIdx.x * 2) * C + cb + c] = x;
     part[(int64_t)(blockIdx.x * 2 + 1) * C + cb + c] = y;
   }
@@ -240,10 +251,12 @@ __global__ __launch_bounds__(FT) void bnf_stats_kernel(const float* __restrict__
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
   float4 mu = s;
   if (BWD) mu = *(const float4*)(mean + c);
+  else if (rb < re) mu = *(const float4*)(x + (int64_t)rb * C + c);  // forward: the shift k
   for (int r = rb + r0; r < re; r += rp) {
     const int64_t off = (int64_t)r * C + c;
-    const float4 xv = *(const float4*)(x + off);
+    float4 xv = *(const float4*)(x + off);
     if (!BWD) {
+      xv.x -= mu.x; xv.y -= mu.y; xv.z -= mu.z; xv.w -= mu.w;
       s.x += xv.x; s.y += xv.y; s.z += xv.z; s.w += xv.w;
       q.x += xv.x * xv.x; q.y += xv.y * xv.y; q.z += xv.z * xv.z; q.w += xv.w * xv.w;
     } else {
@@ -258,11 +271,12 @@ __global__ __launch_bounds__(FT) void bnf_stats_kernel(const float* __restrict__
       q.z += d.z * (xv.z - mu.z); q.w += d.w * (xv.w - mu.w);
     }
   }
-  block_reduce4(s, q, part, C, cb);
+  if (BWD) block_reduce4(s, q, part, C, cb);
+  else block_reduce4(s, q, part, C, cb, x, rb, max(re - rb, 1));
 }
 
 struct BnF32Fin {
-  int M, C, nblk;
+  int M, C, nblk, rpb;
   float eps, momentum;
   const float* gamma; const float* beta;
   float* rmean; float* rvar; int64_t* nbt;
@@ -278,13 +292,27 @@ __global__ void bnf_finalize_kernel(const float* __restrict__ part, BnF32Fin f) 
   if (!BWD && c == 0 && f.nbt) f.nbt[0] += 1;
   if (c >= f.C) return;
   double s = 0.0, q = 0.0;
-  for (int b = 0; b < f.nblk; ++b) {
-    s += part[(int64_t)(2 * b) * f.C + c];
-    q += part[(int64_t)(2 * b + 1) * f.C + c];
+  if (BWD) {
+    for (int b = 0; b < f.nblk; ++b) {
+      s += part[(int64_t)(2 * b) * f.C + c];
+      q += part[(int64_t)(2 * b + 1) * f.C + c];
+    }
+  } else {
+    // Chan's parallel merge of the blocks' (count, mean, M2), in block order, fp64
+    double n = 0.0;
+    for (int b = 0; b < f.nblk; ++b) {
+      const double nb = (double)(min(f.M, (b + 1) * f.rpb) - b * f.rpb);
+      if (nb <= 0) continue;
+      const double mb = part[(int64_t)(2 * b) * f.C + c], m2b = part[(int64_t)(2 * b + 1) * f.C + c];
+      const double d = mb - s, nn = n + nb;
+      s += d * nb / nn;
+      q += m2b + d * d * n * nb / nn;
+      n = nn;
+    }
   }
   if (!BWD) {
-    const double mean = s / f.M;
-    double var = q / f.M - mean * mean;
+    const double mean = s;
+    double var = q / f.M;
     if (var < 0) var = 0;
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
     f.save_mean[c] = (float)mean;
@@ -508,7 +536,7 @@ MI_API int mi_f32_bn_fwd_train(const float* x, const float* res, float* y, int M
   hipLaunchKernelGGL(bnf_stats_kernel<false>, dim3(nblk, cdiv(C, tpr * 4)), dim3(FT), 0, st, x, nullptr, nullptr,
                      nullptr, part, M, C, rpb, 0);
   BnF32Fin f{};
-  f.M = M; f.C = C; f.nblk = nblk; f.eps = eps; f.momentum = momentum; f.gamma = gamma; f.beta = beta;
+  f.M = M; f.C = C; f.nblk = nblk; f.rpb = rpb; f.eps = eps; f.momentum = momentum; f.gamma = gamma; f.beta = beta;
   f.rmean = rmean; f.rvar = rvar; f.nbt = nbt; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.scale = scale; f.shift = shift;
   hipLaunchKernelGGL(bnf_finalize_kernel<false>, dim3(cdiv(C, 256)), dim3(256), 0, st, part, f);

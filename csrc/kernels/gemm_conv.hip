@@ -1891,6 +1891,15 @@ MI_API void mi_set_conv256_min_k(int k) {
   g_conv256_min_k = k;
 }
 
+// conv_panel.hip: persistent resident-weight kernel for the short-K 1x1 convolutions (forward)
+extern "C" int mi_panel_stat_rows(int M, int N, int K);
+extern "C" int mi_panel_conv1x1(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C,
+                                int K, int stride, int P, int Q, hipStream_t st);
+static int panel_rows_fwd(int M, int N, int C, int R, int S, int pad, int H, int W, int P, int Q, int stride) {
+  if (R != 1 || S != 1 || pad != 0 || C % 64 != 0 || P != (H - 1) / stride + 1 || Q != (W - 1) / stride + 1) return 0;
+  return mi_panel_stat_rows(M, N, C);
+}
+
 // stem_conv.hip: persistent LDS-ring kernel for the 7x7/2 stem on 8-channel input
 extern "C" int mi_stem_conv_ok(int C, int K, int R, int S, int stride, int pad, int Q);
 extern "C" int mi_stem_conv_stat_rows(int Nb, int P);
@@ -1913,6 +1922,7 @@ MI_API int mi_conv_stat_rows_g(int Nb, int H, int W, int C, int K, int R, int S,
   const int M = Nb * P * Q;
   if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return mi_stem_conv_stat_rows(Nb, P);
   if (C % 64 == 0 && use_gemm256_conv(M, K, C, R * S * C)) return 2 * cdiv(M, 256);
+  if (const int pr = panel_rows_fwd(M, K, C, R, S, pad, H, W, P, Q, stride); pr > 0) return pr;
   const int rp = C % 64 == 0 ? halo_rp(M, K, R, S, stride, pad, C, H, W, P, Q) : 0;
   if (rp > 0) return Nb * cdiv(P, rp);
   return cdiv(M, nt_choice(M, K) == 2 ? 64 : 128);
@@ -1922,6 +1932,8 @@ MI_API int mi_conv_stat_rows_g(int Nb, int H, int W, int C, int K, int R, int S,
 // for shapes outside the halo tiling (1x1 / strided convs, GEMMs).
 MI_API int mi_conv_stat_rows(int M, int N, int Cs, int RS) {
   if (use_gemm256_conv(M, N, Cs, RS * Cs)) return 2 * cdiv(M, 256);
+  if (RS == 1 && Cs % 64 == 0)  // a 1x1 (pad 0) conv forward on the panel kernel
+    if (const int pr = mi_panel_stat_rows(M, N, Cs); pr > 0) return pr;
   const int bm = nt_choice(M, N) == 2 ? 64 : 128;
   return cdiv(M, bm);
 }
@@ -1943,6 +1955,8 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
   if (!out_f32 && !bias && use_gemm256_conv(Nb * P * Q, K, C, R * S * C))
     return mi_gemm256_conv(1, x, w, y, stats, 0, nullptr, nullptr, nullptr, 0, Nb, H, W, C, P, Q, R, S, stride, pad,
                            K, st);
+  if (!out_f32 && !bias && panel_rows_fwd(Nb * P * Q, K, C, R, S, pad, H, W, P, Q, stride) > 0)
+    return mi_panel_conv1x1(x, w, y, stats, Nb, H, W, C, K, stride, P, Q, st);
   NTArgs a{};
   a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias; a.stats = stats;
   a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
@@ -2125,6 +2139,7 @@ MI_API int mi_conv_nol_ok(int Nb, int H, int W, int C, int K, int R, int S, int 
   if (C % 64 != 0 || C > NOL_MAX_C || K % 64 != 0 || stride > 2 || !glds_on()) return 0;
   if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return 0;
   if (use_gemm256_conv(Nb * P * Q, K, C, R * S * C)) return 0;                    // forward
+  if (panel_rows_fwd(Nb * P * Q, K, C, R, S, pad, H, W, P, Q, stride) > 0) return 0;  // forward (panel)
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K)) return 0;    // data gradient
   // small grids keep the materialised path: there the 128-tile kernels split K (nt_split_blocks),
   // which the normalize-on-load variants do not -- and the bytes saved are negligible

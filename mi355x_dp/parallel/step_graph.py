@@ -92,6 +92,30 @@ def capture_safe(engine) -> bool:
     return False
 
 
+def _backend(engine) -> str:
+    import torch.distributed as dist
+    try:
+        pg = engine.process_group if engine.process_group is not None else dist.distributed_c10d._get_default_group()
+        return str(dist.get_backend(pg))
+    except Exception:
+        return ""
+
+
+def gates_stream_high_priority(engine) -> bool:
+    """gates are queued BEFORE the replay, so the stream that carries them (and the collectives
+    behind them) must never share an in-order hardware queue with the normal-priority stream that
+    replays the graph: HIP pools hardware queues per priority, so that stream must be high priority.
+    smddp: its comm stream (MI355X_DP_SMDDP_HIPRIO, default high); otherwise the engine's gate stream
+    (MI355X_DP_GATE_PRIO, default -1 = high).  torch nccl never qualifies: ProcessGroupNCCL's own
+    normal-priority stream would wait on the gate events."""
+    be = _backend(engine)
+    if be == "nccl":
+        return False
+    if be == "smddp" and os.environ.get("MI355X_DP_SMDDP_HIPRIO", "1").startswith("0"):
+        return False
+    return int(os.environ.get("MI355X_DP_GATE_PRIO", "-1")) < 0
+
+
 def comm_mode(engine) -> str:
     """none | capture | gates | after (module docstring)"""
     if not engine.comm_on:
@@ -104,7 +128,7 @@ def comm_mode(engine) -> str:
         if safe:
             return "capture"
         want = "gates"
-    if want == "gates" and GATES:
+    if want == "gates" and GATES and gates_stream_high_priority(engine):
         return "gates"
     return "after"
 

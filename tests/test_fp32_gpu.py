@@ -83,6 +83,34 @@ def test_f32_batchnorm_train(fp32_mode, shape, relu, res):
     assert rel(rm, rm_r) < 1e-6 and rel(rv, rv_r) < 1e-6 and int(nbt) == 1
 
 
+@pytest.mark.parametrize("offset", [100.0, -1000.0])
+def test_f32_batchnorm_large_mean(fp32_mode, offset):
+    """channel means far above the spread (x + 100, x - 1000).  E[x^2] - mean^2 from fp32
+    partials cancels there; the per-block shifted (mean, M2) partials merged with Chan's formula keep
+    the batch variance, invstd and running variance at fp32 accuracy against fp64."""
+    N, C, H = 32, 64, 16
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, C, H, H, generator=g, dtype=torch.float64) * 0.5 + offset
+    gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(C, generator=g, dtype=torch.float64)
+    rm_r, rv_r = torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64)
+    yr = F.batch_norm(x, rm_r, rv_r, gamma, beta, True, 0.1, 1e-5)
+    dev = "cuda"
+    xc = x.float().to(dev).contiguous(memory_format=CL)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    y = fp32_mode.batch_norm_act(xc, gamma.float().to(dev), beta.float().to(dev), rm, rv, nbt, True, 0.1, 1e-5,
+                                 False, None)
+    torch.cuda.synchronize()
+    # the fp32 input itself carries |offset| * 2^-24 of rounding: compare against fp64 of THAT input
+    yr32 = F.batch_norm(xc.double().cpu(), torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64),
+                        gamma, beta, True, 0.1, 1e-5)
+    assert rel(y, yr32) < 1e-5, rel(y, yr32)
+    rv32 = 0.9 + 0.1 * xc.double().cpu().permute(1, 0, 2, 3).reshape(C, -1).var(1, unbiased=True)
+    assert rel(rv, rv32) < 1e-5, rel(rv, rv32)
+    assert rel(y, yr) < 1e-3
+
+
 def test_f32_pool_and_linear(fp32_mode):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(6, 16, 15, 15, generator=g, dtype=torch.float64)

@@ -1018,3 +1018,24 @@ def test_graph_capture_agreement_is_rank_symmetric():
         assert msgs, f"rank {r} did not warn"
     assert "another rank" in out[0][3][0] and "injected" in out[1][3][0]
     assert torch.equal(torch.from_numpy(out[0][0]), torch.from_numpy(out[1][0])), "replicas diverged"
+
+
+def test_graph_comm_mode_gates_need_high_priority(monkeypatch):
+    """ADVICE r5: 'gates' (queued before the replay) only on a high-priority gate / comm stream;
+    torch nccl, or a normal-priority gate or smddp comm stream, falls back to 'after'."""
+    from types import SimpleNamespace
+    from mi355x_dp.parallel import step_graph
+    eng = SimpleNamespace(comm_on=True, reducer=object(), _comm_hook=None)
+    monkeypatch.setattr(step_graph, "capture_safe", lambda e: False)
+    monkeypatch.setattr(step_graph, "GRAPH_COMM", "auto")
+    for be, env, want in [("smddp", {}, "gates"), ("smddp", {"MI355X_DP_SMDDP_HIPRIO": "0"}, "after"),
+                          ("smddp", {"MI355X_DP_GATE_PRIO": "0"}, "after"), ("nccl", {}, "after"),
+                          ("gloo", {}, "gates")]:
+        monkeypatch.setattr(step_graph, "_backend", lambda e, be=be: be)
+        for k in ("MI355X_DP_SMDDP_HIPRIO", "MI355X_DP_GATE_PRIO"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        assert step_graph.comm_mode(eng) == want, (be, env)
+    monkeypatch.setattr(step_graph, "capture_safe", lambda e: True)
+    assert step_graph.comm_mode(eng) == "capture"
