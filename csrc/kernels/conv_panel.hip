@@ -20,10 +20,11 @@
 //    loads in one in-order counter, so the count adds the epilogue stores issued since the target
 //    load (every epilogue issues a fixed number of stores: rows past M go to an out-of-range
 //    buffer offset and are dropped, never skipped);
-//  * the epilogue stages the unit's bf16 tile through the ring slot it just consumed (free until
-//    the next issue), reads it back as 16-byte row chunks (one fixed 8-channel chunk per lane) and
-//    stores full chunks; the lane accumulates that chunk's statistics over ALL its units in
-//    registers, reduced across lanes and waves once per block (one statistics row per block).
+//  * the epilogue stores the unit's bf16 tile straight from the accumulators (permlane16 swaps
+//    widen the MFMA fragments to 16-byte row chunks): nothing in the loop writes LDS, because an
+//    LDS store with LDS-DMA in flight makes hipcc drain vmcnt(0) before it; every lane accumulates
+//    the statistics of the columns it stores over ALL its units in registers, reduced across
+//    lanes and waves once per block (one statistics row per block).
 #include "common.h"
 
 #include <algorithm>
@@ -48,43 +49,58 @@ struct PanelArgs {
   int a_bytes, b_bytes, c_bytes;
   // row m -> element offset of its A row: plain (gather == 0): m * lda; 1x1 stride-s gather:
   // pixel (img, p, q) of the P x Q output grid reads input pixel (img, p * s, q * s) of H x W
+  // gather 2: 3x3 / stride-1 / pad-1 taps (k-step kt = tap kt / cpt, channel chunk kt % cpt): row
+  //   m = pixel (img, h, w) reads pixel (h + tsg (r - 1), w + tsg (s - 1)) of the same H x W grid, zero
+  //   outside (tsg +1: forward, -1: data gradient, whose weights wt = [C][3][3][K] run the flipped taps)
   int gather, lda, H, W, stride;
+  int tsg, cpt;
   FastDiv fPQ, fQ;
+  // data-gradient epilogues (EPI 1; nt_kernel's epi 0 / 3 / 4 / 5 with the same rounding points):
+  //   epi 3: C <- bf16(acc) + aux;  epi 4: dz = bf16(acc) * mask;  epi 5: dz = (bf16(acc) + C) * mask
+  //   (C read before it is overwritten: a block input's residual gradient sum), mask = the ReLU of
+  //   the BN that produced this conv's input: bit of mbits (one byte per 8 channels) or y = aux > 0;
+  //   stats <- (sum dz, sum dz * (aux2 - mean)) with aux2 the BN input
+  //   aux_even: the gradient in C exists only at even (h, w) of the P x Q grid (fPQ / fQ), 0 elsewhere
+  int epi, bn_relu, aux_even;
+  const bf16_t* aux;
+  const bf16_t* aux2;
+  const float* mean;
+  const uint8_t* mbits;
 };
 
 #define PN_VMWAIT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-template <int S, int ST>
-__device__ __forceinline__ void pn_wait(int cnt) {
-  // younger ops than the target k-step's loads: (S - 1) k-steps of 4 loads + cnt epilogues of ST
-  // stores; vmcnt holds 6 bits (every count here is <= 12 + 3 * 8 = 36)
-  static_assert(4 * (S - 1) + ST * (S - 1) <= 63, "vmcnt range");
-  if constexpr (S == 2) {
-    if (cnt == 0) PN_VMWAIT(4); else if constexpr (ST == 8) PN_VMWAIT(12); else PN_VMWAIT(8);
-  } else if constexpr (S == 3) {
-    if constexpr (ST == 8) {
-      if (cnt == 0) PN_VMWAIT(8); else if (cnt == 1) PN_VMWAIT(16); else PN_VMWAIT(24);
-    } else {
-      if (cnt == 0) PN_VMWAIT(8); else if (cnt == 1) PN_VMWAIT(12); else PN_VMWAIT(16);
-    }
-  } else {
-    static_assert(S == 4, "ring depth 2-4");
-    if constexpr (ST == 8) {
-      if (cnt == 0) PN_VMWAIT(12); else if (cnt == 1) PN_VMWAIT(20); else if (cnt == 2) PN_VMWAIT(28); else PN_VMWAIT(36);
-    } else {
-      if (cnt == 0) PN_VMWAIT(12); else if (cnt == 1) PN_VMWAIT(16); else if (cnt == 2) PN_VMWAIT(20); else PN_VMWAIT(24);
-    }
-  }
+template <int N>
+__device__ __forceinline__ void pn_vmwait() {
+  static_assert(N >= 0 && N <= 63, "vmcnt holds 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// BN: block panel width (columns), WN: wave tile width (64 or 128), S: ring slots per wave
-template <int BN, int WN, int S>
-__global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
+// wait for the k-step issued S - 1 issues ago: younger ops are (S - 1) k-steps of 4 loads plus cnt
+// epilogue events of EV ops each (the stores of a unit, and in EPI 1 the next unit's operand loads)
+template <int S, int EV>
+__device__ __forceinline__ void pn_wait(int cnt) {
+  constexpr int B = 4 * (S - 1);
+  if (cnt <= 0) pn_vmwait<B>();
+  else if (cnt == 1) pn_vmwait<B + EV>();
+  else if (S == 2 || cnt == 2) pn_vmwait<B + 2 * EV < 64 ? B + 2 * EV : 63>();
+  else pn_vmwait<B + 3 * EV < 64 ? B + 3 * EV : 63>();
+}
+
+// BN: block panel width (columns), WN: wave tile width (64 or 128), S: ring slots per wave,
+// EPI: 0 forward (+ (sum, sumsq) statistics), 1 data gradient (PanelArgs::epi, WN 64)
+template <int BN, int WN, int S, int EPI>
+__global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
   constexpr int WNW = BN / WN, WMW = 8 / WNW;  // waves along N / along M
   constexpr int NJ = WN / 16;
-  constexpr int ST = WN / 16;                  // epilogue stores per lane per unit (32 x WN bf16)
+  constexpr int NP = NJ / 2;                   // fragment pairs: one 16-byte chunk each per row block
+  constexpr int ST = 2 * NP;                   // epilogue stores per lane per unit (32 x WN bf16)
+  // EPI 1: the next unit's epilogue operands are loaded right after a unit's stores, one unit ahead:
+  // per chunk the accumulated-into gradient (or the residual), the BN input and the ReLU source
+  constexpr int EL = EPI == 1 ? 3 * ST : 0;
   constexpr int RING_U4 = 8 * S * PN_SLOT_U4;
   static_assert(WNW * WMW == 8 && (WN == 64 || WN == 128), "8 waves");
+  static_assert(EPI == 0 || WN == 64, "data-gradient operands held in registers: 64-column waves");
   // ONE LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
   // [8 waves][S slots] A rings, then the weight panel [nk][BN][8 chunks]
   __shared__ __attribute__((aligned(16))) uint4 smem[PN_LDS_U4];
@@ -102,6 +118,17 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)a.C, (short)0, a.c_bytes, 0x00020000);
+  // EPI 1 operand resources (same layout as C; mbits: one byte per 8 channels)
+  __amdgpu_buffer_rsrc_t rsY = rsC, rsX = rsC, rsK = rsC;
+  if constexpr (EPI == 1) {
+    rsY = __builtin_amdgcn_make_buffer_rsrc((void*)(a.epi == 3 ? a.aux : a.C), (short)0,
+                                            (a.epi == 3 || a.epi == 5) ? a.c_bytes : 0, 0x00020000);
+    rsX = __builtin_amdgcn_make_buffer_rsrc((void*)a.aux2, (short)0, (a.epi >= 4 && a.stats) ? a.c_bytes : 0,
+                                            0x00020000);
+    const bool relu = a.epi >= 4 && a.bn_relu;
+    rsK = a.mbits ? __builtin_amdgcn_make_buffer_rsrc((void*)a.mbits, (short)0, relu ? a.c_bytes / 16 : 0, 0x00020000)
+                  : __builtin_amdgcn_make_buffer_rsrc((void*)a.aux, (short)0, relu ? a.c_bytes : 0, 0x00020000);
+  }
 
   // ---- the weight panel, once: piece p = 8 rows x 128 B of k-step kt (lane-linear image, chunk
   // c of row n holds logical chunk c ^ (n & 7))
@@ -131,6 +158,7 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
   const int lr = lane >> 3, lc = (lane & 7) ^ (lane >> 3);  // lane's row in a piece, source chunk
   uint32_t ioff[4];
   bool iok[4];
+  int ih[4], iw[4];  // gather 2: the row's pixel (h, w)
   int iu = 0, ikt = 0;
   auto set_rows = [&](int lu) {
 #pragma unroll
@@ -139,7 +167,13 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
       iok[u] = lu < nu && m < a.M;
       const uint32_t mm = iok[u] ? (uint32_t)m : 0u;
       uint32_t rowe;
-      if (a.gather) {
+      if (a.gather == 2) {
+        const uint32_t img = fdiv(mm, a.fPQ), rem = mm - img * a.fPQ.d;
+        const uint32_t p = fdiv(rem, a.fQ), q = rem - p * a.fQ.d;
+        ih[u] = (int)p;
+        iw[u] = (int)q;
+        rowe = mm * (uint32_t)a.lda;  // the tap's shift is added per k-step
+      } else if (a.gather) {
         const uint32_t img = fdiv(mm, a.fPQ), rem = mm - img * a.fPQ.d;
         const uint32_t p = fdiv(rem, a.fQ), q = rem - p * a.fQ.d;
         rowe = ((img * (uint32_t)a.H + p * (uint32_t)a.stride) * (uint32_t)a.W + q * (uint32_t)a.stride) *
@@ -152,10 +186,23 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
   };
   auto issue_next = [&](int slot) {
     uint4* dst = ring + slot * PN_SLOT_U4;
+    if (a.gather == 2) {
+      const int t = ikt / a.cpt, kc = ikt - t * a.cpt;
+      const int r = t / 3, sx = t - 3 * r;
+      const int dh = a.tsg * (r - 1), dw = a.tsg * (sx - 1);
+      const int dpix = (dh * a.W + dw) * a.lda + kc * 64;  // element shift of the tap
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t vo = iok[u] ? ioff[u] + (uint32_t)ikt * 128u : PN_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = iok[u] && (unsigned)(ih[u] + dh) < (unsigned)a.H && (unsigned)(iw[u] + dw) < (unsigned)a.W;
+        const uint32_t vo = ok ? ioff[u] + (uint32_t)dpix * 2u : PN_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t vo = iok[u] ? ioff[u] + (uint32_t)ikt * 128u : PN_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
+      }
     }
     if (++ikt == nk) {
       ikt = 0;
@@ -169,15 +216,54 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float s1[8], s2[8];
+  // per-lane statistics of the columns the lane stores (see epilogue): pair p of fragments, 8 columns
+  float s1[NP][8], s2[NP][8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) { s1[q] = 0.f; s2[q] = 0.f; }
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { s1[p][q] = 0.f; s2[p][q] = 0.f; }
   const bool want_stats = a.stats != nullptr;
-  // the lane's fixed epilogue chunk (8 channels) and the rows it reads back
-  constexpr int CPR = WN / 8;     // 16-B chunks per staged row
-  constexpr int RPI = 64 / CPR;   // rows per read instruction
-  const int ec = lane % CPR, er = lane / CPR;
-  const int ncol = n0 + wn * WN + ec * 8;  // output column of the lane's chunk
+  // the lane's first output column within a fragment pair (after the permlane16 swap)
+  const int pcol = 16 * (fq & 1) + 8 * (fq >> 1);
+  const int ncol0 = n0 + wn * WN + pcol;
+  // EPI 1: the BN mean of the lane's columns, and the epilogue operands of the next unit
+  float mu[EPI == 1 ? NP : 1][8];
+  uint4 ey[2][NP], ex[2][NP], ek[2][NP];  // ek: mask byte in .x (mbits) or the BN output chunk
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) mu[p][q] = (a.epi >= 4 && a.stats) ? a.mean[ncol0 + 32 * p + q] : 0.f;
+  }
+  // EL loads per call, every lane, whatever the epilogue needs (an unused operand's resource has
+  // range 0: the load is dropped but still counted, so the waits' counts never depend on it)
+  auto epi_issue = [&](int lu) {
+    if constexpr (EPI == 1) {
+      const int mb = (u0 + lu) * 32 + fr;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = mb + 16 * i;
+        bool even = true;
+        if (a.aux_even && m < a.M) {
+          const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
+          const uint32_t h = fdiv(rem, a.fQ), w = rem - h * a.fQ.d;
+          even = ((h | w) & 1u) == 0u;
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const int col = ncol0 + 32 * p;
+          const bool ok = lu < nu && m < a.M;
+          const uint32_t off = ok ? (uint32_t)(m * a.ldc + col) * 2u : PN_OOB;
+          ey[i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsY, even ? off : PN_OOB, 0, 2));
+          ex[i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsX, off, 0, 0));
+          if (a.mbits)
+            ek[i][p].x = __builtin_amdgcn_raw_buffer_load_b8(rsK, ok ? off >> 4 : PN_OOB, 0, 0);
+          else
+            ek[i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsK, off, 0, 2));
+        }
+      }
+    }
+  };
 
   auto compute = [&](const uint4* As, int kt) {
     const uint4* Bs = bpanel + (kt * BN + wn * WN) * 8;
@@ -197,41 +283,63 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
     }
   };
 
-  // epilogue of unit lu through the 4 KB slot it consumed: lane (fr, fq) holds D[n = 16 j + 4 fq +
-  // r][m = 16 i + fr]; rows are staged with the 16-B chunk index XOR-swizzled by the row (ds_write_b64
-  // groups of 16 rows hit distinct bank pairs), read back one chunk per lane
-  auto epilogue = [&](uint4* Cs, int lu) {
-    char* cb = (char*)Cs;
-    constexpr int HALVES = WN == 128 ? 2 : 1;  // 16 rows x 256 B or 32 rows x 128 B per pass
+  // epilogue of unit lu straight from the accumulators -- no LDS write (an LDS store while LDS-DMA
+  // loads are in flight makes hipcc drain vmcnt(0) first: the prefetch would die at every unit).
+  // Lane (fr, fq) holds D[n = 16 j + 4 fq + r][m = 16 i + fr] of each fragment; the permlane16 swap
+  // of fragment pair (2p, 2p + 1) leaves it row 16 i + fr, columns 32 p + pcol + [0, 8): one 16-byte
+  // store per (i, p), 16 rows x 64 contiguous bytes per store instruction (gemm256p.hip's flush)
+  auto epilogue = [&](int lu) {
+    const int mb = (u0 + lu) * 32 + fr;
 #pragma unroll
-    for (int h = 0; h < HALVES; ++h) {
+    for (int i = 0; i < 2; ++i) {
+      const int m = mb + 16 * i;
 #pragma unroll
-      for (int ii = 0; ii < 2 / HALVES; ++ii) {
-        const int i = h + ii;  // fragment row block
-        const int row = WN == 128 ? fr : 16 * i + fr;
-        const int sw = WN == 128 ? row : ((row >> 1) & 7);
+      for (int p = 0; p < NP; ++p) {
+        const f32x4 v0 = acc[i][2 * p], v1 = acc[i][2 * p + 1];
+        const uint32_t p0 = pack2bf(v0[0], v0[1]), p1 = pack2bf(v0[2], v0[3]);
+        const uint32_t q0 = pack2bf(v1[0], v1[1]), q1 = pack2bf(v1[2], v1[3]);
+        const auto x0 = __builtin_amdgcn_permlane16_swap(p0, q0, false, false);
+        const auto x1 = __builtin_amdgcn_permlane16_swap(p1, q1, false, false);
+        uint4 o = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+        if constexpr (EPI == 0) {
+          if (want_stats) {
+            float f[8];
+            unpack8(o, f);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const f32x4 v = acc[i][j];
-          const int pc = (2 * j + (fq >> 1)) ^ sw;
-          *(uint2*)(cb + row * (WN * 2) + pc * 16 + (fq & 1) * 8) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-        }
-      }
-      constexpr int NR = WN == 128 ? 16 : 32;  // rows staged in this pass
+            for (int q = 0; q < 8; ++q) { s1[p][q] += f[q]; s2[p][q] = fmaf(f[q], f[q], s2[p][q]); }
+          }
+        } else if (a.epi == 3) {
+          float f[8], g[8];
+          unpack8(o, f);
+          unpack8(ey[i][p], g);
 #pragma unroll
-      for (int u = 0; u < NR / RPI; ++u) {
-        const int rr = er + RPI * u;
-        const int sw = WN == 128 ? rr : ((rr >> 1) & 7);
-        const uint4 v = *(const uint4*)(cb + rr * (WN * 2) + ((ec ^ sw) * 16));
-        const int m = (u0 + lu) * 32 + (WN == 128 ? 16 * h : 0) + rr;
-        if (want_stats) {
+          for (int q = 0; q < 8; ++q) f[q] += g[q];
+          o = pack8(f);
+        } else if (a.epi >= 4) {
           float f[8];
-          unpack8(v, f);
+          unpack8(o, f);
+          if (a.epi == 5) {
+            float g[8];
+            unpack8(ey[i][p], g);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] = fmaf(f[q], f[q], s2[q]); }
+            for (int q = 0; q < 8; ++q) f[q] += g[q];
+          }
+          if (a.bn_relu) {
+            const uint32_t bits = a.mbits ? ek[i][p].x : nz_bits8(ek[i][p]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = ((bits >> q) & 1u) ? f[q] : 0.f;
+          }
+          o = pack8(f);
+          if (want_stats) {
+            float xv[8];
+            unpack8(ex[i][p], xv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { s1[p][q] += f[q]; s2[p][q] = fmaf(f[q], xv[q] - mu[p][q], s2[p][q]); }
+          }
         }
-        const uint32_t off = (m < a.M && ncol < a.N) ? (uint32_t)(m * a.ldc + ncol) * 2u : PN_OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsC, off, 0, 0);
+        const int col = ncol0 + 32 * p;
+        const uint32_t off = (m < a.M && col < a.N) ? (uint32_t)(m * a.ldc + col) * 2u : PN_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsC, off, 0, 0);
       }
     }
 #pragma unroll
@@ -241,6 +349,7 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
   };
 
   // ---- main loop over the wave's k-steps
+  epi_issue(0);  // before every ring load: never younger than a k-step's loads
   set_rows(0);
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue_next(s);
@@ -248,12 +357,13 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
   int kt = 0, lu = 0, slot = 0;
   for (int g = 0; g < G; ++g) {
     issue_next(slot == 0 ? S - 1 : slot - 1);  // k-step g + S - 1 into the slot k-step g - 1 used
-    pn_wait<S, ST>(__builtin_popcount(ehist & ((1u << (S - 1)) - 1u)));
+    pn_wait<S, ST + EL>(__builtin_popcount(ehist & ((1u << (S - 1)) - 1u)));
     uint4* cur = ring + slot * PN_SLOT_U4;
     compute(cur, kt);
     ehist <<= 1;
     if (++kt == nk) {
-      epilogue(cur, lu);
+      epilogue(lu);
+      epi_issue(lu + 1);  // past the last unit: dropped loads (the counts hold)
       ehist |= 1u;
       kt = 0;
       ++lu;
@@ -261,26 +371,31 @@ __global__ __launch_bounds__(512) void panel_fwd_kernel(PanelArgs a) {
     slot = slot + 1 == S ? 0 : slot + 1;
   }
 
-  // ---- statistics: lanes sharing a chunk, then the WMW waves of each column sub-panel (fixed order)
+  // ---- statistics: the 16 lanes of a row share their columns (xor over fr), then the WMW waves of
+  // each column sub-panel through LDS, in a fixed order
   if (want_stats) {
 #pragma unroll
-    for (int o = CPR; o < 64; o <<= 1)
+    for (int o = 1; o < 16; o <<= 1)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        s1[q] += __shfl_xor(s1[q], o, 64);
-        s2[q] += __shfl_xor(s2[q], o, 64);
-      }
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          s1[p][q] += __shfl_xor(s1[p][q], o, 64);
+          s2[p][q] += __shfl_xor(s2[p][q], o, 64);
+        }
   }
   PN_VMWAIT(0);  // the ring's trailing dummy loads still write LDS
   __syncthreads();
   if (want_stats) {
     float* red = (float*)smem;  // [8 waves][2][WN]
-    if (lane < CPR) {
+    if (fr == 0) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        red[(wid * 2 + 0) * WN + ec * 8 + q] = s1[q];
-        red[(wid * 2 + 1) * WN + ec * 8 + q] = s2[q];
-      }
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          red[(wid * 2 + 0) * WN + 32 * p + pcol + q] = s1[p][q];
+          red[(wid * 2 + 1) * WN + 32 * p + pcol + q] = s2[p][q];
+        }
     }
     __syncthreads();
     for (int c = tid; c < 2 * BN; c += 512) {
@@ -304,14 +419,15 @@ struct PanelPlan {
   int bn = 0, wn = 0, s = 0, npanel = 0, nb = 0;
 };
 
-// panel width / ring depth for an N x K weight panel; bn == 0: not eligible
-PanelPlan panel_plan(int M, int N, int K) {
+// panel width / ring depth for an N x K weight panel; bn == 0: not eligible.  dgrad: the data-gradient
+// variant (64-column waves: its next-unit epilogue operands live in registers)
+PanelPlan panel_plan(int M, int N, int K, bool dgrad) {
   PanelPlan p;
   if (g_pn_mode < 0) {
     const char* e = std::getenv("MI355X_DP_PANEL");
     g_pn_mode = (e && e[0] == '0') ? 0 : 1;
   }
-  if (!g_pn_mode || K % 64 != 0 || K > 512 || N % 64 != 0 || M < (g_pn_mode == 2 ? 1 : PN_MIN_M)) return p;
+  if (!g_pn_mode || K % 64 != 0 || K > 576 || N % 64 != 0 || M < (g_pn_mode == 2 ? 1 : PN_MIN_M)) return p;
   if (g_pn_cus == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -320,16 +436,18 @@ PanelPlan panel_plan(int M, int N, int K) {
   }
   const int64_t kb = (int64_t)K * 2;  // bytes per panel row
   if (N % 256 == 0 && 256 * kb <= 64 * 1024) {
-    p.bn = 256; p.wn = 128;
+    p.bn = 256;
   } else if (N % 128 == 0 && 128 * kb <= 64 * 1024) {
-    p.bn = 128; p.wn = 128;
-  } else if (64 * kb <= 64 * 1024) {
-    p.bn = 64; p.wn = 64;
+    p.bn = 128;
+  } else if (64 * kb <= 96 * 1024) {
+    p.bn = 64;
   } else {
     return PanelPlan{};
   }
+  p.wn = dgrad ? 64 : std::min(p.bn, 128);
+  // ring depth from what the weight panel leaves of the 160 KB: 8 waves x S x 4 KB
   const int64_t bpanel = p.bn * kb;
-  p.s = bpanel <= 32 * 1024 ? 4 : 3;
+  p.s = bpanel <= 32 * 1024 ? 4 : (bpanel <= 64 * 1024 ? 3 : 2);
   p.npanel = N / p.bn;
   const int units = cdiv(M, 32);
   const int wm = 8 / (p.bn / p.wn);
@@ -337,9 +455,34 @@ PanelPlan panel_plan(int M, int N, int K) {
   return p;
 }
 
-template <int BN, int WN, int S>
-void launch_panel(const PanelArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((panel_fwd_kernel<BN, WN, S>), dim3(grid), dim3(512), 0, st, a);
+template <int BN, int WN, int EPI>
+void launch_panel(const PanelArgs& a, int s, int grid, hipStream_t st) {
+  if (s == 4)
+    hipLaunchKernelGGL((panel_kernel<BN, WN, 4, EPI>), dim3(grid), dim3(512), 0, st, a);
+  else if (s == 3)
+    hipLaunchKernelGGL((panel_kernel<BN, WN, 3, EPI>), dim3(grid), dim3(512), 0, st, a);
+  else if constexpr (BN == 64)  // a 64-column panel of a 3x3 conv over 64 channels (72 KB)
+    hipLaunchKernelGGL((panel_kernel<BN, WN, 2, EPI>), dim3(grid), dim3(512), 0, st, a);
+}
+
+template <int EPI>
+int launch_plan(const PanelPlan& p, PanelArgs& a, hipStream_t st, const char* what) {
+  a.npanel = p.npanel;
+  a.nunits = cdiv(a.M, 32);
+  const int grid = p.npanel * p.nb;
+  if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
+    fprintf(stderr, "[gemm] panel-%s %d/%d s%d M=%d N=%d K=%d epi=%d stats=%d blocks=%d\n", what, p.bn, p.wn, p.s, a.M,
+            a.N, a.K, a.epi, a.stats != nullptr, grid);
+  if constexpr (EPI == 0) {
+    if (p.bn == 256) launch_panel<256, 128, 0>(a, p.s, grid, st);
+    else if (p.bn == 128) launch_panel<128, 128, 0>(a, p.s, grid, st);
+    else launch_panel<64, 64, 0>(a, p.s, grid, st);
+  } else {
+    if (p.bn == 256) launch_panel<256, 64, 1>(a, p.s, grid, st);
+    else if (p.bn == 128) launch_panel<128, 64, 1>(a, p.s, grid, st);
+    else launch_panel<64, 64, 1>(a, p.s, grid, st);
+  }
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -349,40 +492,67 @@ MI_API int mi_set_panel(int mode) {
   return 0;
 }
 
-// statistics rows the panel kernel writes for an M x N x K conv (0: not routed there)
-MI_API int mi_panel_stat_rows(int M, int N, int K) {
-  const PanelPlan p = panel_plan(M, N, K);
+// statistics rows the panel kernel writes for an M x N x K conv forward (dgrad = 0) or data gradient
+// (dgrad = 1); 0: not routed there
+MI_API int mi_panel_stat_rows2(int M, int N, int K, int dgrad) {
+  const PanelPlan p = panel_plan(M, N, K, dgrad != 0);
   return p.bn ? p.nb : 0;
 }
+MI_API int mi_panel_stat_rows(int M, int N, int K) { return mi_panel_stat_rows2(M, N, K, 0); }
 
-// 1x1 conv forward (pad 0, stride s) on the panel kernel: x NHWC [Nb,H,W,C], w [K][C], y NHWC
-// [Nb,P,Q,K] bf16; stats: [mi_panel_stat_rows][2][K].  hipErrorNotSupported: shape not eligible.
-MI_API int mi_panel_conv1x1(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C,
-                                int K, int stride, int P, int Q, hipStream_t st) {
+// conv forward on the panel kernel: 1x1 (pad 0, stride s) or 3x3 (stride 1, pad 1); x NHWC [Nb,H,W,C],
+// w [K][R][R][C], y NHWC [Nb,P,Q,K] bf16; stats: [mi_panel_stat_rows][2][K].  hipErrorNotSupported:
+// shape not eligible.
+MI_API int mi_panel_conv(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C, int K, int R,
+                         int stride, int pad, int P, int Q, hipStream_t st) {
   const int M = Nb * P * Q;
-  const PanelPlan p = panel_plan(M, K, C);
+  const bool tap3 = R == 3;
+  if (!((R == 1 && pad == 0) || (tap3 && stride == 1 && pad == 1 && P == H && Q == W)) || C % 64 != 0)
+    return (int)hipErrorNotSupported;
+  const PanelPlan p = panel_plan(M, K, R * R * C, false);
   if (!p.bn) return (int)hipErrorNotSupported;
-  const int64_t ab = (int64_t)Nb * H * W * C * 2, cb = (int64_t)M * K * 2, bb = (int64_t)K * C * 2;
+  const int64_t ab = (int64_t)Nb * H * W * C * 2, cb = (int64_t)M * K * 2, bb = (int64_t)K * R * R * C * 2;
   if (ab > 0x7FFFFFF0LL || cb > 0x7FFFFFF0LL || bb > 0x7FFFFFF0LL) return (int)hipErrorNotSupported;
   PanelArgs a{};
   a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = (bf16_t*)y; a.stats = stats;
-  a.M = M; a.N = K; a.K = C; a.ldc = K;
-  a.nk = C / 64; a.npanel = p.npanel; a.nunits = cdiv(M, 32);
+  a.M = M; a.N = K; a.K = R * R * C; a.ldc = K;
+  a.nk = a.K / 64;
   a.a_bytes = (int)ab; a.b_bytes = (int)bb; a.c_bytes = (int)cb;
-  a.gather = (stride != 1 || P != H || Q != W) ? 1 : 0;
+  a.gather = tap3 ? 2 : ((stride != 1 || P != H || Q != W) ? 1 : 0);
   a.lda = C; a.H = H; a.W = W; a.stride = stride;
+  a.tsg = 1; a.cpt = C / 64;
   a.fPQ = make_fastdiv((uint32_t)(P * Q));
   a.fQ = make_fastdiv((uint32_t)Q);
-  const int grid = p.npanel * p.nb;
-  if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
-    fprintf(stderr, "[gemm] panel%d/%d s%d M=%d N=%d K=%d stride=%d stats=%d blocks=%d\n", p.bn, p.wn, p.s, M, K, C,
-            stride, stats != nullptr, grid);
-  if (p.bn == 256) {
-    if (p.s == 4) launch_panel<256, 128, 4>(a, grid, st); else launch_panel<256, 128, 3>(a, grid, st);
-  } else if (p.bn == 128) {
-    if (p.s == 4) launch_panel<128, 128, 4>(a, grid, st); else launch_panel<128, 128, 3>(a, grid, st);
-  } else {
-    if (p.s == 4) launch_panel<64, 64, 4>(a, grid, st); else launch_panel<64, 64, 3>(a, grid, st);
-  }
-  return (int)hipGetLastError();
+  return launch_plan<0>(p, a, st, tap3 ? "fwd3x3" : "fwd");
+}
+MI_API int mi_panel_conv1x1(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C, int K,
+                            int stride, int P, int Q, hipStream_t st) {
+  return mi_panel_conv(x, w, y, stats, Nb, H, W, C, K, 1, stride, 0, P, Q, st);
+}
+
+// 1x1 or 3x3 (pad 1) / stride-1 conv data gradient on the panel kernel: dy NHWC [Nb,H,W,K], wt [C][R][R][K], dx NHWC
+// [Nb,H,W,C] with nt_kernel's epilogues (PanelArgs::epi; mbits or aux = the BN output for the ReLU
+// mask; stats [mi_panel_stat_rows2(.., 1)][2][C]).  hipErrorNotSupported: not eligible.
+MI_API int mi_panel_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                          int epi, const void* aux, const void* aux2, const float* mean, int bn_relu, float* stats,
+                          int aux_even, const void* mbits, hipStream_t st) {
+  const int M = Nb * H * W;
+  if ((R != 1 && R != 3) || K % 64 != 0) return (int)hipErrorNotSupported;
+  const PanelPlan p = panel_plan(M, C, R * R * K, true);
+  if (!p.bn || !(epi == 0 || epi == 3 || epi == 4 || epi == 5)) return (int)hipErrorNotSupported;
+  const int64_t ab = (int64_t)M * K * 2, cb = (int64_t)M * C * 2, bb = (int64_t)C * R * R * K * 2;
+  if (ab > 0x7FFFFFF0LL || cb > 0x7FFFFFF0LL || bb > 0x7FFFFFF0LL) return (int)hipErrorNotSupported;
+  PanelArgs a{};
+  a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = (bf16_t*)dx;
+  a.stats = epi >= 4 ? stats : nullptr;
+  a.M = M; a.N = C; a.K = R * R * K; a.ldc = C;
+  a.nk = a.K / 64;
+  a.a_bytes = (int)ab; a.b_bytes = (int)bb; a.c_bytes = (int)cb;
+  a.gather = R == 3 ? 2 : 0; a.lda = K; a.H = H; a.W = W; a.stride = 1;
+  a.tsg = -1; a.cpt = K / 64;
+  a.fPQ = make_fastdiv((uint32_t)(H * W));
+  a.fQ = make_fastdiv((uint32_t)W);
+  a.epi = epi; a.bn_relu = epi >= 4 ? bn_relu : 0; a.aux_even = (epi == 3 || epi == 5) ? aux_even : 0;
+  a.aux = (const bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.mbits = (const uint8_t*)mbits;
+  return launch_plan<1>(p, a, st, R == 3 ? "dgrad3x3" : "dgrad");
 }

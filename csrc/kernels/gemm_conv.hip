@@ -1893,10 +1893,24 @@ MI_API void mi_set_conv256_min_k(int k) {
 
 // conv_panel.hip: persistent resident-weight kernel for the short-K 1x1 convolutions (forward)
 extern "C" int mi_panel_stat_rows(int M, int N, int K);
+extern "C" int mi_panel_stat_rows2(int M, int N, int K, int dgrad);
+extern "C" int mi_panel_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
+                              int epi, const void* aux, const void* aux2, const float* mean, int bn_relu, float* stats,
+                              int aux_even, const void* mbits, hipStream_t st);
+extern "C" int mi_panel_conv(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C, int K,
+                             int R, int stride, int pad, int P, int Q, hipStream_t st);
+// a 1x1 or 3x3 (pad 1) stride-1 data gradient runs on the panel kernel (the statistics slab rows it
+// writes), else 0
+static int panel_rows_dgrad(int M, int C, int K, int RS, int stride) {
+  if ((RS != 1 && RS != 9) || stride != 1 || K % 64 != 0) return 0;
+  return mi_panel_stat_rows2(M, C, RS * K, 1);
+}
 extern "C" int mi_panel_conv1x1(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C,
                                 int K, int stride, int P, int Q, hipStream_t st);
 static int panel_rows_fwd(int M, int N, int C, int R, int S, int pad, int H, int W, int P, int Q, int stride) {
-  if (R != 1 || S != 1 || pad != 0 || C % 64 != 0 || P != (H - 1) / stride + 1 || Q != (W - 1) / stride + 1) return 0;
+  if (C % 64 != 0) return 0;
+  if (R == 3 && S == 3 && stride == 1 && pad == 1 && P == H && Q == W) return mi_panel_stat_rows(M, N, 9 * C);
+  if (R != 1 || S != 1 || pad != 0 || P != (H - 1) / stride + 1 || Q != (W - 1) / stride + 1) return 0;
   return mi_panel_stat_rows(M, N, C);
 }
 
@@ -1956,7 +1970,7 @@ MI_API int mi_conv2d_fwd(const void* x, const void* w, void* y, const float* bia
     return mi_gemm256_conv(1, x, w, y, stats, 0, nullptr, nullptr, nullptr, 0, Nb, H, W, C, P, Q, R, S, stride, pad,
                            K, st);
   if (!out_f32 && !bias && panel_rows_fwd(Nb * P * Q, K, C, R, S, pad, H, W, P, Q, stride) > 0)
-    return mi_panel_conv1x1(x, w, y, stats, Nb, H, W, C, K, stride, P, Q, st);
+    return mi_panel_conv(x, w, y, stats, Nb, H, W, C, K, R, stride, pad, P, Q, st);
   NTArgs a{};
   a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = y; a.bias = bias; a.stats = stats;
   a.M = Nb * P * Q; a.N = K; a.K = R * S * C;
@@ -1975,6 +1989,8 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
     return mi_gemm256_conv(2, dy, wt, dx, nullptr, 0, nullptr, nullptr, nullptr, 0, Nb, P, Q, K, H, W, R, S, 1, pad, C,
                            st);
+  if (R == S && pad == (R == 3 ? 1 : 0) && panel_rows_dgrad(Nb * H * W, C, K, R * S, stride) > 0)
+    return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
@@ -2003,6 +2019,7 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
 MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride, int K, int RS) {
   const int M = Nb * H * W;
   if (stride == 1 && use_gemm256_conv(M, C, K, RS * K)) return 2 * cdiv(M, 256);
+  if (const int pr = panel_rows_dgrad(M, C, K, RS, stride); pr > 0) return pr;
   const int bm = nt_choice(M, C) == 2 ? 64 : 128;
   if (stride == 1 && RS == 9) {
     const int rp = halo_rp(M, C, 3, 3, 1, 1, K, P, Q, H, W);
@@ -2084,6 +2101,10 @@ MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb,
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
     return mi_gemm256_conv3(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
                             bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, mbits, st);
+  if (R == S && pad == (R == 3 ? 1 : 0) && panel_rows_dgrad(Nb * H * W, C, K, R * S, stride) > 0) {
+    if (mask_c) return (int)hipErrorNotSupported;  // mi_conv_nol_ok keeps these shapes materialised
+    return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, epi, aux, aux2, mean, bn_relu, stats, aux_even, mbits, st);
+  }
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
@@ -2140,6 +2161,7 @@ MI_API int mi_conv_nol_ok(int Nb, int H, int W, int C, int K, int R, int S, int 
   if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return 0;
   if (use_gemm256_conv(Nb * P * Q, K, C, R * S * C)) return 0;                    // forward
   if (panel_rows_fwd(Nb * P * Q, K, C, R, S, pad, H, W, P, Q, stride) > 0) return 0;  // forward (panel)
+  if (panel_rows_dgrad(Nb * H * W, C, K, R * S, stride) > 0) return 0;               // data gradient (panel)
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K)) return 0;    // data gradient
   // small grids keep the materialised path: there the 128-tile kernels split K (nt_split_blocks),
   // which the normalize-on-load variants do not -- and the bytes saved are negligible

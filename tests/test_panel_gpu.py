@@ -25,6 +25,8 @@ SHAPES = [
     (3, 256, 14, 1024, 1),  # layer-3 expansion, M = 588 (ragged units), 8 panels
     (2, 512, 28, 128, 1),   # K 512: BN 64 panels
     (1, 64, 7, 64, 1),      # tiny: fewer units than wave slots
+    (4, 64, 56, 64, 1, 3),  # layer-1 3x3 (72 KB panel, 2 slots, nine gathered taps)
+    (3, 64, 13, 64, 1, 3),  # 3x3, odd spatial size, ragged M
 ]
 
 
@@ -47,30 +49,33 @@ def _fwd(lib, x, w, stride, stats):
     from mi355x_dp.ops import _lib
     from mi355x_dp.ops._lib import ptr, stream_of
     N, C, H, _ = x.shape
-    K = w.shape[0]
-    P = (H - 1) // stride + 1
+    K, R = w.shape[0], w.shape[2]
+    pad = R // 2
+    P = (H + 2 * pad - R) // stride + 1
     y = torch.empty(N, K, P, P, dtype=BF, device="cuda", memory_format=CL)
-    _lib.call("mi_conv2d_fwd", ptr(x), ptr(w), ptr(y), ptr(None), ptr(stats), N, H, H, C, K, 1, 1, stride, 0, P, P, 0,
-              stream_of(x))
+    _lib.call("mi_conv2d_fwd", ptr(x), ptr(w), ptr(y), ptr(None), ptr(stats), N, H, H, C, K, R, R, stride, pad, P, P,
+              0, stream_of(x))
     return y
 
 
 @pytest.mark.parametrize("shape", SHAPES)
 def test_panel_conv1x1_fwd(lib, shape):
     torch.manual_seed(1)
-    N, C, H, K, s = shape
-    P = (H - 1) // s + 1
+    N, C, H, K, s = shape[:5]
+    R = shape[5] if len(shape) > 5 else 1
+    pad = R // 2
+    P = (H + 2 * pad - R) // s + 1
     M = N * P * P
     x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
-    w = (torch.randn(K, C, 1, 1, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
     lib.mi_set_panel(2)  # any row count
-    rows = lib.mi_panel_stat_rows(M, K, C)
+    rows = lib.mi_panel_stat_rows(M, K, C * R * R)
     assert rows > 0, "shape not routed to the panel kernel"
-    assert lib.mi_conv_stat_rows_g(N, H, H, C, K, 1, 1, s, 0, P, P) == rows
+    assert lib.mi_conv_stat_rows_g(N, H, H, C, K, R, R, s, pad, P, P) == rows
     slab = torch.full((rows + 8, 2, K), float("nan"), device="cuda")
     y = _fwd(lib, x, w, s, slab)
     torch.cuda.synchronize()
-    ref = F.conv2d(x.float(), w.float(), None, s, 0)
+    ref = F.conv2d(x.float(), w.float(), None, s, pad)
     assert rel_err(y, ref) < 1e-2
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, K)
     assert torch.isfinite(slab[:rows]).all(), "statistics rows left unwritten"
@@ -79,7 +84,7 @@ def test_panel_conv1x1_fwd(lib, shape):
     # the replaced 128-tile kernel: same MFMA sequence per element -> identical bf16 output
     lib.mi_set_panel(0)
     lib.mi_set_nt_split_blocks(0)  # the unsplit k-order
-    rows0 = lib.mi_conv_stat_rows_g(N, H, H, C, K, 1, 1, s, 0, P, P)
+    rows0 = lib.mi_conv_stat_rows_g(N, H, H, C, K, R, R, s, pad, P, P)
     y0 = _fwd(lib, x, w, s, torch.empty(rows0, 2, K, device="cuda"))
     lib.mi_set_nt_split_blocks(128)
     lib.mi_set_panel(2)
@@ -89,3 +94,84 @@ def test_panel_conv1x1_fwd(lib, shape):
     y2 = _fwd(lib, x, w, s, None)
     torch.cuda.synchronize()
     assert torch.equal(y2, y)
+
+
+# data gradient (dx channels C, dy channels K): panel widths 256 / 64 (4 and 1 waves across), 64 KB
+# panels (3 slots), 2 panels, ragged M
+DGRAD_SHAPES = [
+    (4, 56, 256, 64), (4, 56, 64, 256), (2, 56, 256, 128), (4, 28, 512, 128), (4, 28, 128, 512), (3, 14, 1024, 256),
+    (4, 56, 64, 64, 3), (3, 13, 64, 64, 3),  # 3x3 / pad 1: the flipped taps of wt = [C][3][3][K]
+]
+# (epi, mask: "bits" | "y" | None, stats, flags): flags bit 1 = the accumulated-into gradient exists
+# only at even (h, w) (a stride-2 downsample's sparse data gradient)
+DGRAD_EPIS = [(0, None, False, 0), (3, None, False, 0), (4, "bits", True, 0), (5, "bits", True, 0),
+              (5, "bits", True, 2), (4, "y", True, 0), (3, None, False, 2)]
+
+
+def _dgrad(lib, dy, wt, dx, epi, aux, x, mean, mask, bits, stats, flags):
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    N, K, H, W = dy.shape
+    C, R = dx.shape[1], wt.shape[1]
+    _lib.call("mi_conv2d_dgrad_ex4", ptr(dy), ptr(wt), ptr(dx), N, H, W, C, K, R, R, 1, R // 2, H, W, epi,
+              ptr(aux), ptr(x), ptr(mean), 1 if mask else 0, ptr(stats), flags, ptr(None), ptr(None),
+              ptr(bits if mask == "bits" else None), stream_of(dy))
+
+
+@pytest.mark.parametrize("epi,mask,stats,flags", DGRAD_EPIS)
+@pytest.mark.parametrize("shape", DGRAD_SHAPES)
+def test_panel_dgrad1x1(lib, shape, epi, mask, stats, flags):
+    """the 1x1 data gradient with nt_kernel's fused epilogues (residual add, BN backward with the ReLU
+    mask from mask bytes or from the BN output, the (sum dz, sum dz (x - mean)) statistics, the
+    sparse even-pixel accumulate): bf16 output bit for bit equal to the 128-tile kernel's, statistics
+    equal up to fp32 summation order"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    torch.manual_seed(2)
+    N, H, C, K = shape[:4]
+    R = shape[4] if len(shape) > 4 else 1
+    if R == 3 and flags:
+        pytest.skip("the sparse even-pixel accumulate only follows 1x1 downsample data gradients")
+    M = N * H * H
+    dy = torch.randn(N, K, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
+    wt = torch.empty(C, R, R, K, dtype=BF, device="cuda")
+    _lib.call("mi_conv_wtrans", ptr(w), ptr(wt), K, R * R, C, stream_of(dy))
+    base = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    if flags & 2:  # only even (h, w) defined: odd pixels hold garbage the kernel must not read
+        base[:, :, 1::2, :] = float("nan")
+        base[:, :, :, 1::2] = float("nan")
+    aux = base if epi == 3 else None
+    x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    y = torch.relu(torch.randn(N, C, H, H, device="cuda")).to(BF).contiguous(memory_format=CL)
+    yb = (y.permute(0, 2, 3, 1).reshape(M, C // 8, 8) > 0).to(torch.int32)
+    bits = (yb << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
+    mean = torch.randn(C, device="cuda") * 0.1
+    out = {}
+    for mode in (2, 0):
+        lib.mi_set_panel(mode)
+        lib.mi_set_nt_split_blocks(0)
+        rows = lib.mi_dgrad_stat_rows(N, H, H, C, H, H, 1, K, R * R)
+        if mode == 2:
+            assert rows == lib.mi_panel_stat_rows2(M, C, R * R * K, 1) > 0, "not routed to the panel kernel"
+        sl = torch.full((rows + 8, 2, C), float("nan"), device="cuda") if stats else None
+        dx = base.clone() if epi == 5 else torch.empty_like(base)
+        _dgrad(lib, dy, wt, dx, epi, aux, x, mean, mask, bits, sl, flags)
+        torch.cuda.synchronize()
+        out[mode] = (dx, sl[:rows] if stats else None)
+    lib.mi_set_nt_split_blocks(128)
+    lib.mi_set_panel(2)
+    dx_p, sl_p = out[2]
+    dx_o, sl_o = out[0]
+    if epi == 3 and flags & 2:
+        # epi 3 reads its residual at every pixel; the NaN-poisoned odd ones propagate alike
+        assert torch.equal(dx_p.isnan(), dx_o.isnan())
+        dx_p, dx_o = torch.nan_to_num(dx_p), torch.nan_to_num(dx_o)
+    assert torch.equal(dx_p, dx_o)
+    if epi == 0:
+        ref = torch.nn.grad.conv2d_input(dx_p.shape, w.float(), dy.float(), 1, R // 2)
+        assert rel_err(dx_p, ref) < 1e-2
+    if stats:
+        assert torch.isfinite(sl_p).all(), "statistics rows left unwritten"
+        for k in (0, 1):
+            assert rel_err(sl_p[:, k].sum(0), sl_o[:, k].sum(0)) < 1e-4

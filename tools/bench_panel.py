@@ -16,10 +16,16 @@ import torch  # noqa: E402
 
 BF, CL = torch.bfloat16, torch.channels_last
 
-# (C, H, K, stride, count per ResNet-50 step) at batch 256
+# forward: (C, H, K, stride, R, count per ResNet-50 step) at batch 256
 SHAPES = [
-    (64, 56, 64, 1, 1), (64, 56, 256, 1, 4), (256, 56, 64, 1, 2), (256, 56, 128, 1, 1),
-    (128, 28, 512, 1, 4), (512, 28, 128, 1, 3), (256, 56, 512, 2, 1), (256, 14, 1024, 1, 6),
+    (64, 56, 64, 1, 1, 1), (64, 56, 256, 1, 1, 4), (256, 56, 64, 1, 1, 2), (256, 56, 128, 1, 1, 1),
+    (128, 28, 512, 1, 1, 4), (512, 28, 128, 1, 1, 3), (256, 56, 512, 2, 1, 1), (256, 14, 1024, 1, 1, 6),
+    (64, 56, 64, 1, 3, 3),
+]
+# data gradient with the step's epilogues: (C = dx channels, H, K = dy channels, R, epi, count)
+DGRAD = [
+    (256, 56, 64, 1, 5, 2), (64, 56, 256, 1, 4, 3), (256, 56, 128, 1, 5, 1), (512, 28, 128, 1, 5, 3),
+    (128, 28, 512, 1, 4, 4), (1024, 14, 256, 1, 5, 5), (256, 14, 1024, 1, 4, 6), (64, 56, 64, 3, 4, 3),
 ]
 
 
@@ -34,22 +40,10 @@ def main():
     from mi355x_dp.ops._lib import ptr, stream_of
     lib = _lib.load(True)
     Nb = a.batch
-    print("| C H K s | panel us | nt us | speedup | panel TB/s | nt TB/s | x count |")
+    print("| conv | panel us | old us | speedup | panel TB/s | old TB/s | x count |")
     print("|---|---:|---:|---:|---:|---:|---:|")
     tot_p = tot_o = 0.0
-    for (C, H, K, s, cnt) in SHAPES:
-        P = (H - 1) // s + 1
-        M = Nb * P * P
-        x = torch.randn(Nb, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
-        w = (torch.randn(K, C, 1, 1, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
-        y = torch.empty(Nb, K, P, P, dtype=BF, device="cuda", memory_format=CL)
-        slab = torch.empty(8192, 2, K, device="cuda")
-        st = stream_of(x)
-
-        def run():
-            _lib.call("mi_conv2d_fwd", ptr(x), ptr(w), ptr(y), ptr(None), ptr(slab), Nb, H, H, C, K, 1, 1, s, 0, P, P,
-                      0, st)
-
+    def ab(run):
         def timed():
             run()
             torch.cuda.synchronize()
@@ -60,7 +54,6 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / a.iters * 1e3
-
         tp, to = [], []
         for _ in range(a.rounds):
             lib.mi_set_panel(1)
@@ -68,13 +61,55 @@ def main():
             lib.mi_set_panel(0)
             to.append(timed())
         lib.mi_set_panel(1)
-        mp, mo = statistics.median(tp), statistics.median(to)
-        routed = lib.mi_panel_stat_rows(M, K, C) > 0
+        return statistics.median(tp), statistics.median(to)
+
+    for (C, H, K, s, R, cnt) in SHAPES:
+        pad = R // 2
+        P = (H + 2 * pad - R) // s + 1
+        M = Nb * P * P
+        x = torch.randn(Nb, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+        w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
+        y = torch.empty(Nb, K, P, P, dtype=BF, device="cuda", memory_format=CL)
+        slab = torch.empty(8192, 2, K, device="cuda")
+        st = stream_of(x)
+
+        def run():
+            _lib.call("mi_conv2d_fwd", ptr(x), ptr(w), ptr(y), ptr(None), ptr(slab), Nb, H, H, C, K, R, R, s, pad, P,
+                      P, 0, st)
+
+        mp, mo = ab(run)
+        routed = lib.mi_panel_stat_rows(M, K, C * R * R) > 0
         byts = (Nb * H * H * C if s == 1 else M * C) * 2 + M * K * 2
         tot_p += mp * cnt
         tot_o += mo * cnt
-        print(f"| {C} {H} {K} {s} | {mp:.1f}{'' if routed else ' (not routed)'} | {mo:.1f} | {mo / mp:.2f}x | "
-              f"{byts / mp / 1e6:.2f} | {byts / mo / 1e6:.2f} | {cnt} |")
+        print(f"| fwd {C} {H} {K} s{s} {R}x{R} | {mp:.1f}{'' if routed else ' (not routed)'} | {mo:.1f} | "
+              f"{mo / mp:.2f}x | {byts / mp / 1e6:.2f} | {byts / mo / 1e6:.2f} | {cnt} |")
+        del x, w, y
+    for (C, H, K, R, epi, cnt) in DGRAD:
+        M = Nb * H * H
+        dy = torch.randn(Nb, K, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+        w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
+        wt = torch.empty(C, R, R, K, dtype=BF, device="cuda")
+        st = stream_of(dy)
+        _lib.call("mi_conv_wtrans", ptr(w), ptr(wt), K, R * R, C, st)
+        dx = torch.randn(Nb, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+        xin = torch.randn_like(dx)
+        bits = torch.randint(0, 255, (M, C // 8), dtype=torch.uint8, device="cuda")
+        mean = torch.zeros(C, device="cuda")
+        slab = torch.empty(8192, 2, C, device="cuda")
+
+        def run():
+            _lib.call("mi_conv2d_dgrad_ex4", ptr(dy), ptr(wt), ptr(dx), Nb, H, H, C, K, R, R, 1, R // 2, H, H, epi,
+                      ptr(None), ptr(xin), ptr(mean), 1, ptr(slab), 0, ptr(None), ptr(None), ptr(bits), st)
+
+        mp, mo = ab(run)
+        routed = lib.mi_panel_stat_rows2(M, C, K * R * R, 1) > 0
+        byts = M * K * 2 + M * C * 2 * (3 if epi == 5 else 2) + M * C // 8
+        tot_p += mp * cnt
+        tot_o += mo * cnt
+        print(f"| dgrad{epi} {C} {H} {K} {R}x{R} | {mp:.1f}{'' if routed else ' (not routed)'} | {mo:.1f} | "
+              f"{mo / mp:.2f}x | {byts / mp / 1e6:.2f} | {byts / mo / 1e6:.2f} | {cnt} |")
+        del dy, w, wt, dx, xin
     print(f"\nper ResNet-50 step (x count): panel {tot_p / 1e3:.3f} ms vs nt {tot_o / 1e3:.3f} ms")
 
 
