@@ -57,6 +57,10 @@ def parse(argv=None):
     p.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                    help="cpu: rehearse the distributed path on CPU ranks (tests; not a GPU number)")
     p.add_argument("--bucket-mb", type=float, default=None)
+    p.add_argument("--comm-emulate", type=int, default=int(os.environ.get("MI355X_DP_COMM_EMULATE", "0") or 0),
+                   help="world 1: run every gradient all-reduce as one rank of an N-rank ring on the smddp "
+                        "backend's comm stream (memory traffic, CU footprint, xGMI-paced duration; "
+                        "mi_ring_emulate) -- implies --backend smddp --force-comm")
     p.add_argument("--force-comm", action="store_true",
                    help="create the process group and issue every bucket collective even at N=1 "
                         "(comm-stream / overlap traces on one GPU); the headline N=1 run leaves it off")
@@ -77,6 +81,9 @@ def parse(argv=None):
     p.add_argument("--launcher", default=os.environ.get("MI355X_DP_BENCH_LAUNCHER", "native"),
                    choices=("native", "torchrun"), help="how --gpus N > 1 spawns its ranks without WORLD_SIZE")
     a = p.parse_args(argv)
+    if a.comm_emulate > 1:
+        a.backend, a.force_comm = "smddp", True
+        os.environ["MI355X_DP_COMM_EMULATE"] = str(a.comm_emulate)
     if a.backend is None:
         a.backend = "nccl" if a.device == "cuda" else "gloo"
     return a
@@ -380,6 +387,16 @@ def main(argv=None):
         torch.cuda.empty_cache()
         secondary = {m: run_child_bench(1, args, args.backend, model=m, timeout_s=180)
                      for m in ("resnet152", "vit_b_16")}
+    emulated = None
+    if (rank == 0 and world == 1 and cuda and not args.force_comm
+            and os.environ.get("MI355X_DP_BENCH_EMULATE", "1") == "1"):
+        # after the timed region, as its own process: the same step with every bucket all-reduce run
+        # as one rank of an 8-rank ring on the smddp comm stream (mi_ring_emulate: the rank's memory
+        # traffic on 32 resident workgroups, paced to xGMI time) -- at world 1 RCCL launches nothing,
+        # so this is the single-GPU estimate of what an 8-GPU gradient exchange costs the backward
+        # (VERDICT r5 item 3); the headline above stays the plain world-1 step
+        torch.cuda.empty_cache()
+        emulated = run_child_bench(1, args, "smddp", timeout_s=180, extra=["--comm-emulate", "8"])
     ipc_probe = None
     if (rank == 0 and world > 1 and cuda and world <= torch.cuda.device_count()
             and os.environ.get("MI355X_DP_BENCH_IPC_PROBE", "1") == "1"):
@@ -432,6 +449,8 @@ def main(argv=None):
             "ipc_probe": ipc_probe,
             "smddp_job": smddp_job,
             "secondary_models": secondary,
+            "emulated_comm_dp8": emulated,
+            "comm_emulated_world": args.comm_emulate if args.comm_emulate > 1 else None,
             # GPU event times (ms from the forward's start) of one step after the timed region
             "comm_timeline": comm_timeline,
             "bucket_launch_ms": comm_timeline["buckets"] if comm_timeline else None,
@@ -475,7 +494,7 @@ def _child_env():
     return env
 
 
-def run_child_bench(world: int, args, backend: str, timeout_s: int = 150, model: str = None):
+def run_child_bench(world: int, args, backend: str, timeout_s: int = 150, model: str = None, extra=()):
     """``bench.py`` again as a fresh N-rank job (native launcher) through ``backend``, a few steps of
     the same configuration (or of ``model``), started by rank 0 after the benchmark finished (a
     failure cannot cost the measurement).  Returns its img/s, ranks seen, backend, replica check and
@@ -499,6 +518,7 @@ def run_child_bench(world: int, args, backend: str, timeout_s: int = 150, model:
            "--device", args.device, "--grad-comm", args.grad_comm, "--wgrad-stream", wgs]
     if args.shard_optimizer:
         cmd.append("--shard-optimizer")
+    cmd += list(extra)
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
         out, err = proc.communicate(timeout=timeout_s)
@@ -517,7 +537,9 @@ def run_child_bench(world: int, args, backend: str, timeout_s: int = 150, model:
                     "comm_library": d["config"]["comm_library"], "img_s": d["value"],
                     "ms_per_step": d["ms_per_step"], "steps": d["steps"], "warmup": d["warmup"],
                     "per_gpu_batch": d["config"]["per_gpu_batch"], "ranks_seen": d["ranks_seen"],
-                    "replicas_identical": d["replicas_identical"], "buckets": d["config"]["buckets"]}
+                    "replicas_identical": d["replicas_identical"], "buckets": d["config"]["buckets"],
+                    "comm_emulated_world": d.get("comm_emulated_world"),
+                    "comm_exposed_ms": d.get("comm_exposed_ms"), "comm_timeline": d.get("comm_timeline")}
     return f"failed: rc={proc.returncode}: {(err or out)[-400:]}"
 
 

@@ -207,6 +207,7 @@ class SmddpBackend : public c10d::Backend {
       TORCH_CHECK(!ipc_only_ || size == 1 || ipc_on_, "smddp: MI355X_DP_SMDDP_IPC_ONLY=1 but the IPC path is unavailable");
     }
     if (!ipc_on_ && !(ipc_only_ && size == 1)) comm();  // eager RCCL bootstrap unless IPC may serve the collectives
+    if (size == 1) setup_emulation();
     watchdog_ = std::thread([this] { watchdog_loop(); });
     std::lock_guard<std::mutex> lk(g_live_mu);
     g_live.push_back(this);
@@ -268,6 +269,46 @@ class SmddpBackend : public c10d::Backend {
   using IpcAgFn = int (*)(const void* const*, uint32_t* const*, int, int, const void*, void*, int64_t, int64_t,
                           uint32_t, int*, uint32_t, hipStream_t);
 
+  // MI355X_DP_COMM_EMULATE=N (N >= 2) at world 1: every all-reduce runs mi_ring_emulate on the comm
+  // stream -- one rank's memory traffic, CU footprint (MI355X_DP_COMM_EMULATE_WGS, default 32) and
+  // xGMI-paced duration of an N-rank ring (MI355X_DP_COMM_EMULATE_GBPS per link, default 153, over
+  // N - 1 links; MI355X_DP_COMM_EMULATE_ALPHA_US per step, default 1) -- instead of RCCL's no-op
+  void setup_emulation() {
+    const char* e = std::getenv("MI355X_DP_COMM_EMULATE");
+    const int n = e ? atoi(e) : 0;
+    if (n < 2) return;
+    const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
+    void* h = lib ? dlopen(lib, RTLD_NOW | RTLD_GLOBAL) : nullptr;
+    emu_fn_ = h ? (EmuFn)dlsym(h, "mi_ring_emulate") : nullptr;
+    TORCH_CHECK(emu_fn_, "smddp: MI355X_DP_COMM_EMULATE set but mi_ring_emulate is unavailable (kernel library ",
+                lib ? lib : "unset", ")");
+    emu_world_ = std::min(n, 64);
+    if (const char* c = std::getenv("MI355X_DP_COMM_EMULATE_WGS")) emu_wgs_ = std::max(1, atoi(c));
+    if (const char* c = std::getenv("MI355X_DP_COMM_EMULATE_GBPS")) emu_gbps_ = atof(c);
+    if (const char* c = std::getenv("MI355X_DP_COMM_EMULATE_ALPHA_US")) emu_alpha_us_ = atof(c);
+  }
+
+  void emulate(const at::Tensor& t, hipStream_t s) {
+    const int64_t bytes = t.numel() * t.element_size();
+    TORCH_CHECK(t.is_contiguous() && bytes % 4 == 0, "smddp emulation: contiguous tensors of whole words");
+    if ((size_t)bytes > emu_cap_) {
+      TORCH_CHECK(!capturing_, "smddp emulation: scratch cannot grow inside a graph capture");
+      HIPCHECK(hipStreamSynchronize(s));
+      if (emu_tmp_) HIPCHECK(hipFree(emu_tmp_));
+      if (emu_zero_) HIPCHECK(hipFree(emu_zero_));
+      emu_cap_ = std::max<size_t>((size_t)bytes, 16u << 20);
+      HIPCHECK(hipMalloc(&emu_tmp_, emu_cap_));
+      HIPCHECK(hipMalloc(&emu_zero_, emu_cap_));
+      HIPCHECK(hipMemset(emu_zero_, 0, emu_cap_));
+    }
+    HIPCHECK((hipError_t)emu_fn_(t.data_ptr(), bytes, emu_tmp_, emu_zero_, emu_world_, emu_wgs_, emu_gbps_,
+                                 emu_world_ - 1, emu_alpha_us_, s));
+  }
+
+ public:
+  int emulated_world() const { return emu_world_; }
+
+ private:
   void setup_ipc() {
     const char* lib = std::getenv("MI355X_DP_KERNELS_LIB");
     void* h = lib ? dlopen(lib, RTLD_NOW | RTLD_GLOBAL) : nullptr;
@@ -544,6 +585,10 @@ class SmddpBackend : public c10d::Backend {
   // ------------------------------------------------------------ collectives
   c10::intrusive_ptr<c10d::Work> allreduce(std::vector<at::Tensor>& tensors,
                                            const c10d::AllreduceOptions& opts) override {
+    if (emu_world_ > 1)
+      return run(c10d::OpType::ALLREDUCE, tensors, tensors, [&](hipStream_t s) {
+        for (auto& t : tensors) emulate(t, s);
+      });
     if (solo()) return run(c10d::OpType::ALLREDUCE, tensors, tensors, [](hipStream_t) {});
     if (ipc_eligible(tensors, opts)) {
       const bool avg = opts.reduceOp == c10d::ReduceOp::AVG;
@@ -748,7 +793,8 @@ class SmddpBackend : public c10d::Backend {
     return {{"on", ipc_on_ ? 1 : 0}, {"only", ipc_only_ ? 1 : 0}, {"cap_bytes", (int64_t)ipc_cap_},
             {"oneshot_bytes", (int64_t)ipc_oneshot_bytes_}, {"threshold_bytes", (int64_t)ipc_threshold_},
             {"flags_uncached", std::string(flags_kind_) == "uncached" ? 1 : 0},
-            {"flags_finegrained", std::string(flags_kind_) == "finegrained" ? 1 : 0}};
+            {"flags_finegrained", std::string(flags_kind_) == "finegrained" ? 1 : 0},
+            {"emulated_world", emu_world_}};
   }
   // every rank must set the same values (the path of a collective must agree across ranks)
   void set_ipc_paths(int64_t threshold_bytes, int64_t oneshot_bytes) {
@@ -824,6 +870,13 @@ class SmddpBackend : public c10d::Backend {
   std::atomic<bool> stop_{false};
   std::thread watchdog_;
   bool capturing_ = false;  // run() is issuing a collective into a HIP graph capture
+  using EmuFn = int (*)(void*, int64_t, void*, const void*, int, int, double, int, double, hipStream_t);
+  EmuFn emu_fn_ = nullptr;
+  int emu_world_ = 0, emu_wgs_ = 32;
+  double emu_gbps_ = 153.0, emu_alpha_us_ = 1.0;
+  void* emu_tmp_ = nullptr;
+  void* emu_zero_ = nullptr;
+  size_t emu_cap_ = 0;
 };
 
 static void stop_all_watchdogs() {

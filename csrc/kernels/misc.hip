@@ -497,3 +497,48 @@ MI_API int mi_host_word_alloc(int** host, int** dev) {
   **host = 0;
   return (int)hipHostGetDevicePointer((void**)dev, *host, 0);
 }
+
+// ------------------------------------------------------------ world-1 ring all-reduce emulation
+// at world 1 RCCL launches no kernel for an all-reduce, so a single-GPU bench
+// cannot show what an 8-rank gradient exchange costs the backward it overlaps.  With
+// MI355X_DP_COMM_EMULATE=N the smddp backend (csrc/comm/smddp_backend.cpp) runs this kernel on its
+// comm stream for every world-1 all-reduce instead: the local memory traffic of one rank of an N-rank
+// ring (reduce-scatter: N - 1 steps reading the bucket chunk and a received chunk and writing the
+// result; all-gather: N - 1 steps copying a chunk into the bucket; 5 (N - 1) / N x S bytes in all) on
+// `wgs` workgroups -- RCCL's channel footprint of resident CUs -- paced so no step ends before the
+// xGMI time of its S / N bytes plus a per-step latency (host-computed `step_ticks`, 100 MHz).  The
+// bucket's values are unchanged: the "received" chunk is a zero word XORed in, the all-gather copies
+// back what the reduce-scatter wrote.
+__global__ __launch_bounds__(256) void ring_emulate_kernel(uint32_t* __restrict__ buf, uint32_t* __restrict__ tmp,
+                                                           const uint32_t* __restrict__ zero, int64_t nw, int world,
+                                                           uint64_t step_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int64_t chunk = (nw + world - 1) / world;
+  const int64_t per = (chunk + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per;
+  const int steps = 2 * (world - 1);
+  for (int k = 0; k < steps; ++k) {
+    const int c = k % (world - 1);  // the all-gather revisits the chunks the reduce-scatter wrote
+    const int64_t b = (int64_t)c * chunk + lo;
+    const int64_t e = min(min(b + per, (int64_t)c * chunk + chunk), nw);
+    if (k < world - 1) {
+      for (int64_t i = b + threadIdx.x; i < e; i += 256) tmp[i] = buf[i] ^ zero[i];
+    } else {
+      for (int64_t i = b + threadIdx.x; i < e; i += 256) buf[i] = tmp[i];
+    }
+    // pace: the step may not end before the wire time of its chunk (every wave polls its own clock)
+    const uint64_t until = t0 + (uint64_t)(k + 1) * step_ticks;
+    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// bytes: the all-reduced tensor (a multiple of 4), tmp / zero: scratch of >= bytes (zero all zeros)
+MI_API int mi_ring_emulate(void* buf, int64_t bytes, void* tmp, const void* zero, int world, int wgs, double link_gbps,
+                           int links, double alpha_us, hipStream_t st) {
+  if (world < 2 || bytes <= 0 || (bytes & 3) || wgs < 1) return (int)hipErrorInvalidValue;
+  const double step_s = alpha_us * 1e-6 + (double)bytes / world / (std::max(1, links) * link_gbps * 1e9);
+  const uint64_t ticks = (uint64_t)(step_s * 1e8);  // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(ring_emulate_kernel, dim3(wgs), dim3(256), 0, st, (uint32_t*)buf, (uint32_t*)tmp,
+                     (const uint32_t*)zero, (int64_t)(bytes / 4), world, ticks);
+  return (int)hipGetLastError();
+}

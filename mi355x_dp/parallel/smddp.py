@@ -68,8 +68,10 @@ def create_backend(store, rank, world_size, timeout):
         if mod is None:
             raise RuntimeError("smddp: native backend extension (_smddp_native_ext) is not built; run "
                                "`python -m mi355x_dp.build` or set MI355X_DP_SMDDP_IMPL=nccl")
-        if os.environ.get("MI355X_DP_SMDDP_IPC") == "1" or os.environ.get("MI355X_DP_SMDDP_IPC_ONLY") == "1":
-            # the one-shot IPC all-reduce kernel lives in the HIP kernel library
+        if (os.environ.get("MI355X_DP_SMDDP_IPC") == "1" or os.environ.get("MI355X_DP_SMDDP_IPC_ONLY") == "1"
+                or int(os.environ.get("MI355X_DP_COMM_EMULATE", "0") or 0) > 1):
+            # the one-shot IPC all-reduce kernel and the world-1 ring emulation live in the HIP
+            # kernel library
             from mi355x_dp.ops import _lib
             _lib.load(True)
             os.environ.setdefault("MI355X_DP_KERNELS_LIB", _lib.KERNEL_LIB)
