@@ -61,20 +61,11 @@ __device__ __forceinline__ void store4bf(bf16_t* p, f32x4 v, float s) {
 // rows [0, TP) of two [T][ld] bf16 matrices (64 columns each) -> LDS [TP][KSTR], zero rows >= T.
 // All of a thread's global loads are issued before any LDS store (fully unrolled, fixed trip
 // count), so the staging costs one memory latency instead of one per 16-byte chunk.
-#ifndef MI_ATT_LIBEXP
-#define MI_ATT_LIBEXP 0  // 1: the device library's exp2f (A/B)
-#endif
 // softmax exponentials: every argument is <= 0 (scores minus the row max / the saved LSE), so
 // the hardware v_exp_f32 is exact enough and its flush of results below 2^-126 to zero is
 // harmless; the library exp2f wraps it in denormal range scaling (~10 VALU per call, 56 calls
 // per 16-query tile and wave in the forward)
-__device__ __forceinline__ float att_exp2(float x) {
-#if MI_ATT_LIBEXP
-  return exp2f(x);
-#else
-  return __builtin_amdgcn_exp2f(x);
-#endif
-}
+__device__ __forceinline__ float att_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // First 16-row tile of wave wv (it then takes every NW-th).  13 tiles (T = 197) cannot be dealt
 // evenly over a workgroup's 4 SIMDs (waves w and w + 4 share SIMD w % 4): one SIMD carries 4 tiles,

@@ -109,26 +109,17 @@ __device__ __forceinline__ uint32_t nz_bits8(const uint4& v) {
   return b;
 }
 
-// streaming 16-byte load (nontemporal: read once, do not keep in the caches; MI_NTLOAD=0 A/B
-// builds: plain loads)
-#ifndef MI_NTLOAD
-#define MI_NTLOAD 1
-#endif
+// streaming 16-byte load (nontemporal: read once, do not keep in the caches)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_nt16(const void* base, int64_t v) {
-  if (MI_NTLOAD) return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)base + v));
-  return ((const uint4*)base)[v];
+  return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)base + v));
 }
 
-// GEMM-epilogue operand loads (A/B builds): MI_EPI_NT_CY = 1 reads the accumulated-into C and the
-// aux operand (residual / GELU derivative / ReLU source) non-temporally, MI_EPI_NT_X = 1 the BN
-// input read for the BN-backward statistics
-#ifndef MI_EPI_NT_CY
-#define MI_EPI_NT_CY 1
-#endif
-#ifndef MI_EPI_NT_X
-#define MI_EPI_NT_X 0
-#endif
+// GEMM-epilogue operand loads: the accumulated-into C and the aux operand (residual / GELU
+// derivative / ReLU source) are read once -- non-temporally (kEpiNtCY: +3.3 % on ResNet-50, round
+// 5); the BN input read for the BN-backward statistics stays cached (kEpiNtX)
+constexpr bool kEpiNtCY = true;
+constexpr bool kEpiNtX = false;
 template <bool NTL>
 __device__ __forceinline__ uint4 epi_ld16(const void* p) {
   if (NTL) return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)p));

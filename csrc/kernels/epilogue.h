@@ -2,10 +2,6 @@
 #pragma once
 #include "common.h"
 
-#ifndef MI_GELU_OCML
-#define MI_GELU_OCML 0  // 1: the device library's erff (A/B builds)
-#endif
-
 // erf(z) without branches (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 -- far below the bf16
 // output's 2^-9 relative rounding): one reciprocal, one exp, five FMAs.  The device library's erff
 // is a multi-range routine that made the GELU epilogues of the ViT GEMMs VALU-bound (fc1 +0.22 ms,
@@ -22,35 +18,22 @@ __device__ __forceinline__ float erf_fast(float z, float& e_out) {
 
 // erf-form GELU (nn.GELU default) and its derivative
 __device__ __forceinline__ float gelu_f(float x) {
-#if MI_GELU_OCML
-  return 0.5f * x * (1.f + erff(x * 0.70710678f));
-#else
   float e;
   return 0.5f * x * (1.f + erf_fast(x * 0.70710678f, e));
-#endif
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-#if MI_GELU_OCML
-  return 0.5f * (1.f + erff(x * 0.70710678f)) + x * 0.39894228f * __expf(-0.5f * x * x);
-#else
   float e;  // exp(-x^2 / 2)
   const float r = erf_fast(x * 0.70710678f, e);
   return 0.5f * (1.f + r) + x * 0.39894228f * e;
-#endif
 }
 
 // GELU and its derivative at one point, from one erf / exp: the forward epilogue stores the
 // derivative for the backward instead of the pre-activation (see epilogue_op_v, epi 1 / 2)
 __device__ __forceinline__ float gelu_fg(float x, float& d) {
-#if MI_GELU_OCML
-  d = gelu_grad_f(x);
-  return gelu_f(x);
-#else
   float e;  // exp(-x^2 / 2)
   const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678f, e));
   d = cdf + x * 0.39894228f * e;
   return x * cdf;
-#endif
 }
 
 // elementwise op on one 16-byte chunk (8 bf16) of the bf16 epilogue; aux has C's layout.

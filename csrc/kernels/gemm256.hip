@@ -27,37 +27,15 @@
 //    ds_read_b128 fragment reads spread over the banks;
 //  * XCD-aware, M-grouped tile order (GROUP_M 8) for L2 reuse of the B panel.
 #include "common.h"
-#ifndef MI_MASK_PROBE
-#define MI_MASK_PROBE 0  // timing probe (tools/gpu_call_maskprobe.sh)
-#endif
+#include "epilogue.h"
+
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
-#ifndef MI_CONV_NTSTORE
-#define MI_CONV_NTSTORE 0
-#endif
-#ifndef MI_TN_NOATOMIC
-#define MI_TN_NOATOMIC 0  // timing experiment only (wrong results)
-#endif
-#include "epilogue.h"
-#include <algorithm>
 #include <mutex>
-#include <cstdlib>
 
-#ifndef MI_G256_CPOL_A
-#define MI_G256_CPOL_A 0  // cache-policy bits of the conv modes' gathered A operand loads (A/B builds)
-#endif
-#ifndef MI_G256_EPI_U0
-#define MI_G256_EPI_U0 8  // plain-GEMM epilogue: row steps per group of batched operand loads (A/B)
-#endif
-#ifndef MI_G256_EPI_PIPE
-#define MI_G256_EPI_PIPE 0  // conv epilogue operand loads software-pipelined one group ahead (A/B)
-#endif
-#ifndef MI_G256_EPI_UBN
-#define MI_G256_EPI_UBN 4  // conv epilogues (BN statistics / BN backward): row steps per load group
-#endif
-#ifndef MI_FENCE_HANDOFF
-#define MI_FENCE_HANDOFF 0  // 1: tail split-K hand-off through a __threadfence pair (A/B only)
-#endif
+// epilogue row steps per group of batched operand loads: plain GEMM / conv (BN) epilogues
+constexpr int kG256EpiU0 = 8, kG256EpiUBN = 4;
 
 namespace {
 
@@ -96,24 +74,12 @@ struct G256Args {
   const uint8_t* mbits; // epi 4 / 5: ReLU mask bytes (8 channels each) instead of aux (gemm_conv.hip NTArgs)
 };
 
-// Wave priority (A/B knob, MI_G256_PRIO): 0 none; 1 static s_setprio 1 for the second-dispatched
-// half (waves 4-7) before the main loop -- the guard must be provably wave-uniform
-// (readfirstlane), a plain `if (wid >= 4)` lowers to s_and_saveexec + an UNCONDITIONAL
-// s_setprio, i.e. every wave at priority 1; 2 per-MFMA-cluster setprio(1)/(0) flips (keeps hipcc
-// from moving the cluster's MFMAs across the phase's loads / barriers).
-#ifndef MI_G256_PRIO
-#define MI_G256_PRIO 1
-#endif
+// Wave priority: static s_setprio 1 for the second-dispatched half (waves 4-7) before the main loop
+// (MI355X_MICROARCH.md, two waves per SIMD, item 4) -- the guard must be provably wave-uniform
+// (readfirstlane): a plain `if (wid >= 4)` lowers to s_and_saveexec + an UNCONDITIONAL s_setprio,
+// i.e. every wave at priority 1.  (Per-MFMA-cluster setprio flips measured no better; removed.)
 __device__ __forceinline__ void static_prio() {
-#if MI_G256_PRIO == 1
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
-}
-template <int P>
-__device__ __forceinline__ void cluster_prio() {
-#if MI_G256_PRIO == 2
-  __builtin_amdgcn_s_setprio(P);
-#endif
 }
 
 __device__ __forceinline__ void vm_wait6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
@@ -220,7 +186,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const uint32_t vo = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
         MI_ASSERT(vo == OOB || vo + 16u <= (uint32_t)a.a_bytes, vo);  // valid taps never rely on zero fill
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0,
-                                                 MI_G256_CPOL_A);
+                                                 0);
       }
     }
   };
@@ -252,7 +218,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         f[j][kk] = __builtin_bit_cast(bf16x8, src[(wn * 32 + j * 16 + fr) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
   };
   auto mma = [&](const bf16x8 (&af_)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
-    cluster_prio<1>();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -261,7 +226,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af_[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
-    cluster_prio<0>();
   };
 
   // One k-tile = 4 quadrant phases:
@@ -318,32 +282,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     // arrival with an agent-scope atomic; the last arriver reads the partials with sc1 loads.  The
     // acq_rel __threadfence pair this replaces cost ~3.5 us per fence.
     const size_t tile_f = (size_t)G_BM * G_BN;
-#if MI_FENCE_HANDOFF  // A/B build: the former plain stores + acq_rel fence pair
-    f32x4* mine0 = (f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + split) * tile_f) + tid;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mine0[(i * 4 + j) * 512] = acc[i][j];
-    __syncthreads();
-    int* flag = (int*)smem;
-    if (tid == 0) {
-      __threadfence();
-      flag[0] = atomicAdd(a.counters + tail_tile, 1) == a.tail_split - 1;
-      if (flag[0]) __threadfence();
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    for (int q = 0; q < a.tail_split; ++q) {
-      const f32x4* part = (const f32x4*)(a.ws + ((size_t)tail_tile * a.tail_split + q) * tile_f) + tid;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 v = __builtin_nontemporal_load(part + (i * 4 + j) * 512);
-          acc[i][j] = q == 0 ? v : acc[i][j] + v;
-        }
-    }
-#else
     const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
         a.ws + (size_t)tail_tile * a.tail_split * tile_f, (short)0, (int)(a.tail_split * tile_f * 4), 0x00020000);
     constexpr int SC1 = 16;  // cache-policy bits of the buffer intrinsics: sc1
@@ -370,7 +308,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
           acc[i][j] = q == 0 ? v : acc[i][j] + v;
         }
     }
-#endif
     if (tid == 0) a.counters[tail_tile] = 0;  // ready for the next launch (stream order)
     __syncthreads();
   }
@@ -433,12 +370,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     // 8 row steps in groups of EPI_U: a group's global operand loads (residual C, relu source,
     // BN input) are all issued before its first store, so their HBM latency overlaps instead of
     // serialising behind each step's store (the compiler cannot move a load across a store to C).
-    // MI_G256_EPI_PIPE (conv epilogues): group g + 1's loads are issued before group g is processed
-    // and stored -- two register slots of half the group size, the same footprint
-    constexpr bool PIPE = BN_EPI && MI_G256_EPI_PIPE;
-    constexpr int EPI_U = MODE == 0 ? MI_G256_EPI_U0 : (PIPE ? MI_G256_EPI_UBN / 2 : MI_G256_EPI_UBN);
+    constexpr int EPI_U = MODE == 0 ? kG256EpiU0 : kG256EpiUBN;
     constexpr int NG = 8 / EPI_U;
-    constexpr int SL = PIPE ? 2 : 1;
+    constexpr int SL = 1;
     uint4 cv[SL][EPI_U], yq[SL][EPI_U], xq[SL][EPI_U];
     size_t offs[SL][EPI_U];
     bool ok[SL][EPI_U];
@@ -457,21 +391,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         }
         if (BN_EPI && ok[sl][u] && a.epi >= 4) {
           if (a.epi == 5)
-            cv[sl][u] = acc_ok ? epi_ld16<MI_EPI_NT_CY>((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
-#if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
-          if (a.stats) xq[sl][u] = epi_ld16<MI_EPI_NT_X>(a.aux2 + offs[sl][u]);
-          if (a.bn_relu) yq[sl][u] = xq[sl][u];
-#else
+            cv[sl][u] = acc_ok ? epi_ld16<kEpiNtCY>((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
           if (a.bn_relu) {
             if (a.mbits)
               yq[sl][u].x = a.mbits[offs[sl][u] >> 3];  // mask byte (offs is a multiple of 8)
             else
-              yq[sl][u] = epi_ld16<MI_EPI_NT_CY>(a.aux + offs[sl][u]);
+              yq[sl][u] = epi_ld16<kEpiNtCY>(a.aux + offs[sl][u]);
           }
-          if (a.stats) xq[sl][u] = epi_ld16<MI_EPI_NT_X>(a.aux2 + offs[sl][u]);
-#endif
+          if (a.stats) xq[sl][u] = epi_ld16<kEpiNtX>(a.aux2 + offs[sl][u]);
         } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
-          yq[sl][u] = acc_ok ? epi_ld16<MI_EPI_NT_CY>(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
+          yq[sl][u] = acc_ok ? epi_ld16<kEpiNtCY>(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
         }
       }
     };
@@ -519,26 +448,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
             for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
           }
         }
-#if MI_CONV_NTSTORE
-        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16_t*)a.C + off));
-#else
         *(uint4*)((bf16_t*)a.C + off) = o;
-#endif
       }
     };
-    if constexpr (PIPE) {
-      load_grp(0, 0);
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        if (g + 1 < NG) load_grp(g + 1, (g + 1) & 1);
-        proc_grp(g, g & 1);
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        load_grp(g, 0);
-        proc_grp(g, 0);
-      }
+    for (int g = 0; g < NG; ++g) {
+      load_grp(g, 0);
+      proc_grp(g, 0);
     }
     lgkm_wait0();  // this wave's reads of the slice retire before the next quadrant row overwrites it
   }
@@ -672,7 +588,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
       for (int kk = 0; kk < 2; ++kk) f[j][kk] = tr_frag(src, (wn >> 1) * 64 + (wn & 1) * 32 + j * 16, kk);
   };
   auto mma = [&](const bf16x8 (&af_)[4][2], const bf16x8 (&bf)[2][2], int mq, int nq) {
-    cluster_prio<1>();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -681,7 +596,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af_[i][kk], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
-    cluster_prio<0>();
   };
   auto ktile = [&](int t, bf16x8 (&bc)[2][2], bf16x8 (&bn)[2][2]) {
     issue(t + 1, 1, 0);
@@ -743,9 +657,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_tn_kernel(G256TNArgs a) {
       if (n >= a.N) continue;
       float* dst = a.C + (size_t)m * a.ldc + n;
       const f32x4 v = acc[i][j];
-      if (a.splits > 1 && MI_TN_NOATOMIC) {
-        *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
-      } else if (a.splits > 1) {
+      if (a.splits > 1) {
         atomicAdd(dst, v[0]); atomicAdd(dst + 1, v[1]); atomicAdd(dst + 2, v[2]); atomicAdd(dst + 3, v[3]);
       } else {
         const float4 o = *(float4*)dst;

@@ -21,9 +21,6 @@
 //    reduce kernel sums the splits into the fp32 gradient (deterministic; the
 //    fp32-atomic variant cost ~1 ms per ResNet-50 step at ~1.3 TB/s of atomics).
 #include "common.h"
-#ifndef MI_MASK_PROBE
-#define MI_MASK_PROBE 0  // timing probe (tools/gpu_call_maskprobe.sh)
-#endif
 #include "epilogue.h"
 #include <algorithm>
 #include <array>
@@ -32,48 +29,13 @@
 #include <mutex>
 #include <cstdlib>
 
-#ifndef MI_NT_PROBE
-#define MI_NT_PROBE 0  // timing probes (wrong results): 1 = no output stores, 2 = no operand loads
-#endif
-#ifndef MI_CONV_NTSTORE
-#define MI_CONV_NTSTORE 0
-#endif
-#ifndef MI_SLAB_NT
-#define MI_SLAB_NT 0  // split-K weight-gradient slabs written / reduced non-temporally (A/B builds)
-#endif
-#ifndef MI_NT_CPOL_A
-#define MI_NT_CPOL_A 0  // cache-policy bits of the NT kernel's A (activation) operand loads (A/B builds)
-#endif
-#ifndef MI_TN_CPOL_A
-#define MI_TN_CPOL_A 0  // cache-policy bits of the TN (weight-gradient) operand loads (A/B builds: 2 = nt)
-#endif
-#ifndef MI_TN_CPOL_B
-#define MI_TN_CPOL_B 0
-#endif
-#ifndef MI_NT_EPI_PIPE
-#define MI_NT_EPI_PIPE 0  // NT epilogue operand loads software-pipelined one group ahead (A/B)
-#endif
-#ifndef MI_NT_EPI_EU
-#define MI_NT_EPI_EU 4  // NT epilogue: row steps whose operand loads are issued together
-#endif
-#ifndef MI_NT_BLOCKS_PER_CU
-#define MI_NT_BLOCKS_PER_CU 4
-#endif
-#ifndef MI_NT64_BLOCKS_PER_CU
-#define MI_NT64_BLOCKS_PER_CU 4  // BN = 64 tiles (24.6 KB of LDS)
-#endif
-#ifndef MI_TN_BLOCKS_PER_CU
-#define MI_TN_BLOCKS_PER_CU 3
-#endif
-#ifndef MI_TN_CONV_BLOCKS_PER_CU
-#define MI_TN_CONV_BLOCKS_PER_CU 3  // conv weight-gradient variant (A/B: 4)
-#endif
-#ifndef MI_REDUCE_OLD
-#define MI_REDUCE_OLD 0
-#endif
-#ifndef MI_TN_NOATOMIC
-#define MI_TN_NOATOMIC 0  // timing experiment only: split-K partials stored, not added (wrong results)
-#endif
+// tuned launch occupancies (blocks per CU the kernels are compiled for): 128x128 / 128x64 NT tiles
+// (4 single-stage blocks keep more k-steps and epilogues of the short-K 1x1 convs in flight than 3),
+// TN weight-gradient tiles (plain GEMM / conv)
+constexpr int kNtBlocksPerCu = 4, kNt64BlocksPerCu = 4;
+constexpr int kTnBlocksPerCu = 3, kTnConvBlocksPerCu = 3;
+// NT epilogue: row steps whose operand loads are issued together
+constexpr int kNtEpiEU = 4;
 
 namespace {
 
@@ -114,7 +76,6 @@ struct NTArgs {
   // halo_pb = row blocks per image; fPB / fHW2 divide by halo_pb / (Q + 2)
   int halo_rp, halo_pb;
   FastDiv fPB, fHW2;
-  int halo_breg;  // 64-channel halo tiles: weight fragments of all taps in registers (see nt_kernel)
   // mode 3: blockIdx.y -> parity class (empty classes -- no tap reaches them -- can be skipped when
   // their zero output is not needed); epi 3 / 5 with aux_even: the gradient accumulated into is
   // defined only at even (h, w) of the row grid (a stride-2 1x1 data gradient written by class
@@ -169,9 +130,6 @@ constexpr int BK = 64;
 // decomposed by output parity class (stride 2: only the taps that hit real dY pixels).
 // halo tile capacity (pixels of one 64-channel chunk, 128 B each): (rp + 2) x (Q + 2) <= HALO_PX
 constexpr int HALO_PX = 256;
-#ifndef MI_HALO_BREG
-#define MI_HALO_BREG 0  // 1: A/B build with the register-weight 64-channel halo path (nt_kernel)
-#endif
 
 
 // normalize-on-load: per-channel (scale, shift) table of the gathered tensor, right after the
@@ -204,7 +162,7 @@ __device__ __forceinline__ void nol_chunk(uint4* p, const float* tab, int ch) {
 // <= 128 VGPRs) keep more k-steps and epilogues of the short-K 1x1 convs in flight than 3 did
 template <int BN, int STAGES, bool HALO>
 constexpr int nt_occupancy() {
-  return HALO ? 2 : (STAGES == 1 ? (BN == 64 ? MI_NT64_BLOCKS_PER_CU : MI_NT_BLOCKS_PER_CU) : 2);
+  return HALO ? 2 : (STAGES == 1 ? (BN == 64 ? kNt64BlocksPerCu : kNtBlocksPerCu) : 2);
 }
 
 // STAGES = 1: one LDS buffer, load -> barrier -> MFMA -> barrier per k-step, 3 blocks per CU (the other
@@ -388,7 +346,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       const uint32_t vo = ok ? (uint32_t)(a_base[i] + koffA) * 2u : OOB;
       a_okm |= (ok ? 1u : 0u) << i;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &As[(buf * BM + 32 * i + 8 * wid) * 8]), 16, vo,
-                                               0, 0, MI_NT_CPOL_A);
+                                               0, 0, 0);
     }
     const bool kok = (!SMALLC && a.mode != 0) || (kt * BK + lc * 8 < a.K);
 #pragma unroll
@@ -464,7 +422,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
         const bool ok = px < HP && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
         const uint32_t vo = ok ? (uint32_t)((((hi * H + ih) * W + iw) * Cs + kc + ((chp ^ (px & 7)) * 8)) * 2) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, &Hs[it * 256 + wid * 64]), 16, vo, 0, 0,
-                                                 MI_NT_CPOL_A);
+                                                 0);
       }
     };
     auto load_b = [&](int t, int kc, int buf) {
@@ -500,57 +458,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     };
-    // 64x64-channel 3x3 (ResNet layer 1, BN = 64, one channel chunk), A/B build only (MI_HALO_BREG=1,
-    // then MI355X_DP_HALO_BREG=1 at run time):
-    // the wave's weight fragments of all nine taps (32 columns x 576 k = 144 VGPRs) go to registers
-    // with the halo load, so the nine taps run back to back -- one memory wait per tile instead of a
-    // weight-tile load, vmcnt(0) and barrier per tap.  Measured slower: ResNet-50 12,624 / 12,611 vs
-    // 12,845 / 12,861 img/s (the kernel's 198 VGPRs cost the third resident block per CU that hid
-    // the per-tap waits; profiles/raw/r5/halo_breg/)
-    bool breg_done = false;
-#if MI_HALO_BREG  // compiled only into the A/B build: its registers would lower every BN = 64 halo launch's occupancy
-    if constexpr (BN == 64 && NOL == 0) {
-      if (Cs == 64 && a.halo_breg) {
-        breg_done = true;
-        load_halo(0);
-        bf16x8 breg[9][2][NJ];
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const int n = n0 + wn * WN + 16 * j + fr;  // n < N: BN == 64 == N on this path
-              breg[t][kk][j] = __builtin_bit_cast(
-                  bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, (uint32_t)((n * a.ldb + t * 64 + (kk * 4 + fq) * 8) * 2),
-                                                                0, 0));
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int r = t / 3, sx = t - 3 * r;
-          const int hoff = (a.mode == 1) ? r * HW2 + sx : (2 - r) * HW2 + (2 - sx);
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            bf16x8 af[MI];
-#pragma unroll
-            for (int i = 0; i < MI; ++i) {
-              const int hx = hb[i] + hoff;
-              af[i] = __builtin_bit_cast(bf16x8, Hs[hx * 8 + ((kk * 4 + fq) ^ (hx & 7))]);
-            }
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-              for (int j = 0; j < NJ; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[t][kk][j], af[i], acc[i][j], 0, 0, 0);
-          }
-        }
-        __syncthreads();  // the epilogue's C tile overwrites the halo
-      }
-    }
-#endif
-    for (int kc = 0; kc < Cs && !breg_done; kc += 64) {
+    for (int kc = 0; kc < Cs; kc += 64) {
       load_halo(kc);
       load_b(0, kc, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -602,11 +510,7 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
     }
   } else if constexpr (STAGES == 1) {
     for (int kt = kt0; kt < nk; ++kt) {
-#if MI_NT_PROBE == 2  // timing probe only: no operand loads (LDS left as is)
-      if (kt < 0) issue_loads(kt, 0);
-#else
       issue_loads(kt, 0);
-#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (NOL == 1) {
         if (nol_a) {  // this thread's own A chunks (one row each, logical chunk lc), real pixels only
@@ -772,17 +676,13 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
   // row steps in groups of EU: a group's global operand loads (residual C, relu source, BN input,
   // epilogue aux) are all issued before its first store, so their latency overlaps instead of
   // serialising behind each step's store (the compiler cannot move a load across a store to C).
-  // MI_NT_EPI_PIPE: software-pipelined -- group g + 1's loads are issued before group g is
-  // processed and stored, so operand loads stay in flight through every store phase (two register
-  // slots of EU steps; the default EU halves so the register footprint is unchanged)
   constexpr int NSTEP = BM / RPP;
   // (the mask-from-c 128x128 variant loads one operand per step instead of two: half the group)
-  constexpr int EU1 = (NOL == 2 && BN == 128) ? MI_NT_EPI_EU / 2 : MI_NT_EPI_EU;
-  constexpr int EU0 = MI_NT_EPI_PIPE ? (EU1 / 2 > 0 ? EU1 / 2 : 1) : EU1;
+  constexpr int EU0 = (NOL == 2 && BN == 128) ? kNtEpiEU / 2 : kNtEpiEU;
   constexpr int EU = NSTEP < EU0 ? NSTEP : EU0;
   constexpr int NG = NSTEP / EU;
   static_assert(NSTEP % EU == 0, "epilogue groups must tile the row steps");
-  constexpr int SLOTS = MI_NT_EPI_PIPE ? 2 : 1;
+  constexpr int SLOTS = 1;
   uint4 cv[SLOTS][EU], yq[SLOTS][EU], xq[SLOTS][EU];
   size_t offs[SLOTS][EU];
   bool ok[SLOTS][EU];
@@ -804,21 +704,16 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
       }
       if (ok[sl][u] && a.epi >= 4) {
         if (a.epi == 5)
-          cv[sl][u] = acc_ok ? epi_ld16<MI_EPI_NT_CY>((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
-#if MI_MASK_PROBE  // timing probe only (wrong results): the relu source is not read
-        if (a.stats) xq[sl][u] = epi_ld16<MI_EPI_NT_X>(a.aux2 + offs[sl][u]);
-        if (a.bn_relu) yq[sl][u] = xq[sl][u];
-#else
+          cv[sl][u] = acc_ok ? epi_ld16<kEpiNtCY>((const bf16_t*)a.C + offs[sl][u]) : make_uint4(0, 0, 0, 0);
         if (!MASKC && a.bn_relu) {
           if (a.mbits)
             yq[sl][u].x = a.mbits[offs[sl][u] >> 3];  // mask byte (offs is a multiple of 8)
           else
-            yq[sl][u] = epi_ld16<MI_EPI_NT_CY>(a.aux + offs[sl][u]);
+            yq[sl][u] = epi_ld16<kEpiNtCY>(a.aux + offs[sl][u]);
         }
-        if (a.stats || mask_c) xq[sl][u] = epi_ld16<MI_EPI_NT_X>(a.aux2 + offs[sl][u]);
-#endif
+        if (a.stats || mask_c) xq[sl][u] = epi_ld16<kEpiNtX>(a.aux2 + offs[sl][u]);
       } else if (ok[sl][u] && (a.epi == 2 || a.epi == 3)) {
-        yq[sl][u] = acc_ok ? epi_ld16<MI_EPI_NT_CY>(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
+        yq[sl][u] = acc_ok ? epi_ld16<kEpiNtCY>(a.aux + offs[sl][u]) : make_uint4(0, 0, 0, 0);
       }
     }
   };
@@ -877,29 +772,13 @@ __global__ __launch_bounds__(256, (nt_occupancy<BN, STAGES, HALO>())) void nt_ke
           for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] += f[q] * f[q]; }
         }
       }
-#if MI_NT_PROBE == 1  // timing probe only: output stores dropped (kept alive, never taken)
-      if (o.x == 0x7fc17fc1u && o.y == 0x7fc27fc2u) *(uint4*)((bf16_t*)a.C + off) = o;
-#else
-      if (MI_CONV_NTSTORE)
-        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16_t*)a.C + off));
-      else
-        *(uint4*)((bf16_t*)a.C + off) = o;
-#endif
+      *(uint4*)((bf16_t*)a.C + off) = o;
     }
   };
-  if constexpr (MI_NT_EPI_PIPE) {
-    load_grp(0, 0);
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (g + 1 < NG) load_grp(g + 1, (g + 1) & 1);
-      proc_grp(g, g & 1);
-    }
-  } else {
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      load_grp(g, 0);
-      proc_grp(g, 0);
-    }
+  for (int g = 0; g < NG; ++g) {
+    load_grp(g, 0);
+    proc_grp(g, 0);
   }
   if (a.stats) {
     // the lanes of a wave sharing a column chunk (lane mod CPR) are reduced by xor shuffles, then
@@ -944,7 +823,7 @@ __device__ __forceinline__ int tr_swz(int k) {
 // gather bookkeeping nor the colsum accumulators occupy registers in the variants that do not use
 // them (the conv variant fits 128 VGPRs and runs 4 blocks per CU).
 template <int BM, int BN, int STAGES, int MODE = 1, bool CS = false, bool NOL = false>
-__global__ __launch_bounds__(256, STAGES == 1 ? (MODE == 1 && !CS ? MI_TN_CONV_BLOCKS_PER_CU : MI_TN_BLOCKS_PER_CU) : 2)
+__global__ __launch_bounds__(256, STAGES == 1 ? (MODE == 1 && !CS ? kTnConvBlocksPerCu : kTnBlocksPerCu) : 2)
 void tn_kernel(TNArgs a) {
   static_assert(!NOL || (MODE == 1 && STAGES == 1 && !CS), "normalize-on-load: conv weight gradients");
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -1035,7 +914,7 @@ void tn_kernel(TNArgs a) {
       const bool ok = k < kend && a_m < a.M;
       const uint32_t vo = ok ? (uint32_t)(k * a.lda + a_m) * 2u : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsA, LDS_PTR(void, &As[(buf * BK + A_RSTEP * i + wid * A_RPI) * AU]), 16, vo, 0, 0, MI_TN_CPOL_A);
+          rsA, LDS_PTR(void, &As[(buf * BK + A_RSTEP * i + wid * A_RPI) * AU]), 16, vo, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -1055,7 +934,7 @@ void tn_kernel(TNArgs a) {
         b_q[i] = q; b_p[i] = p; b_img[i] = img;
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsB, LDS_PTR(void, &Bs[(buf * BK + B_RSTEP * i + wid * B_RPI) * BU]), 16, vo, 0, 0, MI_TN_CPOL_B);
+          rsB, LDS_PTR(void, &Bs[(buf * BK + B_RSTEP * i + wid * B_RPI) * BU]), 16, vo, 0, 0, 0);
     }
   };
 
@@ -1231,7 +1110,7 @@ void tn_kernel(TNArgs a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         f32x4* q = slab + ((i * NJ + j) * 4 + wid) * 64 + lane;
-        if (MI_SLAB_NT) __builtin_nontemporal_store(acc[i][j], q); else *q = acc[i][j];
+        *q = acc[i][j];
       }
   } else {
 #pragma unroll
@@ -1246,7 +1125,6 @@ void tn_kernel(TNArgs a) {
           if (m >= a.M) continue;
           float* dst = a.C + (size_t)m * a.ldc + n;
           if (single) *dst += acc[i][j][r];
-          else if (MI_TN_NOATOMIC) *dst = acc[i][j][r];
           else atomicAdd(dst, acc[i][j][r]);
         }
       }
@@ -1271,13 +1149,6 @@ __global__ __launch_bounds__(256) void tn_splitk_reduce_kernel(const f32x4* __re
   const int pl = threadIdx.x & (PB - 1), grp = threadIdx.x >> (8 - log2g);
   const int p = blockIdx.x * PB + pl;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-#if MI_REDUCE_OLD  // A/B build: the former loop
-  if (p < PER) {
-    const f32x4* src = ws + (size_t)tile * splits * PER + p;
-#pragma unroll 4
-    for (int s = grp; s < splits; s += G) v += src[(size_t)s * PER];
-  }
-#else
   {
     // 8 split reads per chunk all in flight (clamped indices, selected after the loads): the
     // unrolled `v += src[...]` loop left a vmcnt(0) behind every other load -- a reduce of 8
@@ -1288,14 +1159,13 @@ __global__ __launch_bounds__(256) void tn_splitk_reduce_kernel(const f32x4* __re
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const f32x4* q = src + (size_t)min(s0 + i * G, splits - 1) * PER;
-        r[i] = MI_SLAB_NT ? __builtin_nontemporal_load(q) : *q;
+        r[i] = *q;
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (s0 + i * G < splits) v += r[i];
     }
   }
-#endif
   part[threadIdx.x] = v;
   __syncthreads();
   if (grp != 0 || p >= PER) return;
@@ -1588,24 +1458,11 @@ static void trace_gemm(const char* what, int mode, int M, int N, int K, int Cs, 
           mode, M, N, K, Cs, R, stride, epi, stats, blocks, splits);
 }
 
-// 64-channel halo convs: per-tap LDS weight tiles (default) or weight fragments in registers
-// (A/B: MI355X_DP_HALO_BREG=1, mi_set_halo_breg)
-static int g_halo_breg = -1;
-MI_API int mi_set_halo_breg(int on) {
-  g_halo_breg = on ? 1 : 0;
-  return 0;
-}
-
 hipError_t dispatch_nt(NTArgs& a, hipStream_t st) {
   if (a.mode == 1 || a.mode == 2) {
     const ConvGeom& g = a.g;
     const int rp = halo_rp(a.M, a.N, g.R, g.S, g.stride, g.pad, g.Cs, g.H, g.W, g.P, g.Q);
     if (rp > 0) {
-      if (g_halo_breg < 0) {
-        const char* e = std::getenv("MI355X_DP_HALO_BREG");
-        g_halo_breg = (e && e[0] == '1') ? 1 : 0;
-      }
-      a.halo_breg = g_halo_breg;
       a.halo_rp = rp;
       a.halo_pb = cdiv(g.P, rp);
       a.fPB = make_fastdiv((uint32_t)a.halo_pb);

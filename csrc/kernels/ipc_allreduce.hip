@@ -36,11 +36,9 @@
 // full-CU compute block (gemm256: 8 waves x 256 VGPRs), so backward on the same GPU stalls behind
 // the collective -- and with two ranks sharing a GPU the peer's backward never reaches its
 // collective at all (a deadlock until the spin bound).  64 blocks keep 3/4 of the CUs free.
-#ifndef MI_IPC_MAX_GRID
-#define MI_IPC_MAX_GRID 64
-#endif
-
 namespace {
+
+constexpr int kIpcMaxGrid = 64;
 
 constexpr int IPC_MAX_PEERS = 8;
 constexpr int IPC_MAX_BLOCKS = 256;
@@ -94,7 +92,7 @@ __device__ __forceinline__ bool ipc_block_sync(const IpcRaw& p, int rank, int wo
 }
 
 int ipc_grid(int64_t work) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>(MI_IPC_MAX_GRID, (work + 255) / 256));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kIpcMaxGrid, (work + 255) / 256));
 }
 
 // ------------------------------------------------------------------ partition of a payload
@@ -427,7 +425,7 @@ MI_API int mi_ipc_allreduce2_f32(const float* const* data, uint32_t* const* flag
   const bool vec = make_peers(p, (const void* const*)data, flags, world) && n % 4 == 0 &&
                    ((uintptr_t)out & 15) == 0 && ((uintptr_t)in & 15) == 0;
   const int64_t shard = ((n + world - 1) / world + 3) & ~(int64_t)3;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(IPC_MAX_BLOCKS, MI_IPC_MAX_GRID),
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(IPC_MAX_BLOCKS, kIpcMaxGrid),
                                                                   (shard + 2047) / 2048));
   const int64_t chunk = ((shard + blocks - 1) / blocks + 3) & ~(int64_t)3;
   if (vec)

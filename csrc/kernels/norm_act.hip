@@ -17,9 +17,9 @@
 namespace {
 
 constexpr int NT = 256;
-#ifndef MI_BNX_NT
-#define MI_BNX_NT 0  // BN-backward statistics and stem BN+pool passes: non-temporal input loads (A/B builds)
-#endif
+// BN-backward statistics and stem BN+pool passes: cached input loads (non-temporal ones measured
+// neutral or slower, round 5: profiles/raw/r5/bnx/)
+constexpr bool kBnxNt = false;
 
 struct SlabGeom {
   int tpr;   // threads per row (each covers 8 channels)
@@ -79,13 +79,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const bf16_t* __restrict__
 // Reduce the [nblk][2][C] partial slab for 64 consecutive channels per block:
 // 1024 threads = 64 channel lanes x 16 row groups, coalesced 256-B row reads,
 // fp64 accumulation, LDS tree over the 16 groups.  Result in (s, q) of tid<64.
-#ifndef MI_FIN_T
-#define MI_FIN_T 1024
-#endif
-#ifndef MI_FENCE_HANDOFF
-#define MI_FENCE_HANDOFF 0  // 1: last-arriver hand-offs through __threadfence pairs (A/B only)
-#endif
-constexpr int FIN_T = MI_FIN_T, FIN_G = FIN_T / 64;
+constexpr int FIN_T = 1024, FIN_G = FIN_T / 64;
 
 // a += sum of p[2 i * C + c], b += sum of p[(2 i + 1) * C + c] over rows i = i0, i0 + step, .. < i1,
 // in row order (bitwise the plain loop's result), with FIN_U rows' loads in flight at once: the
@@ -213,33 +207,17 @@ __global__ void bn_eval_coeffs_kernel(int C, float eps, const float* __restrict_
 // apart, so every wave-instruction stays 1 KB contiguous) in flight before using any, instead of
 // one load -> use -> store chain per iteration.  Channel of vector v: (8 v) mod C, advanced
 // incrementally by the (uniform) stride's channel step.
-#ifndef MI_EW_U
-#define MI_EW_U 4
-#endif
-#ifndef MI_EW_GRID_CAP
-#define MI_EW_GRID_CAP 65536
-#endif
-#ifndef MI_EW_NTSTORE
-#define MI_EW_NTSTORE 1
-#endif
-constexpr int EW_U = MI_EW_U;
+constexpr int EW_U = 4;
+constexpr int kEwGridCap = 65536;  // default elementwise grid cap (MI355X_DP_EW_GRID_CAP)
 
-// 16-byte store of an elementwise result (MI_EW_NTSTORE=1: non-temporal, streaming past L2)
+// 16-byte store of an elementwise result: non-temporal, streaming past L2 (plain stores measured
+// -1.0 % on the BN-backward apply, round 5)
 __device__ __forceinline__ void st16(void* base, int64_t v, uint4 val) {
-  if (MI_EW_NTSTORE)
-    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, val), (u32x4*)base + v);
-  else
-    ((uint4*)base)[v] = val;
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4, val), (u32x4*)base + v);
 }
-// the forward apply's output (the next conv's input): MI_EW_NTSTORE_FWD A/B builds
-#ifndef MI_EW_NTSTORE_FWD
-#define MI_EW_NTSTORE_FWD MI_EW_NTSTORE
-#endif
+// the forward apply's output (the next conv's input): the same policy
 __device__ __forceinline__ void st16f(void* base, int64_t v, uint4 val) {
-  if (MI_EW_NTSTORE_FWD)
-    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, val), (u32x4*)base + v);
-  else
-    ((uint4*)base)[v] = val;
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4, val), (u32x4*)base + v);
 }
 
 struct EwIter {
@@ -354,11 +332,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(const bf16_t* __restri
   for (int r = rb + r0; r < re; r += g.rp) {
     const size_t off = (size_t)r * C + cc;
     float d[8], xv[8];
-    unpack8(epi_ld16<MI_BNX_NT>(dy + off), d);
-    unpack8(epi_ld16<MI_BNX_NT>(x + off), xv);
+    unpack8(epi_ld16<kBnxNt>(dy + off), d);
+    unpack8(epi_ld16<kBnxNt>(x + off), xv);
     if (relu) {
       float yv[8];
-      unpack8(epi_ld16<MI_BNX_NT>(y + off), yv);
+      unpack8(epi_ld16<kBnxNt>(y + off), yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
     }
@@ -434,19 +412,6 @@ __device__ __forceinline__ bool split_fin_body(const float* __restrict__ part, i
   // agent-scope atomic; the finalizer reads the rows with sc1 loads.  The acq_rel __threadfence
   // pair this replaces cost ~3.5 us per fence on the compute stream's critical path, 89 times per
   // ResNet-50 step.
-#if MI_FENCE_HANDOFF  // A/B build: the former acq_rel fence pair
-  if (rg == 0 && c < C) {
-    for (int g = 1; g < TG; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
-    out[(size_t)(2 * split) * C + c] = (float)a;
-    out[(size_t)(2 * split + 1) * C + c] = (float)b;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    *last = atomicAdd(cnt + cg, 1) == S - 1;
-    if (*last) __threadfence();
-  }
-#else
   if (rg == 0) {
     if (c < C) {
       for (int g = 1; g < TG; ++g) { a += red[0][g][cl]; b += red[1][g][cl]; }
@@ -457,7 +422,6 @@ __device__ __forceinline__ bool split_fin_body(const float* __restrict__ part, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) *last = atomicAdd(cnt + cg, 1) == S - 1;
   }
-#endif
   __syncthreads();
   if (!*last) return false;
   if (threadIdx.x == 0) {
@@ -549,13 +513,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const bf16_t* __restri
 // then waits for `ready` (one lane polls with sc1 loads and s_sleep), reads its channel octet's
 // coefficients with sc1 loads (MI355X_MICROARCH.md hand-off table, first row) and sweeps its vectors.
 // The finalizer blocks have the lowest block indices, so they are dispatched first; a bounded wait
-// never hangs anyway: an apply block that waited MI_FIN_WAIT_TICKS (100 MHz) computes the
+// never hangs anyway: an apply block that waited kFinWaitTicks (100 MHz) computes the
 // coefficients itself from the slab (no dgamma / dbeta writes) and counts the event in sync[3].
 // `ready` is reset for the next launch by whichever of {the A apply blocks after their wait, the
 // block that raised it} arrives last (sync[2]); sync[0] counts finalized groups.
-#ifndef MI_FIN_WAIT_TICKS
-#define MI_FIN_WAIT_TICKS 200000  // 2 ms
-#endif
+constexpr uint64_t kFinWaitTicks = 200000;  // 2 ms
 constexpr int FUSED_MAX_C = 2048;
 constexpr int FUSED_T = 512, FUSED_G = FUSED_T / 64;  // 2 waves per SIMD: up to 256 VGPRs, no spills
 struct FusedBwdArgs {
@@ -613,7 +575,7 @@ __global__ __launch_bounds__(FUSED_T) void bn_bwd_fin_apply_kernel(FusedBwdArgs 
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int good = 1;
     while (__hip_atomic_load(p.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)MI_FIN_WAIT_TICKS) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kFinWaitTicks) {
         good = 0;
         break;
       }
@@ -895,7 +857,7 @@ __global__ __launch_bounds__(NT) void bnpool3_fwd_kernel(const bf16_t* __restric
         const int ih = h0 - 1 + r, iw = w0 - 1 + u;
         const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
         ok[r * 3 + u] = in;
-        v[r * 3 + u] = epi_ld16<MI_BNX_NT>(base + ((size_t)(in ? ih : h0) * W + (in ? iw : w0)) * C);
+        v[r * 3 + u] = epi_ld16<kBnxNt>(base + ((size_t)(in ? ih : h0) * W + (in ? iw : w0)) * C);
       }
     }
     float a[8], b[8], best[8];
@@ -938,8 +900,8 @@ __device__ __forceinline__ void bnpool3_quad(const bf16_t* __restrict__ dy, cons
   const size_t o00 = (((size_t)n * P + p) * Q + q) * C + cc;
   const size_t o01 = qn ? o00 + C : o00, o10 = pn ? o00 + (size_t)Q * C : o00;
   const size_t o11 = (pn && qn) ? o00 + (size_t)Q * C + C : o00;
-  const uint4 g00 = epi_ld16<MI_BNX_NT>(dy + o00), g01 = epi_ld16<MI_BNX_NT>(dy + o01);
-  const uint4 g10 = epi_ld16<MI_BNX_NT>(dy + o10), g11 = epi_ld16<MI_BNX_NT>(dy + o11);
+  const uint4 g00 = epi_ld16<kBnxNt>(dy + o00), g01 = epi_ld16<kBnxNt>(dy + o01);
+  const uint4 g10 = epi_ld16<kBnxNt>(dy + o10), g11 = epi_ld16<kBnxNt>(dy + o11);
   const uint2 i00 = *(const uint2*)(idx + o00), i01 = *(const uint2*)(idx + o01);
   const uint2 i10 = *(const uint2*)(idx + o10), i11 = *(const uint2*)(idx + o11);
   const int h0 = 2 * p, w0 = 2 * q;
@@ -948,7 +910,7 @@ __device__ __forceinline__ void bnpool3_quad(const bf16_t* __restrict__ dy, cons
   for (int i = 0; i < 4; ++i) {
     const int h = h0 + (i >> 1), w = w0 + (i & 1);
     valid[i] = h < H && w < W;
-    xv[i] = epi_ld16<MI_BNX_NT>(c + (((size_t)n * H + (valid[i] ? h : h0)) * W + (valid[i] ? w : w0)) * C + cc);
+    xv[i] = epi_ld16<kBnxNt>(c + (((size_t)n * H + (valid[i] ? h : h0)) * W + (valid[i] ? w : w0)) * C + cc);
   }
   float f00[8], f01[8], f10[8], f11[8];
   unpack8(g00, f00); unpack8(g01, f01); unpack8(g10, f10); unpack8(g11, f11);
@@ -1040,13 +1002,13 @@ __global__ __launch_bounds__(NT) void bnpool3_bwd_apply_kernel(const bf16_t* __r
 }
 
 // grid of the elementwise BN passes: one EW_U-vector batch per thread, capped at
-// MI355X_DP_EW_GRID_CAP blocks (default MI_EW_GRID_CAP; a cap near the resident block count turns
+// MI355X_DP_EW_GRID_CAP blocks (default kEwGridCap; a cap near the resident block count turns
 // the launch into a grid-stride sweep without block turnover)
 inline int ew_grid_cap() {
   static int cap = -1;
   if (cap < 0) {
     const char* e = std::getenv("MI355X_DP_EW_GRID_CAP");
-    cap = (e && std::atoi(e) > 0) ? std::atoi(e) : MI_EW_GRID_CAP;
+    cap = (e && std::atoi(e) > 0) ? std::atoi(e) : kEwGridCap;
   }
   return cap;
 }
@@ -1092,9 +1054,7 @@ inline void launch_bn_bwd_apply(const void* dy, const void* y, const void* x, co
 // shift; backward: dgamma / dbeta).  Saves a launch and a dependent kernel boundary per BN per
 // direction (~40 per step of the reference's per-GPU shape, where each cost ~5 us).
 constexpr int SMALL_T = 256, SMALL_G = SMALL_T / 64;
-#ifndef MI_BN_SMALL_ELEMS
-#define MI_BN_SMALL_ELEMS (1 << 20)  // M * C at or below which the fused path runs (0: never)
-#endif
+constexpr int64_t kBnSmallElems = 1 << 20;  // M * C at or below which the fused path runs
 
 __device__ __forceinline__ void small_slab_reduce(const float* __restrict__ part, int nblk, int C, int c, double& s,
                                                   double& q, double (*red)[SMALL_G][64]) {
@@ -1201,7 +1161,7 @@ static int64_t g_bn_small_elems = -1;  // MI355X_DP_BN_SMALL_ELEMS, or mi_bn_set
 inline bool bn_small(int M, int C, int nblk) {
   if (g_bn_small_elems < 0) {
     const char* e = std::getenv("MI355X_DP_BN_SMALL_ELEMS");
-    g_bn_small_elems = e ? std::max(0LL, std::atoll(e)) : (int64_t)MI_BN_SMALL_ELEMS;
+    g_bn_small_elems = e ? std::max(0LL, std::atoll(e)) : kBnSmallElems;
   }
   return (int64_t)M * C <= g_bn_small_elems && C % 64 == 0 && nblk <= 256 && M > 0;
 }
@@ -1232,17 +1192,15 @@ inline void slab_launch_dims(int M, int C, int& nblk, int& rows_per_block, dim3&
 // Tall slabs (e.g. one row per conv M-tile) are first reduced by a (C/64) x S grid into S rows
 // written just past the slab (callers allocate SLAB_EXTRA_ROWS spare rows), then finalized.
 // split rows: the split stage is latency-bound (a 6272-row x 256-channel slab is 12.8 MB read by
-// S x C/64 blocks), so tall slabs are cut into more, shorter splits (MI_SLAB_SPLIT_ROWS rows each;
+// S x C/64 blocks), so tall slabs are cut into more, shorter splits (kSlabSplitRows rows each;
 // A/B on RN50 bs256: 16 rows 22.38 ms, 32 22.03, 64 21.89, 128 21.87, 256 22.04 ms/step)
-#ifndef MI_SLAB_SPLIT_ROWS
-#define MI_SLAB_SPLIT_ROWS 128
-#endif
+constexpr int kSlabSplitRows = 128;
 constexpr int SLAB_EXTRA_ROWS = 256;
 
 inline int tall_slab_split(float* part, int nblk, int C, hipStream_t st, const float*& fin) {
   fin = part;
   if (nblk <= 256) return nblk;
-  const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, MI_SLAB_SPLIT_ROWS));
+  const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, kSlabSplitRows));
   const int rows_per = cdiv(nblk, S);
   float* out = part + (size_t)nblk * 2 * C;
   hipLaunchKernelGGL(slab_split_kernel, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, C, rows_per, out);
@@ -1294,7 +1252,7 @@ inline void slab_finalize(float* part, int nblk, const FinArgs& f, hipStream_t s
   const int C = f.C;
   int* cnt = nblk > 256 ? fin_counters(cdiv(C, 64), st) : nullptr;
   if (cnt) {
-    const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, MI_SLAB_SPLIT_ROWS));
+    const int S = std::min(SLAB_EXTRA_ROWS, cdiv(nblk, kSlabSplitRows));
     const int rows_per = cdiv(nblk, S);
     float* out = part + (size_t)nblk * 2 * C;
     hipLaunchKernelGGL(slab_split_fin_kernel<BWD>, dim3(cdiv(C, 64), S), dim3(FIN_T), 0, st, part, nblk, rows_per,

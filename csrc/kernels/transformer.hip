@@ -11,12 +11,8 @@
 namespace {
 
 constexpr int LN_MAXV = 8;  // 4-element (8-byte) vectors per lane: D <= 64 * 4 * 8 = 2048
-#ifndef MI_LN_REPLICAS
-#define MI_LN_REPLICAS 32  // LayerNorm parameter-gradient replicas (0: atomics straight into dw / db)
-#endif
-#ifndef MI_LN_BWD_RW
-#define MI_LN_BWD_RW 2  // LayerNorm backward rows in flight per wave (D <= 1024); A/B knob
-#endif
+constexpr int kLnReplicas = 32;  // LayerNorm parameter-gradient replicas (0: atomics straight into dw / db)
+constexpr int kLnBwdRW = 2;      // LayerNorm backward rows in flight per wave (D <= 1024)
 
 __device__ __forceinline__ void load4(const bf16_t* p, float* f) {
   const uint2 v = *(const uint2*)p;
@@ -111,7 +107,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   // discarded -- so all of them are in flight together: issued under `if`s, the compiler put a
   // vmcnt wait between every group and the row's ~20 loads paid their latency one group at a
   // time (3.4 TB/s at D = 768).  The weight chunks are loaded once, before the row loop.
-  constexpr int RW = LN_V <= 4 ? MI_LN_BWD_RW : 1;
+  constexpr int RW = LN_V <= 4 ? kLnBwdRW : 1;
   float wr[LN_V][4];
 #pragma unroll
   for (int i = 0; i < LN_V; ++i) {
@@ -198,9 +194,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 // on 2 rows at a time (RW16 row pairs in flight), every load / store is a 16-byte access (half the
 // memory instructions of the 8-byte, full-wave-row kernel), and the row reductions are 5-step
 // half-wave xor shuffles.  dw / db partials as ln_bwd_kernel, over 8 half-waves per block.
-#ifndef MI_LN16_RW
-#define MI_LN16_RW 2   // row pairs in flight per wave
-#endif
+constexpr int kLn16RW = 2;  // row pairs in flight per wave
 
 __device__ __forceinline__ float half_sum(float v) {
 #pragma unroll
@@ -216,7 +210,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const bf16_t* __restrict_
                                                        float* __restrict__ dw, float* __restrict__ db, int M, int D,
                                                        float* __restrict__ rep, int R) {
   extern __shared__ float red[];  // [8 half-waves][D]
-  constexpr int RW = MI_LN16_RW;
+  constexpr int RW = kLn16RW;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5, hl = lane & 31;
   float pw[V][8], pb[V][8], wr[V][8];
 #pragma unroll
@@ -419,7 +413,7 @@ __global__ __launch_bounds__(256) void ln_rep_reduce_kernel(float* __restrict__ 
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= 2 * D) return;
   const int pass = i / D, col = i - pass * D;
-  constexpr int RMAX = MI_LN_REPLICAS > 0 ? MI_LN_REPLICAS : 1;
+  constexpr int RMAX = kLnReplicas > 0 ? kLnReplicas : 1;
   float v[RMAX];  // every replica's load in flight at once, then the fixed-order sum
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) v[r] = r < R ? rep[((size_t)r * 2 + pass) * D + col] : 0.f;
@@ -463,7 +457,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 // [LN_REPLICAS][2][D] zeroed fp32 replicas of the LayerNorm parameter gradients, one per (device,
 // stream), grown on demand (the first call of a shape allocates and zeroes: never inside a graph
 // capture -- a warm-up step runs first); ln_rep_reduce_kernel leaves them zeroed for the next call.
-constexpr int LN_REPLICAS = MI_LN_REPLICAS;
+constexpr int LN_REPLICAS = kLnReplicas;
 struct LnRep { float* p = nullptr; int D = 0; };
 static std::mutex g_lnrep_mu;
 static std::map<std::pair<int, hipStream_t>, LnRep> g_lnrep;
@@ -540,7 +534,7 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
     resident[{dev, lds}] = cus * per_cu;
     return cus * per_cu;
   };
-  const int rw = nvec <= 4 ? MI_LN_BWD_RW : 1;
+  const int rw = nvec <= 4 ? kLnBwdRW : 1;
   float* rep = (dw && db) ? ln_rep_workspace(D, st) : nullptr;
   const int R = LN_REPLICAS;
   static int ln16 = -1;  // MI355X_DP_LN_BWD16=0: always the full-wave-row kernel (A/B)
@@ -569,7 +563,7 @@ MI_API int mi_layernorm_bwd(const void* dy, const void* x, const float* w, const
 #define MI_LN_BWD16_CASE(V)                                                                              \
   case V:                                                                                                \
     hipLaunchKernelGGL(ln_bwd16_kernel<V>,                                                               \
-                       dim3(min(cdiv(M, 8 * MI_LN16_RW), cap16((const void*)ln_bwd16_kernel<V>))), dim3(256), \
+                       dim3(min(cdiv(M, 8 * kLn16RW), cap16((const void*)ln_bwd16_kernel<V>))), dim3(256), \
                        lds16, st, (const bf16_t*)dy, (const bf16_t*)x, w, mean, rstd, (const bf16_t*)dres,    \
                        (bf16_t*)dx, dw, db, M, D, rep, R);                                               \
     break;
