@@ -20,11 +20,13 @@
 //    loads in one in-order counter, so the count adds the epilogue stores issued since the target
 //    load (every epilogue issues a fixed number of stores: rows past M go to an out-of-range
 //    buffer offset and are dropped, never skipped);
-//  * the epilogue stores the unit's bf16 tile straight from the accumulators (permlane16 swaps
-//    widen the MFMA fragments to 16-byte row chunks): nothing in the loop writes LDS, because an
-//    LDS store with LDS-DMA in flight makes hipcc drain vmcnt(0) before it; every lane accumulates
-//    the statistics of the columns it stores over ALL its units in registers, reduced across
-//    lanes and waves once per block (one statistics row per block).
+//  * the epilogue stages the unit's bf16 tile through the ring slot it just consumed (free until
+//    the next issue) and stores full 16-byte row chunks; the staging stores are inline asm, because
+//    an LDS store hipcc can see while LDS-DMA loads are in flight makes it drain vmcnt(0) first
+//    (measured: register-direct permlane16 stores of 16 rows x 64 B per instruction instead were
+//    up to 1.35x slower on the 512-wide expansions); every lane accumulates the statistics of its
+//    fixed 8-channel chunk over ALL its units in registers, reduced across lanes and waves once
+//    per block (one statistics row per block).
 #include "common.h"
 
 #include <algorithm>
@@ -216,52 +218,50 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // per-lane statistics of the columns the lane stores (see epilogue): pair p of fragments, 8 columns
-  float s1[NP][8], s2[NP][8];
+  // epilogue layout: the unit's bf16 tile is staged in the ring slot it consumed and read back one
+  // 16-byte row chunk per lane: lane chunk ec (8 channels) of rows er + RPI u
+  constexpr int CPR = WN / 8;     // 16-B chunks per staged row
+  constexpr int RPI = 64 / CPR;   // rows per read instruction
+  constexpr int NR = WN == 128 ? 16 : 32;  // rows staged per pass (4 KB)
+  constexpr int NU = NR / RPI;    // chunks a lane reads per pass
+  constexpr int HALVES = 32 / NR;
+  const int ec = lane % CPR, er = lane / CPR;
+  const int ncol = n0 + wn * WN + ec * 8;  // output column of the lane's chunk
+  // per-lane statistics of that chunk, over every unit of the wave
+  float s1[8], s2[8];
 #pragma unroll
-  for (int p = 0; p < NP; ++p)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { s1[p][q] = 0.f; s2[p][q] = 0.f; }
+  for (int q = 0; q < 8; ++q) { s1[q] = 0.f; s2[q] = 0.f; }
   const bool want_stats = a.stats != nullptr;
-  // the lane's first output column within a fragment pair (after the permlane16 swap)
-  const int pcol = 16 * (fq & 1) + 8 * (fq >> 1);
-  const int ncol0 = n0 + wn * WN + pcol;
-  // EPI 1: the BN mean of the lane's columns, and the epilogue operands of the next unit
-  float mu[EPI == 1 ? NP : 1][8];
-  uint4 ey[2][NP], ex[2][NP], ek[2][NP];  // ek: mask byte in .x (mbits) or the BN output chunk
-  if constexpr (EPI == 1) {
+  // EPI 1: the BN mean of the lane's channels, and the epilogue operands of the next unit
+  float mu[8];
+  uint4 ey[HALVES * NU], ex[HALVES * NU], ek[HALVES * NU];  // ek: mask byte in .x (mbits) or the BN output
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) mu[p][q] = (a.epi >= 4 && a.stats) ? a.mean[ncol0 + 32 * p + q] : 0.f;
-  }
+  for (int q = 0; q < 8; ++q) mu[q] = (EPI == 1 && a.epi >= 4 && a.stats) ? a.mean[ncol + q] : 0.f;
+  auto row_of = [&](int lu, int h, int u) { return (u0 + lu) * 32 + h * NR + er + RPI * u; };
   // EL loads per call, every lane, whatever the epilogue needs (an unused operand's resource has
   // range 0: the load is dropped but still counted, so the waits' counts never depend on it)
   auto epi_issue = [&](int lu) {
     if constexpr (EPI == 1) {
-      const int mb = (u0 + lu) * 32 + fr;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int m = mb + 16 * i;
-        bool even = true;
-        if (a.aux_even && m < a.M) {
-          const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
-          const uint32_t h = fdiv(rem, a.fQ), w = rem - h * a.fQ.d;
-          even = ((h | w) & 1u) == 0u;
-        }
+      for (int h = 0; h < HALVES; ++h)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          const int col = ncol0 + 32 * p;
+        for (int u = 0; u < NU; ++u) {
+          const int m = row_of(lu, h, u), k = h * NU + u;
+          bool even = true;
+          if (a.aux_even && m < a.M) {
+            const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
+            const uint32_t hh = fdiv(rem, a.fQ), w = rem - hh * a.fQ.d;
+            even = ((hh | w) & 1u) == 0u;
+          }
           const bool ok = lu < nu && m < a.M;
-          const uint32_t off = ok ? (uint32_t)(m * a.ldc + col) * 2u : PN_OOB;
-          ey[i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsY, even ? off : PN_OOB, 0, 2));
-          ex[i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsX, off, 0, 0));
+          const uint32_t off = ok ? (uint32_t)(m * a.ldc + ncol) * 2u : PN_OOB;
+          ey[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsY, even ? off : PN_OOB, 0, 2));
+          ex[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsX, off, 0, 0));
           if (a.mbits)
-            ek[i][p].x = __builtin_amdgcn_raw_buffer_load_b8(rsK, ok ? off >> 4 : PN_OOB, 0, 0);
+            ek[k].x = __builtin_amdgcn_raw_buffer_load_b8(rsK, ok ? off >> 4 : PN_OOB, 0, 0);
           else
-            ek[i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsK, off, 0, 2));
+            ek[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsK, off, 0, 2));
         }
-      }
     }
   };
 
@@ -283,35 +283,67 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
     }
   };
 
-  // epilogue of unit lu straight from the accumulators -- no LDS write (an LDS store while LDS-DMA
-  // loads are in flight makes hipcc drain vmcnt(0) first: the prefetch would die at every unit).
-  // Lane (fr, fq) holds D[n = 16 j + 4 fq + r][m = 16 i + fr] of each fragment; the permlane16 swap
-  // of fragment pair (2p, 2p + 1) leaves it row 16 i + fr, columns 32 p + pcol + [0, 8): one 16-byte
-  // store per (i, p), 16 rows x 64 contiguous bytes per store instruction (gemm256p.hip's flush)
-  auto epilogue = [&](int lu) {
-    const int mb = (u0 + lu) * 32 + fr;
+  // epilogue of unit lu through the slot cur it consumed: lane (fr, fq) holds D[n = 16 j + 4 fq + r]
+  // [m = 16 i + fr] of each fragment -> row-major bf16 rows in the slot, the 16-B chunk index XOR-
+  // swizzled by the row (the ds_write_b64 groups of 16 rows hit distinct bank pairs); read back as
+  // full row chunks, one 16-byte store each.  The staging stores are inline asm: an LDS store the
+  // compiler can see, with LDS-DMA loads in flight, makes hipcc drain vmcnt(0) before it, and the
+  // ring's prefetch would die at every unit (the slot is this wave's own and free until the next
+  // issue; its k-step reads completed before the MFMAs that consumed them)
+  auto epilogue = [&](uint4* Cs, int lu) {
+    const uint32_t cbase = (uint32_t)(uintptr_t)LDS_PTR(void, Cs);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = mb + 16 * i;
+    for (int h = 0; h < HALVES; ++h) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const f32x4 v0 = acc[i][2 * p], v1 = acc[i][2 * p + 1];
-        const uint32_t p0 = pack2bf(v0[0], v0[1]), p1 = pack2bf(v0[2], v0[3]);
-        const uint32_t q0 = pack2bf(v1[0], v1[1]), q1 = pack2bf(v1[2], v1[3]);
-        const auto x0 = __builtin_amdgcn_permlane16_swap(p0, q0, false, false);
-        const auto x1 = __builtin_amdgcn_permlane16_swap(p1, q1, false, false);
-        uint4 o = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+      for (int ii = 0; ii < 2 / HALVES; ++ii) {
+        const int i = h + ii;  // fragment row block
+        const int row = WN == 128 ? fr : 16 * i + fr;
+        const int sw = WN == 128 ? row : ((row >> 1) & 7);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const f32x4 v = acc[i][j];
+          const int pc = (2 * j + (fq >> 1)) ^ sw;
+          const uint32_t addr = cbase + (uint32_t)(row * (WN * 2) + pc * 16 + (fq & 1) * 8);
+          const uint2 d = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+          asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(d) : "memory");
+        }
+      }
+      // the read-back, also opaque to hipcc (a visible ds_read of the slot gets a vmcnt(0) as well):
+      // the NU reads and their wait in ONE statement, so no consumer can run ahead of the data
+      uint32_t ra[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int rr = er + RPI * u;
+        const int sw = WN == 128 ? rr : ((rr >> 1) & 7);
+        ra[u] = cbase + (uint32_t)(rr * (WN * 2) + ((ec ^ sw) * 16));
+      }
+      static_assert(NU == 4, "four read-back chunks per pass");
+      u32x4 rb[4];
+      asm volatile(
+          "ds_read_b128 %0, %4\n\t"
+          "ds_read_b128 %1, %5\n\t"
+          "ds_read_b128 %2, %6\n\t"
+          "ds_read_b128 %3, %7\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(rb[0]), "=&v"(rb[1]), "=&v"(rb[2]), "=&v"(rb[3])
+          : "v"(ra[0]), "v"(ra[1]), "v"(ra[2]), "v"(ra[3])
+          : "memory");
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int k = h * NU + u;
+        uint4 o = __builtin_bit_cast(uint4, rb[u]);
+        const int m = row_of(lu, h, u);
         if constexpr (EPI == 0) {
           if (want_stats) {
             float f[8];
             unpack8(o, f);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) { s1[p][q] += f[q]; s2[p][q] = fmaf(f[q], f[q], s2[p][q]); }
+            for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] = fmaf(f[q], f[q], s2[q]); }
           }
         } else if (a.epi == 3) {
           float f[8], g[8];
           unpack8(o, f);
-          unpack8(ey[i][p], g);
+          unpack8(ey[k], g);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += g[q];
           o = pack8(f);
@@ -320,25 +352,24 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
           unpack8(o, f);
           if (a.epi == 5) {
             float g[8];
-            unpack8(ey[i][p], g);
+            unpack8(ey[k], g);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] += g[q];
           }
           if (a.bn_relu) {
-            const uint32_t bits = a.mbits ? ek[i][p].x : nz_bits8(ek[i][p]);
+            const uint32_t bits = a.mbits ? ek[k].x : nz_bits8(ek[k]);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] = ((bits >> q) & 1u) ? f[q] : 0.f;
           }
           o = pack8(f);
           if (want_stats) {
             float xv[8];
-            unpack8(ex[i][p], xv);
+            unpack8(ex[k], xv);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) { s1[p][q] += f[q]; s2[p][q] = fmaf(f[q], xv[q] - mu[p][q], s2[p][q]); }
+            for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] = fmaf(f[q], xv[q] - mu[q], s2[q]); }
           }
         }
-        const int col = ncol0 + 32 * p;
-        const uint32_t off = (m < a.M && col < a.N) ? (uint32_t)(m * a.ldc + col) * 2u : PN_OOB;
+        const uint32_t off = (m < a.M && ncol < a.N) ? (uint32_t)(m * a.ldc + ncol) * 2u : PN_OOB;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsC, off, 0, 0);
       }
     }
@@ -362,7 +393,7 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
     compute(cur, kt);
     ehist <<= 1;
     if (++kt == nk) {
-      epilogue(lu);
+      epilogue(cur, lu);
       epi_issue(lu + 1);  // past the last unit: dropped loads (the counts hold)
       ehist |= 1u;
       kt = 0;
@@ -371,31 +402,27 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
     slot = slot + 1 == S ? 0 : slot + 1;
   }
 
-  // ---- statistics: the 16 lanes of a row share their columns (xor over fr), then the WMW waves of
+  // ---- statistics: lanes sharing a chunk (xor over the row bits of the lane), then the WMW waves of
   // each column sub-panel through LDS, in a fixed order
   if (want_stats) {
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
+    for (int o = CPR; o < 64; o <<= 1)
 #pragma unroll
-      for (int p = 0; p < NP; ++p)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          s1[p][q] += __shfl_xor(s1[p][q], o, 64);
-          s2[p][q] += __shfl_xor(s2[p][q], o, 64);
-        }
+      for (int q = 0; q < 8; ++q) {
+        s1[q] += __shfl_xor(s1[q], o, 64);
+        s2[q] += __shfl_xor(s2[q], o, 64);
+      }
   }
   PN_VMWAIT(0);  // the ring's trailing dummy loads still write LDS
   __syncthreads();
   if (want_stats) {
     float* red = (float*)smem;  // [8 waves][2][WN]
-    if (fr == 0) {
+    if (lane < CPR) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          red[(wid * 2 + 0) * WN + 32 * p + pcol + q] = s1[p][q];
-          red[(wid * 2 + 1) * WN + 32 * p + pcol + q] = s2[p][q];
-        }
+      for (int q = 0; q < 8; ++q) {
+        red[(wid * 2 + 0) * WN + ec * 8 + q] = s1[q];
+        red[(wid * 2 + 1) * WN + ec * 8 + q] = s2[q];
+      }
     }
     __syncthreads();
     for (int c = tid; c < 2 * BN; c += 512) {

@@ -319,7 +319,7 @@ __global__ void bnf_finalize_kernel(const float* __restrict__ part, BnF32Fin f) 
     f.save_invstd[c] = invstd;
     const float gm = f.gamma ? f.gamma[c] : 1.f, bt = f.beta ? f.beta[c] : 0.f;
     f.scale[c] = gm * invstd;
-    f.shift[c] = bt - (float)mean * gm * invstd;
+    f.shift[c] = bt;  // the apply centres x on save_mean (bnf_apply_kernel)
     if (f.rmean) {
       const double unbiased = f.M > 1 ? var * f.M / (f.M - 1) : var;
       f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (float)mean;
@@ -340,15 +340,21 @@ __global__ void bnf_finalize_kernel(const float* __restrict__ part, BnF32Fin f) 
   }
 }
 
-// y = act(x * scale + shift (+ res))
+// y = act(x * scale + shift (+ res)); center (training forward, the batch mean): y = act((x - center) *
+// scale + shift (+ res)) with shift = beta -- the centred form keeps fp32 accuracy when |mean| >> std,
+// where x * scale and beta - mean * scale would cancel (as PyTorch's (x - mean) * invstd * w + b)
 __global__ __launch_bounds__(FT) void bnf_apply_kernel(const float* __restrict__ x, const float* __restrict__ res,
                                                        float* __restrict__ y, const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, int64_t nvec, int C,
-                                                       int relu) {
+                                                       const float* __restrict__ shift, const float* __restrict__ center,
+                                                       int64_t nvec, int C, int relu) {
   for (int64_t v = blockIdx.x * (int64_t)FT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * FT) {
     const int c = (int)((v * 4) % C);
     float4 a = ((const float4*)x)[v];
     const float4 sc = *(const float4*)(scale + c), sh = *(const float4*)(shift + c);
+    if (center) {
+      const float4 mu = *(const float4*)(center + c);
+      a.x -= mu.x; a.y -= mu.y; a.z -= mu.z; a.w -= mu.w;
+    }
     a.x = a.x * sc.x + sh.x; a.y = a.y * sc.y + sh.y; a.z = a.z * sc.z + sh.z; a.w = a.w * sc.w + sh.w;
     if (res) {
       const float4 r = ((const float4*)res)[v];
@@ -542,7 +548,8 @@ MI_API int mi_f32_bn_fwd_train(const float* x, const float* res, float* y, int M
   hipLaunchKernelGGL(bnf_finalize_kernel<false>, dim3(cdiv(C, 256)), dim3(256), 0, st, part, f);
   if (y) {
     const int64_t nvec = (int64_t)M * C / 4;
-    hipLaunchKernelGGL(bnf_apply_kernel, dim3(ew_grid(nvec)), dim3(FT), 0, st, x, res, y, scale, shift, nvec, C, relu);
+    hipLaunchKernelGGL(bnf_apply_kernel, dim3(ew_grid(nvec)), dim3(FT), 0, st, x, res, y, scale, shift, save_mean,
+                       nvec, C, relu);
   }
   return (int)hipGetLastError();
 }
@@ -552,7 +559,8 @@ MI_API int mi_f32_bn_apply(const float* x, const float* res, float* y, int M, in
                            const float* shift, int relu, hipStream_t st) {
   if (C % 4) return (int)hipErrorInvalidValue;
   const int64_t nvec = (int64_t)M * C / 4;
-  hipLaunchKernelGGL(bnf_apply_kernel, dim3(ew_grid(nvec)), dim3(FT), 0, st, x, res, y, scale, shift, nvec, C, relu);
+  hipLaunchKernelGGL(bnf_apply_kernel, dim3(ew_grid(nvec)), dim3(FT), 0, st, x, res, y, scale, shift, nullptr, nvec,
+                     C, relu);
   return (int)hipGetLastError();
 }
 

@@ -494,6 +494,31 @@ def test_graphed_engine_two_ranks_gated_buckets():
               f"{end:.2f} ms")
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL needs one device per rank (>= 2 GPUs)")
+@pytest.mark.parametrize("backend", ["nccl", "smddp"])
+def test_graphed_engine_two_ranks_captured_rccl(backend):
+    """the default graphed comm mode, 'capture' (bucket all-reduces, the BN-buffer
+    broadcast, the join and the 1/world scaling recorded INTO the backward graph), at world 2 over
+    RCCL on two devices -- torch nccl and the native smddp backend on its RCCL path: graphed == eager
+    bit for bit (losses and flat fp32 parameters) and identical replicas."""
+    import json
+    env = {**os.environ, "PYTHONPATH": ROOT, "GRAPHED_BACKEND": backend, "MI355X_DP_SMDDP_IPC_ONLY": "0",
+           "MI355X_DP_SMDDP_IPC": "0"}
+    env.pop("MI355X_DP_SMDDP_DEVICE", None)
+    r = subprocess.run([sys.executable, "-m", "mi355x_dp.launch", "--nproc", "2",
+                        os.path.join(ROOT, "tools", "graphed_world2.py")], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = [json.loads(l[l.index("{"):]) for l in r.stdout.splitlines() if '"rank"' in l]
+    assert len(rows) == 2, r.stdout[-2000:]
+    for row in rows:
+        assert row["comm_modes"] == ["capture"], row
+        assert row["replays"] == 6 and row["replays_eager"] == 0, row
+        assert row["losses_graphed"] == row["losses_eager"], row
+        assert row["graphed_equals_eager"] and row["replicas_identical"], row
+    assert rows[0]["losses_graphed"] != rows[1]["losses_graphed"]
+
+
 @pytest.mark.skipif(REF_CODE is None, reason="reference scripts not staged (run build())")
 def test_reference_job_per_gpu_shape():
     """tools/reference_job.py: the unmodified reference script as a local job at the reference's

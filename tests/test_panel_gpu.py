@@ -141,9 +141,9 @@ def test_panel_dgrad1x1(lib, shape, epi, mask, stats, flags):
     if flags & 2:  # only even (h, w) defined: odd pixels hold garbage the kernel must not read
         base[:, :, 1::2, :] = float("nan")
         base[:, :, :, 1::2] = float("nan")
-    aux = base if epi == 3 else None
     x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
     y = torch.relu(torch.randn(N, C, H, H, device="cuda")).to(BF).contiguous(memory_format=CL)
+    aux = base if epi == 3 else (y if mask == "y" else None)  # the residual, or the BN output for the mask
     yb = (y.permute(0, 2, 3, 1).reshape(M, C // 8, 8) > 0).to(torch.int32)
     bits = (yb << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
     mean = torch.randn(C, device="cuda") * 0.1

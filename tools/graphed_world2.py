@@ -7,7 +7,9 @@ and prints one JSON line: per-step losses of both runs, whether the final flat f
 bit-identical between the runs, the replica checksum of every rank, and the gate trace of the last
 graphed step (ms from the replay's start at which each bucket's collective was released, and the ms
 at which the replayed backward ended).  Launched by tests/test_gpu_integration.py through the
-native launcher with IPC-only smddp (ranks may share one GPU)."""
+native launcher with IPC-only smddp (ranks may share one GPU), or -- on a box with >= 2 GPUs -- over
+RCCL (GRAPHED_BACKEND=nccl, or smddp with MI355X_DP_SMDDP_IPC_ONLY=0), where the collectives are
+captured into the backward graph (comm mode "capture")."""
 import json
 import os
 import sys
@@ -21,7 +23,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 import smdistributed.dataparallel.torch.torch_smddp  # noqa: E402,F401  (installs the engine-backed DDP)
 
-dist.init_process_group(backend="smddp")
+BACKEND = os.environ.get("GRAPHED_BACKEND", "smddp")  # "nccl": torch's ProcessGroupNCCL (RCCL)
+if BACKEND == "nccl":
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+dist.init_process_group(backend=BACKEND)
 r, w = dist.get_rank(), dist.get_world_size()
 STEPS = int(os.environ.get("GRAPHED_STEPS", "8"))
 # per-rank batch / image size (default: the reference's 32 at 32x32).  The gate-overlap check of the
