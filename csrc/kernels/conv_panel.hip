@@ -436,8 +436,9 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
 }
 
 // ------------------------------------------------------------------ host side
-// MI355X_DP_PANEL: 1 route eligible 1x1 convs with >= PN_MIN_M output rows here (default), 0 never,
-// 2 any row count (tests: small shapes stay on the split-K 64-tile kernels otherwise)
+// MI355X_DP_PANEL (mi_set_panel): 1 route eligible 1x1 convs with >= PN_MIN_M output rows here
+// (default), 0 never, 2 any row count (tests: small shapes stay on the split-K 64-tile kernels
+// otherwise); + 4 the 3x3 pad-1 stride-1 convs too (off by default, mi_panel_3x3)
 static int g_pn_mode = -1;
 constexpr int PN_MIN_M = 16384;
 static int g_pn_cus = 0;
@@ -452,9 +453,9 @@ PanelPlan panel_plan(int M, int N, int K, bool dgrad) {
   PanelPlan p;
   if (g_pn_mode < 0) {
     const char* e = std::getenv("MI355X_DP_PANEL");
-    g_pn_mode = (e && e[0] == '0') ? 0 : 1;
+    g_pn_mode = (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 1;
   }
-  if (!g_pn_mode || K % 64 != 0 || K > 576 || N % 64 != 0 || M < (g_pn_mode == 2 ? 1 : PN_MIN_M)) return p;
+  if (!(g_pn_mode & 3) || K % 64 != 0 || K > 576 || N % 64 != 0 || M < ((g_pn_mode & 2) ? 1 : PN_MIN_M)) return p;
   if (g_pn_cus == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -515,8 +516,15 @@ int launch_plan(const PanelPlan& p, PanelArgs& a, hipStream_t st, const char* wh
 }  // namespace
 
 MI_API int mi_set_panel(int mode) {
-  g_pn_mode = mode == 2 ? 2 : (mode ? 1 : 0);
+  g_pn_mode = mode & 7;
   return 0;
+}
+
+// the 3x3 (pad 1) convolutions route to the panel kernel only with mode bit 4: measured 0.94x (forward)
+// and 0.98x (data gradient) of the halo-tiled 3x3 kernels on the layer-1 shapes (profiles/panel_r6.md)
+MI_API int mi_panel_3x3() {
+  if (g_pn_mode < 0) (void)panel_plan(0, 0, 0, false);  // env init
+  return (g_pn_mode & 4) ? 1 : 0;
 }
 
 // statistics rows the panel kernel writes for an M x N x K conv forward (dgrad = 0) or data gradient

@@ -1758,15 +1758,17 @@ extern "C" int mi_panel_conv(const void* x, const void* w, void* y, float* stats
                              int R, int stride, int pad, int P, int Q, hipStream_t st);
 // a 1x1 or 3x3 (pad 1) stride-1 data gradient runs on the panel kernel (the statistics slab rows it
 // writes), else 0
+extern "C" int mi_panel_3x3();
 static int panel_rows_dgrad(int M, int C, int K, int RS, int stride) {
-  if ((RS != 1 && RS != 9) || stride != 1 || K % 64 != 0) return 0;
+  if ((RS != 1 && !(RS == 9 && mi_panel_3x3())) || stride != 1 || K % 64 != 0) return 0;
   return mi_panel_stat_rows2(M, C, RS * K, 1);
 }
 extern "C" int mi_panel_conv1x1(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C,
                                 int K, int stride, int P, int Q, hipStream_t st);
 static int panel_rows_fwd(int M, int N, int C, int R, int S, int pad, int H, int W, int P, int Q, int stride) {
   if (C % 64 != 0) return 0;
-  if (R == 3 && S == 3 && stride == 1 && pad == 1 && P == H && Q == W) return mi_panel_stat_rows(M, N, 9 * C);
+  if (R == 3 && S == 3 && stride == 1 && pad == 1 && P == H && Q == W)
+    return mi_panel_3x3() ? mi_panel_stat_rows(M, N, 9 * C) : 0;
   if (R != 1 || S != 1 || pad != 0 || P != (H - 1) / stride + 1 || Q != (W - 1) / stride + 1) return 0;
   return mi_panel_stat_rows(M, N, C);
 }

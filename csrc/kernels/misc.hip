@@ -542,3 +542,33 @@ MI_API int mi_ring_emulate(void* buf, int64_t bytes, void* tmp, const void* zero
                      (const uint32_t*)zero, (int64_t)(bytes / 4), world, ticks);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------ command-processor gates
+// The same bucket gate as mi_flag_gate without a spinning wave: hipStreamWaitValue32 enqueues a wait
+// the command processor evaluates, so no CU slot is held while the replayed backward runs.  The flag
+// must be signal memory (hipMallocSignalMemory, one 8-byte signal per bucket); the graph's bump
+// kernel adds to it like to a plain flag.  There is no device-side timeout: a waiting stream is
+// released from the host (mi_flag_release, a stream write of a value past any target).
+MI_API int mi_wait_value_supported() {
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) return 0;
+  return v;
+}
+
+MI_API int mi_signal_alloc(void** out) {
+  void* p = nullptr;
+  if (hipError_t e = hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory); e != hipSuccess) return (int)e;
+  if (hipError_t e = hipMemset(p, 0, 8); e != hipSuccess) return (int)e;
+  if (hipError_t e = hipDeviceSynchronize(); e != hipSuccess) return (int)e;
+  *out = p;
+  return 0;
+}
+
+MI_API int mi_flag_wait(uint32_t* flag, uint32_t target, hipStream_t st) {
+  return (int)hipStreamWaitValue32(st, flag, target, hipStreamWaitValueGte, 0xFFFFFFFFu);
+}
+
+MI_API int mi_flag_release(uint32_t* flag, uint32_t value, hipStream_t st) {
+  return (int)hipStreamWriteValue32(st, flag, value, 0);
+}

@@ -650,10 +650,11 @@ class DataParallel(nn.Module):
                 g.pending = False
         gated = self.__dict__.pop("_graph_gated", None)
         self.finish_gradient_sync(average=True)
-        if gated is not None:
-            # a gate that timed out let its collective run on stale gradients: find out (host wait for
-            # the last gate, i.e. until the replayed backward reached its last bucket) and raise
-            # before backward() returns -- before any optimizer step can use the result
+        if gated is not None and not gated.gates.cp:
+            # a polling gate that timed out let its collective run on stale gradients: find out (host
+            # wait for the last gate, i.e. until the replayed backward reached its last bucket) and
+            # raise before backward() returns -- before any optimizer step can use the result.
+            # Command-processor gates cannot time out into stale data: no host wait at all
             from .step_graph import BucketGates
             ev = self.__dict__.pop("_last_gate_event", None)
             if ev is not None:

@@ -180,12 +180,20 @@ class _Replay(torch.autograd.Function):
         return None, None, None
 
 
+# how a gate waits: "cp" -- hipStreamWaitValue32 on signal memory, evaluated by the command processor
+# (no wave held on a CU while the replayed backward runs); "kernel" -- a one-wave
+# polling kernel with a device-side timeout (mi_flag_gate); "auto": cp where the device supports it
+GATE_WAIT = os.environ.get("MI355X_DP_GATE_WAIT", "auto")
+
+
 class BucketGates:
     """One flag word per gradient bucket of a captured backward (misc.hip ``mi_flag_bump`` /
-    ``mi_flag_gate``): the graph bumps a bucket's flag right after the bucket's last gradient
-    kernel; after a replay the engine's gate stream waits, per bucket, until the flag reaches the
-    replay count and then launches that bucket's collective -- so bucket k's all-reduce runs while
-    the rest of the replayed backward still computes, as in eager mode."""
+    ``mi_flag_wait`` or ``mi_flag_gate``): the graph bumps a bucket's flag right after the bucket's
+    last gradient kernel; after a replay the engine's gate stream waits, per bucket, until the flag
+    reaches the replay count and then launches that bucket's collective -- so bucket k's all-reduce
+    runs while the rest of the replayed backward still computes, as in eager mode.  With command-
+    processor waits (``cp``) nothing can time out into stale data (a collective simply waits for its
+    bucket), so the end of backward needs no host wait on the last gate."""
 
     TIMEOUT_MS = max(1, int(os.environ.get("MI355X_DP_GATE_TIMEOUT_MS", "60000")))
 
@@ -195,9 +203,19 @@ class BucketGates:
         from mi355x_dp.ops import kernels  # noqa: F401
         self._lib = _lib
         lib = _lib.load(True)
-        p = ctypes.c_void_p()
-        _lib.check(lib.mi_flags_alloc(n, ctypes.byref(p)), "mi_flags_alloc")
-        self.base, self.n = p.value, n  # kept for the process's life, like the graph's pool
+        self.n = n
+        self.cp = GATE_WAIT == "cp" or (GATE_WAIT == "auto" and bool(lib.mi_wait_value_supported()))
+        if self.cp:
+            # one 8-byte signal per bucket (hipMallocSignalMemory), kept for the process's life
+            self.flags = []
+            for _ in range(max(n, 1)):
+                p = ctypes.c_void_p()
+                _lib.check(lib.mi_signal_alloc(ctypes.byref(p)), "mi_signal_alloc")
+                self.flags.append(p.value)
+        else:
+            p = ctypes.c_void_p()
+            _lib.check(lib.mi_flags_alloc(n, ctypes.byref(p)), "mi_flags_alloc")
+            self.flags = [p.value + 4 * b for b in range(max(n, 1))]
         if BucketGates._err is None:
             host, dev = ctypes.c_void_p(), ctypes.c_void_p()
             _lib.check(lib.mi_host_word_alloc(ctypes.byref(host), ctypes.byref(dev)), "mi_host_word_alloc")
@@ -207,7 +225,7 @@ class BucketGates:
 
     def _flag(self, b):
         import ctypes
-        return ctypes.c_void_p(self.base + 4 * b)
+        return ctypes.c_void_p(self.flags[b])
 
     def bump(self, b: int, stream):
         import ctypes
@@ -215,8 +233,11 @@ class BucketGates:
 
     def gate(self, b: int, target: int, stream):
         import ctypes
-        self._lib.call("mi_flag_gate", self._flag(b), target & 0xFFFFFFFF, BucketGates._err[1], self.TIMEOUT_MS,
-                       ctypes.c_void_p(stream.cuda_stream))
+        if self.cp:
+            self._lib.call("mi_flag_wait", self._flag(b), target & 0xFFFFFFFF, ctypes.c_void_p(stream.cuda_stream))
+        else:
+            self._lib.call("mi_flag_gate", self._flag(b), target & 0xFFFFFFFF, BucketGates._err[1], self.TIMEOUT_MS,
+                           ctypes.c_void_p(stream.cuda_stream))
 
     @staticmethod
     def check():

@@ -366,3 +366,18 @@ def test_emulated_dp8_bench_world1():
     # ResNet-50's 102 MB of fp32 gradients: >= 2 * 7/8 * 102 MB / (7 * 153 GB/s) ~ 0.17 ms of paced ring time
     assert tl["comm_ms"] >= 0.15, tl
     assert out["loss_last"] == out["loss_last"]
+
+
+def test_command_processor_gate():
+    """the bucket gate as a command-processor wait (hipStreamWaitValue32 on signal
+    memory, misc.hip mi_flag_wait) instead of a polling wave: a high-priority stream's wait enqueued
+    before the producer opens only after the producer stream's bump, with no host release needed
+    (tools/wait_value_probe.py; a probe that would hang is released from the host)."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "wait_value_probe.py")], capture_output=True,
+                       text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    if not out["supported"]:
+        pytest.skip("hipDeviceAttributeCanUseStreamWaitValue = 0 on this device")
+    assert out["ok"], out

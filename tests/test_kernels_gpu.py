@@ -594,9 +594,19 @@ def test_normalize_on_load_kernels(shape):
     from mi355x_dp.ops import _lib
     from mi355x_dp.ops import kernels  # noqa: F401
     from mi355x_dp.ops._lib import ptr, stream_of
+    lib = _lib.load()
+    # the 1x1 expansions route to the persistent panel kernel by default, which has no NoL variant:
+    # the NoL kernels are checked with the panel route off
+    lib.mi_set_panel(0)
+    try:
+        _check_nol_kernels(lib, _lib, ptr, stream_of, shape)
+    finally:
+        lib.mi_set_panel(1)
+
+
+def _check_nol_kernels(lib, _lib, ptr, stream_of, shape):
     N, C, H, K, R, s, p = shape
     P = (H + 2 * p - R) // s + 1
-    lib = _lib.load()
     assert lib.mi_conv_nol_ok(N, H, H, C, K, R, R, s, p, P, P), "shape no longer routes to a NoL kernel"
     g = torch.Generator(device="cuda").manual_seed(3)
     c = torch.randn(N, C, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)

@@ -68,7 +68,7 @@ def test_panel_conv1x1_fwd(lib, shape):
     M = N * P * P
     x = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
     w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(BF).contiguous(memory_format=CL)
-    lib.mi_set_panel(2)  # any row count
+    lib.mi_set_panel(6)  # any row count, 3x3 included
     rows = lib.mi_panel_stat_rows(M, K, C * R * R)
     assert rows > 0, "shape not routed to the panel kernel"
     assert lib.mi_conv_stat_rows_g(N, H, H, C, K, R, R, s, pad, P, P) == rows
@@ -87,7 +87,7 @@ def test_panel_conv1x1_fwd(lib, shape):
     rows0 = lib.mi_conv_stat_rows_g(N, H, H, C, K, R, R, s, pad, P, P)
     y0 = _fwd(lib, x, w, s, torch.empty(rows0, 2, K, device="cuda"))
     lib.mi_set_nt_split_blocks(128)
-    lib.mi_set_panel(2)
+    lib.mi_set_panel(6)
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
     # no statistics requested: the plain store path
@@ -148,11 +148,11 @@ def test_panel_dgrad1x1(lib, shape, epi, mask, stats, flags):
     bits = (yb << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
     mean = torch.randn(C, device="cuda") * 0.1
     out = {}
-    for mode in (2, 0):
+    for mode in (6, 0):
         lib.mi_set_panel(mode)
         lib.mi_set_nt_split_blocks(0)
         rows = lib.mi_dgrad_stat_rows(N, H, H, C, H, H, 1, K, R * R)
-        if mode == 2:
+        if mode == 6:
             assert rows == lib.mi_panel_stat_rows2(M, C, R * R * K, 1) > 0, "not routed to the panel kernel"
         sl = torch.full((rows + 8, 2, C), float("nan"), device="cuda") if stats else None
         dx = base.clone() if epi == 5 else torch.empty_like(base)
@@ -160,8 +160,8 @@ def test_panel_dgrad1x1(lib, shape, epi, mask, stats, flags):
         torch.cuda.synchronize()
         out[mode] = (dx, sl[:rows] if stats else None)
     lib.mi_set_nt_split_blocks(128)
-    lib.mi_set_panel(2)
-    dx_p, sl_p = out[2]
+    lib.mi_set_panel(6)
+    dx_p, sl_p = out[6]
     dx_o, sl_o = out[0]
     if epi == 3 and flags & 2:
         # epi 3 reads its residual at every pixel; the NaN-poisoned odd ones propagate alike

@@ -56,11 +56,11 @@ def main():
             return e0.elapsed_time(e1) / a.iters * 1e3
         tp, to = [], []
         for _ in range(a.rounds):
-            lib.mi_set_panel(1)
+            lib.mi_set_panel(5)
             tp.append(timed())
             lib.mi_set_panel(0)
             to.append(timed())
-        lib.mi_set_panel(1)
+        lib.mi_set_panel(5)
         return statistics.median(tp), statistics.median(to)
 
     for (C, H, K, s, R, cnt) in SHAPES:
@@ -78,7 +78,7 @@ def main():
                       P, 0, st)
 
         mp, mo = ab(run)
-        routed = lib.mi_panel_stat_rows(M, K, C * R * R) > 0
+        routed = lib.mi_panel_stat_rows(M, K, C * R * R) > 0  # (mode 5: 3x3 included)
         byts = (Nb * H * H * C if s == 1 else M * C) * 2 + M * K * 2
         tot_p += mp * cnt
         tot_o += mo * cnt
