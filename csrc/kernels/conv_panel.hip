@@ -68,7 +68,22 @@ struct PanelArgs {
   const bf16_t* aux2;
   const float* mean;
   const uint8_t* mbits;
+  // folded BatchNorm backward (EPI 1, khalf > 0): the consumer GEMM of a BN's
+  // input gradient dX = k0 dz + k1 c + k2 (per channel k) without materialising dX -- the A operand
+  // is [dz | c] along K (k-steps [0, khalf) read dz from A, [khalf, 2 khalf) read c from A2, same row
+  // geometry), the weight panel [diag(k0) W | diag(k1) W] is scaled in LDS from the bf16 W (row
+  // stride ldb, khalf k-steps) with coef = (k0, k1, k2) [3][64 khalf], and every accumulator starts
+  // at bias[n] = sum_k k2[k] W[n][k]
+  const bf16_t* A2;
+  int a2_bytes, khalf, ldb;
+  const float* coef;
+  const bf16_t* acc_src;  // epi 5: read the accumulated-into gradient from here instead of C (out of place)
 };
+
+__device__ __forceinline__ void pn_load8f(const float* __restrict__ p, float* o) {
+  *(float4*)&o[0] = *(const float4*)p;
+  *(float4*)&o[4] = *(const float4*)(p + 4);
+}
 
 #define PN_VMWAIT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
@@ -120,10 +135,13 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)a.C, (short)0, a.c_bytes, 0x00020000);
+  const int khalf = EPI == 1 ? a.khalf : 0;  // folded BN backward: k-steps per operand half
+  const __amdgpu_buffer_rsrc_t rsA2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(khalf ? a.A2 : a.A), (short)0, khalf ? a.a2_bytes : 0, 0x00020000);
   // EPI 1 operand resources (same layout as C; mbits: one byte per 8 channels)
   __amdgpu_buffer_rsrc_t rsY = rsC, rsX = rsC, rsK = rsC;
   if constexpr (EPI == 1) {
-    rsY = __builtin_amdgcn_make_buffer_rsrc((void*)(a.epi == 3 ? a.aux : a.C), (short)0,
+    rsY = __builtin_amdgcn_make_buffer_rsrc((void*)(a.epi == 3 ? a.aux : (a.acc_src ? a.acc_src : a.C)), (short)0,
                                             (a.epi == 3 || a.epi == 5) ? a.c_bytes : 0, 0x00020000);
     rsX = __builtin_amdgcn_make_buffer_rsrc((void*)a.aux2, (short)0, (a.epi >= 4 && a.stats) ? a.c_bytes : 0,
                                             0x00020000);
@@ -136,16 +154,64 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
   // c of row n holds logical chunk c ^ (n & 7))
   {
     constexpr int PPK = BN / 8;  // pieces per k-step
-    const int np = nk * PPK;
+    const int np = (khalf ? khalf : nk) * PPK;  // folded BN backward: the second half is computed below
     const int pr = lane >> 3, pc = lane & 7;
     for (int p = wid; p < np; p += 8) {
       const int kt = p / PPK, r8 = p - kt * PPK;
       const int n = n0 + r8 * 8 + pr;
-      const uint32_t vo = n < a.N ? (uint32_t)(n * a.K + kt * 64 + ((pc ^ pr) * 8)) * 2u : PN_OOB;
+      const uint32_t vo = n < a.N ? (uint32_t)(n * a.ldb + kt * 64 + ((pc ^ pr) * 8)) * 2u : PN_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, LDS_PTR(void, bpanel + (kt * BN + r8 * 8) * 8), 16, vo, 0, 0, 0);
     }
     PN_VMWAIT(0);
     __syncthreads();
+  }
+  // folded BN backward: W -> [diag(k0) W | diag(k1) W] in place (chunk position c of panel row n holds
+  // channels 8 (c ^ (n & 7)) of its k-step) and bias[n] = sum_k k2[k] W[n][k], reduced over the TPN
+  // threads of a column through the (still unused) ring area; every lane keeps the biases of its
+  // accumulator columns n = 16 j + 4 fq + r of the wave tile in registers
+  float bias_r[WN / 16][4];
+#pragma unroll
+  for (int j = 0; j < WN / 16; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias_r[j][r] = 0.f;
+  if (khalf) {
+    constexpr int TPN = 512 / BN;  // threads per panel column
+    const int n = tid % BN, tq = tid / BN;
+    const int kh = khalf * 64;
+    float bs = 0.f;
+    for (int kt = 0; kt < khalf; ++kt) {
+      for (int c = tq; c < 8; c += TPN) {
+        uint4* pw = bpanel + (kt * BN + n) * 8 + c;
+        const int ch = kt * 64 + ((c ^ (n & 7)) * 8);
+        float w[8], k0[8], k1[8], k2[8], u0[8], u1[8];
+        unpack8(*pw, w);
+        pn_load8f(a.coef + ch, k0);
+        pn_load8f(a.coef + kh + ch, k1);
+        pn_load8f(a.coef + 2 * kh + ch, k2);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          u0[q] = w[q] * k0[q];
+          u1[q] = w[q] * k1[q];
+          bs = fmaf(w[q], k2[q], bs);
+        }
+        *pw = pack8(u0);
+        bpanel[((kt + khalf) * BN + n) * 8 + c] = pack8(u1);
+      }
+    }
+    float* red = (float*)smem;  // [TPN][BN] partial sums, then [BN] biases
+    red[tq * BN + n] = bs;
+    __syncthreads();
+    if (tq == 0) {
+      float t = 0.f;
+      for (int q = 0; q < TPN; ++q) t += red[q * BN + n];
+      red[TPN * BN + n] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < WN / 16; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias_r[j][r] = red[TPN * BN + wn * WN + 16 * j + 4 * fq + r];
+    __syncthreads();  // the ring's first loads overwrite the reduction area
   }
 
   // ---- this wave's 32-row units: a balanced contiguous range over the panel's wave slots
@@ -200,10 +266,24 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
       }
     } else {
+      // folded BN backward: the second half of the k-steps reads c (A2) at the same rows
+      // (readfirstlane: the operand choice must be provably wave-uniform, or the descriptor select
+      // becomes a waterfall loop with a vmcnt(0) in it)
+      const int iktu = __builtin_amdgcn_readfirstlane(ikt);
+      if (khalf && iktu >= khalf) {  // a branch, not a descriptor select (that one went to scratch)
+        const uint32_t kb = (uint32_t)(iktu - khalf) * 128u;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t vo = iok[u] ? ioff[u] + (uint32_t)ikt * 128u : PN_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t vo = iok[u] ? ioff[u] + kb : PN_OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA2, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
+        }
+      } else {
+        const uint32_t kb = (uint32_t)iktu * 128u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t vo = iok[u] ? ioff[u] + kb : PN_OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + u * 64), 16, vo, 0, 0, 0);
+        }
       }
     }
     if (++ikt == nk) {
@@ -214,10 +294,14 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
   };
 
   f32x4 acc[2][NJ];
+  // accumulators start at the folded BN backward's bias (0 otherwise)
+  auto acc_reset = [&]() {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{bias_r[j][0], bias_r[j][1], bias_r[j][2], bias_r[j][3]};
+  };
+  acc_reset();
   // epilogue layout: the unit's bf16 tile is staged in the ring slot it consumed and read back one
   // 16-byte row chunk per lane: lane chunk ec (8 channels) of rows er + RPI u
   constexpr int CPR = WN / 8;     // 16-B chunks per staged row
@@ -365,18 +449,20 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
           if (want_stats) {
             float xv[8];
             unpack8(ex[k], xv);
+            const bool live = m < a.M;  // rows past M hold the folded bias when unmasked
 #pragma unroll
-            for (int q = 0; q < 8; ++q) { s1[q] += f[q]; s2[q] = fmaf(f[q], xv[q] - mu[q], s2[q]); }
+            for (int q = 0; q < 8; ++q) {
+              const float fz = live ? f[q] : 0.f;
+              s1[q] += fz;
+              s2[q] = fmaf(fz, xv[q] - mu[q], s2[q]);
+            }
           }
         }
         const uint32_t off = (m < a.M && ncol < a.N) ? (uint32_t)(m * a.ldc + ncol) * 2u : PN_OOB;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsC, off, 0, 0);
       }
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc_reset();
   };
 
   // ---- main loop over the wave's k-steps
@@ -497,6 +583,7 @@ template <int EPI>
 int launch_plan(const PanelPlan& p, PanelArgs& a, hipStream_t st, const char* what) {
   a.npanel = p.npanel;
   a.nunits = cdiv(a.M, 32);
+  if (!a.ldb) a.ldb = a.K;
   const int grid = p.npanel * p.nb;
   if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
     fprintf(stderr, "[gemm] panel-%s %d/%d s%d M=%d N=%d K=%d epi=%d stats=%d blocks=%d\n", what, p.bn, p.wn, p.s, a.M,
@@ -567,10 +654,11 @@ MI_API int mi_panel_conv1x1(const void* x, const void* w, void* y, float* stats,
 
 // 1x1 or 3x3 (pad 1) / stride-1 conv data gradient on the panel kernel: dy NHWC [Nb,H,W,K], wt [C][R][R][K], dx NHWC
 // [Nb,H,W,C] with nt_kernel's epilogues (PanelArgs::epi; mbits or aux = the BN output for the ReLU
-// mask; stats [mi_panel_stat_rows2(.., 1)][2][C]).  hipErrorNotSupported: not eligible.
+// mask; stats [mi_panel_stat_rows2(.., 1)][2][C]; epi 5 with acc_src: accumulate acc_src into dx out of
+// place).  hipErrorNotSupported: not eligible.
 MI_API int mi_panel_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                           int epi, const void* aux, const void* aux2, const float* mean, int bn_relu, float* stats,
-                          int aux_even, const void* mbits, hipStream_t st) {
+                          int aux_even, const void* mbits, const void* acc_src, hipStream_t st) {
   const int M = Nb * H * W;
   if ((R != 1 && R != 3) || K % 64 != 0) return (int)hipErrorNotSupported;
   const PanelPlan p = panel_plan(M, C, R * R * K, true);
@@ -589,5 +677,47 @@ MI_API int mi_panel_dgrad(const void* dy, const void* wt, void* dx, int Nb, int 
   a.fQ = make_fastdiv((uint32_t)W);
   a.epi = epi; a.bn_relu = epi >= 4 ? bn_relu : 0; a.aux_even = (epi == 3 || epi == 5) ? aux_even : 0;
   a.aux = (const bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.mbits = (const uint8_t*)mbits;
+  a.acc_src = epi == 5 ? (const bf16_t*)acc_src : nullptr;
   return launch_plan<1>(p, a, st, R == 3 ? "dgrad3x3" : "dgrad");
+}
+
+// Folded BatchNorm backward into a 1x1 / stride-1 data gradient: the gradient
+// of the conv's input, dx = dgrad(k0 dz + k1 c + k2) with the BN of THIS conv's output (c, its
+// masked output gradient dz, coef = (k0, k1, k2) [3][K] from the BN-backward finalize), computed as
+// one GEMM over [dz | c] (2K deep) against [diag(k0) W | diag(k1) W] plus a per-column bias, so the
+// BN's input gradient is never written or read.  wt [C][K] (bf16, the dgrad weight layout); the
+// epilogues and statistics are mi_panel_dgrad's (epi 5 may accumulate out of place: acc_src, the
+// gradient added to, and dx, the result, may differ).  hipErrorNotSupported: not eligible.
+MI_API int mi_panel_dgrad_fbb(const void* dz, const void* c, const float* coef, const void* wt, void* dx, int Nb, int H,
+                              int W, int C, int K, int epi, const void* aux, const void* aux2, const float* mean,
+                              int bn_relu, float* stats, int aux_even, const void* mbits, const void* acc_src,
+                              hipStream_t st) {
+  const int M = Nb * H * W;
+  if (K % 64 != 0 || !coef || !(epi == 0 || epi == 3 || epi == 4 || epi == 5)) return (int)hipErrorNotSupported;
+  const PanelPlan p = panel_plan(M, C, 2 * K, true);
+  if (!p.bn) return (int)hipErrorNotSupported;
+  const int64_t ab = (int64_t)M * K * 2, cb = (int64_t)M * C * 2, bb = (int64_t)C * K * 2;
+  if (ab > 0x7FFFFFF0LL || cb > 0x7FFFFFF0LL || bb > 0x7FFFFFF0LL) return (int)hipErrorNotSupported;
+  PanelArgs a{};
+  a.A = (const bf16_t*)dz; a.A2 = (const bf16_t*)c; a.B = (const bf16_t*)wt; a.C = (bf16_t*)dx;
+  a.coef = coef;
+  a.stats = epi >= 4 ? stats : nullptr;
+  a.M = M; a.N = C; a.K = 2 * K; a.ldc = C; a.ldb = K;
+  a.nk = a.K / 64; a.khalf = K / 64;
+  a.a_bytes = (int)ab; a.a2_bytes = (int)ab; a.b_bytes = (int)bb; a.c_bytes = (int)cb;
+  a.gather = 0; a.lda = K; a.H = H; a.W = W; a.stride = 1;
+  a.tsg = -1; a.cpt = K / 64;
+  a.fPQ = make_fastdiv((uint32_t)(H * W));
+  a.fQ = make_fastdiv((uint32_t)W);
+  a.epi = epi; a.bn_relu = epi >= 4 ? bn_relu : 0; a.aux_even = (epi == 3 || epi == 5) ? aux_even : 0;
+  a.aux = (const bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.mbits = (const uint8_t*)mbits;
+  a.acc_src = epi == 5 ? (const bf16_t*)acc_src : nullptr;
+  return launch_plan<1>(p, a, st, "dgrad-fbb");
+}
+
+// statistics rows of mi_panel_dgrad_fbb (M rows, C output channels, K = channels of dz / c); 0: the
+// folded path does not take the shape
+MI_API int mi_panel_fbb_rows(int M, int C, int K) {
+  if (K % 64 != 0) return 0;
+  return mi_panel_stat_rows2(M, C, 2 * K, 1);
 }

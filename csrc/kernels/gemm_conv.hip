@@ -120,6 +120,12 @@ struct TNArgs {
   const float* nol_scale;
   const float* nol_shift;
   ConvGeom g;
+  // folded BN backward (conv_panel.hip mi_panel_dgrad_fbb's weight-gradient twin): A is [dz | c] along
+  // M -- rows m >= msplit read A2 at m - msplit (msplit a multiple of BM: the choice is per block) --
+  // and the CSB variant writes the column sums of B over each split's k-range to bsum[split][N]
+  const bf16_t* A2;
+  int a2_bytes, msplit, lda2;
+  float* bsum;
 };
 
 constexpr int BK = 64;
@@ -822,9 +828,10 @@ __device__ __forceinline__ int tr_swz(int k) {
 // fused bias-gradient column sums (Linear layers only).  Both are compile-time so that neither the
 // gather bookkeeping nor the colsum accumulators occupy registers in the variants that do not use
 // them (the conv variant fits 128 VGPRs and runs 4 blocks per CU).
-template <int BM, int BN, int STAGES, int MODE = 1, bool CS = false, bool NOL = false>
+template <int BM, int BN, int STAGES, int MODE = 1, bool CS = false, bool NOL = false, bool CSB = false>
 __global__ __launch_bounds__(256, STAGES == 1 ? (MODE == 1 && !CS ? kTnConvBlocksPerCu : kTnBlocksPerCu) : 2)
 void tn_kernel(TNArgs a) {
+  static_assert(!CSB || (STAGES == 1 && !CS && !NOL), "folded BN backward: the plain one-stage variant");
   static_assert(!NOL || (MODE == 1 && STAGES == 1 && !CS), "normalize-on-load: conv weight gradients");
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
@@ -899,10 +906,14 @@ void tn_kernel(TNArgs a) {
   // per-step carry deltas for +BK pixels
   const int dq = BK % Q, dp = (BK / Q) % P, dimg = BK / (P * Q);
 
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
+  // folded BN backward: a block's rows lie wholly in dz (A) or in c (A2, rows m - msplit)
+  const bool a_second = CSB && a.msplit && m0 >= a.msplit;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a_second ? a.A2 : a.A), (short)0, a_second ? a.a2_bytes : a.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
   constexpr uint32_t OOB = 0xFFFFFFF0u;
   const int a_m = m0 + a_lc * 8;
+  const int a_mo = a_second ? a_m - a.msplit : a_m;  // row within the operand read
   const int b_n = n0 + b_lc * 8;
 
   uint32_t b_okm = 0;  // NOL: B chunks of the last issued k-step that hold real input pixels
@@ -912,7 +923,7 @@ void tn_kernel(TNArgs a) {
     for (int i = 0; i < A_CH; ++i) {
       const int k = k0 + a_r + A_RSTEP * i;
       const bool ok = k < kend && a_m < a.M;
-      const uint32_t vo = ok ? (uint32_t)(k * a.lda + a_m) * 2u : OOB;
+      const uint32_t vo = ok ? (uint32_t)(k * (a_second ? a.lda2 : a.lda) + a_mo) * 2u : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsA, LDS_PTR(void, &As[(buf * BK + A_RSTEP * i + wid * A_RPI) * AU]), 16, vo, 0, 0, 0);
     }
@@ -954,6 +965,11 @@ void tn_kernel(TNArgs a) {
   short ones_s __attribute__((ext_vector_type(8))) = {0x3F80, 0x3F80, 0x3F80, 0x3F80,
                                                       0x3F80, 0x3F80, 0x3F80, 0x3F80};
   const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_s);
+  // folded BN backward: the column sums of B (every row of ones x B holds them), first row-tile only
+  const bool do_csb = CSB && tile / nbn == 0 && wm == 0;
+  f32x4 acc_sb[CSB ? NJ : 1];
+#pragma unroll
+  for (int j = 0; j < (CSB ? NJ : 1); ++j) acc_sb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -985,6 +1001,11 @@ void tn_kernel(TNArgs a) {
         if (do_cs)
 #pragma unroll
         for (int i = 0; i < MI; ++i) acc_cs[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, acc_cs[i], 0, 0, 0);
+      }
+      if constexpr (CSB) {
+        if (do_csb)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc_sb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[j], acc_sb[j], 0, 0, 0);
       }
     }
   };
@@ -1033,6 +1054,15 @@ void tn_kernel(TNArgs a) {
         const int m = m0 + wm * WM + 16 * i + 4 * g + r;
         if (m < a.M) atomicAdd(a.colsum + m, acc_cs[i][r]);
       }
+  }
+
+  // folded BN backward: this split's column sums of B (lane g == 0 holds row 0 of ones x B)
+  if constexpr (CSB) if (do_csb && g == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * WN + 16 * j + li;
+      if (n < a.N) a.bsum[(size_t)split * a.N + n] = acc_sb[j][0];
+    }
   }
 
   // epilogue: lane holds D[m = 16i + 4g + r][n = 16j + li]
@@ -1589,6 +1619,8 @@ hipError_t launch_tn(TNArgs& a, hipStream_t st, int target_blocks) {
   if (a.nol_scale) {
     if (a.mode != 1 || st_n != 1 || a.cnt) return hipErrorNotSupported;
     hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false, true>), dim3(tiles * splits), dim3(256), 0, st, a);
+  } else if (a.mode == 1 && a.bsum) {  // folded BN backward (mi_conv2d_wgrad_fbb)
+    hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false, false, true>), dim3(tiles * splits), dim3(256), 0, st, a);
   } else if (a.mode == 1) {
     if (st_n == 1) hipLaunchKernelGGL((tn_kernel<BM, BN, 1, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((tn_kernel<BM, BN, 2, 1, false>), dim3(tiles * splits), dim3(256), 0, st, a);
@@ -1753,7 +1785,7 @@ extern "C" int mi_panel_stat_rows(int M, int N, int K);
 extern "C" int mi_panel_stat_rows2(int M, int N, int K, int dgrad);
 extern "C" int mi_panel_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                               int epi, const void* aux, const void* aux2, const float* mean, int bn_relu, float* stats,
-                              int aux_even, const void* mbits, hipStream_t st);
+                              int aux_even, const void* mbits, const void* acc_src, hipStream_t st);
 extern "C" int mi_panel_conv(const void* x, const void* w, void* y, float* stats, int Nb, int H, int W, int C, int K,
                              int R, int stride, int pad, int P, int Q, hipStream_t st);
 // a 1x1 or 3x3 (pad 1) stride-1 data gradient runs on the panel kernel (the statistics slab rows it
@@ -1849,7 +1881,7 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
     return mi_gemm256_conv(2, dy, wt, dx, nullptr, 0, nullptr, nullptr, nullptr, 0, Nb, P, Q, K, H, W, R, S, 1, pad, C,
                            st);
   if (R == S && pad == (R == 3 ? 1 : 0) && panel_rows_dgrad(Nb * H * W, C, K, R * S, stride) > 0)
-    return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, st);
+    return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, st);
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
   a.M = Nb * H * W; a.N = C; a.K = R * S * K;
@@ -1962,7 +1994,8 @@ MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb,
                             bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, mbits, st);
   if (R == S && pad == (R == 3 ? 1 : 0) && panel_rows_dgrad(Nb * H * W, C, K, R * S, stride) > 0) {
     if (mask_c) return (int)hipErrorNotSupported;  // mi_conv_nol_ok keeps these shapes materialised
-    return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, epi, aux, aux2, mean, bn_relu, stats, aux_even, mbits, st);
+    return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, epi, aux, aux2, mean, bn_relu, stats, aux_even, mbits,
+                          nullptr, st);
   }
   NTArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)wt; a.C = dx; a.bias = nullptr;
@@ -2008,6 +2041,91 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
   a.b_bytes = rsrc_bytes((int64_t)Nb * H * W * C);
   a.g = make_geom(H, W, C, P, Q, S, stride, pad, R);
   return (int)dispatch_tn(a, st);
+}
+
+// ---- folded BatchNorm backward, weight-gradient side (conv_panel.hip mi_panel_dgrad_fbb): the weight
+// gradient of a 1x1 / stride-1 conv against its output's BN input gradient dX = k0 dz + k1 c + k2 (per
+// output channel k) without dX.  With c = x W^T, c^T x = W (x^T x), so
+//   dW[k][n] += k0[k] (dz^T x)[k][n] + k1[k] (W G)[k][n] + k2[k] s[n],   G = x^T x, s = colsum(x):
+// ONE TN GEMM of [dz | x] (K + C rows: the conv input x is read a second time instead of the K-wide c)
+// against x, the column sums of x per split (bsum), and a small combine in split order
+// (deterministic).  ws: fp32 [K + C + FBB_MAX_SPLITS][C], zero on entry -- the combine re-zeroes it.
+constexpr int FBB_MAX_SPLITS = 1024;
+
+__global__ __launch_bounds__(256) void fbb_wgrad_combine_kernel(float* __restrict__ T, const float* __restrict__ bsum,
+                                                                int nsplit, const float* __restrict__ coef,
+                                                                const bf16_t* __restrict__ w, float* __restrict__ dw,
+                                                                int K, int C) {
+  // one output channel k per block; T rows [0, K): dz^T x, [K, K + C): G.  Thread t: column
+  // n = t % C (+ 256 strides for C > 256), reduction part t / C of PT = 256 / C parts (split sums of s
+  // and the j terms of (W G)[k][n]), combined through LDS in a fixed order
+  __shared__ float red[2][256];
+  const int k = blockIdx.x;
+  const int PT = C < 256 ? 256 / C : 1;
+  const int part = threadIdx.x / (C < 256 ? C : 256), n0 = threadIdx.x % (C < 256 ? C : 256);
+  const float k0 = coef[k], k1 = coef[K + k], k2 = coef[2 * K + k];
+  const float* G = T + (size_t)K * C;
+  for (int nb = 0; nb < C; nb += 256) {
+    const int n = nb + n0;
+    float sn = 0.f, wg = 0.f;
+    if (part < PT && n < C) {
+      for (int z = part; z < nsplit; z += PT) sn += bsum[(size_t)z * C + n];
+      for (int j = part; j < C; j += PT) wg = fmaf(bf2f(w[(size_t)k * C + j]), G[(size_t)j * C + n], wg);
+    }
+    red[0][threadIdx.x] = sn;
+    red[1][threadIdx.x] = wg;
+    __syncthreads();
+    if (part == 0 && n < C) {
+      for (int q = 1; q < PT; ++q) {
+        sn += red[0][q * (C < 256 ? C : 256) + n0];
+        wg += red[1][q * (C < 256 ? C : 256) + n0];
+      }
+      dw[(size_t)k * C + n] += k0 * T[(size_t)k * C + n] + k1 * wg + k2 * sn;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void fbb_ws_zero_kernel(float* __restrict__ T, int64_t n) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) T[i] = 0.f;
+}
+
+MI_API int mi_conv2d_wgrad_fbb_ws_floats(int K, int C) { return (K + C + FBB_MAX_SPLITS) * C; }
+
+// x NHWC [Nb,H,W,C] (the 1x1 conv's input), dz NHWC [Nb,H,W,K], w bf16 [K][C] (its forward weights),
+// dw fp32 [K][C] (+=), ws: mi_conv2d_wgrad_fbb_ws_floats(K, C) floats, zero.  hipErrorNotSupported:
+// not eligible (the caller keeps the materialised path)
+MI_API int mi_conv2d_wgrad_fbb(const void* x, const void* dz, const void* w, const float* coef, float* dw, float* ws,
+                               int Nb, int H, int W, int C, int K, hipStream_t st) {
+  if (C % 64 != 0 || K % 64 != 0 || !coef || !ws || !w) return (int)hipErrorInvalidValue;
+  const int M2 = K + C, M = Nb * H * W;
+  TNArgs a{};
+  a.A = (const bf16_t*)dz; a.A2 = (const bf16_t*)x; a.B = (const bf16_t*)x; a.C = ws;
+  a.M = M2; a.N = C; a.K = M;
+  a.lda = K; a.lda2 = C; a.ldb = 0; a.ldc = C; a.mode = 1;
+  a.msplit = K;
+  a.a_bytes = rsrc_bytes((int64_t)M * K);
+  a.a2_bytes = a.b_bytes = rsrc_bytes((int64_t)M * C);
+  a.bsum = ws + (size_t)M2 * C;
+  a.g = make_geom(H, W, C, H, W, 1, 1, 0, 1);
+  // the dz / x parts must not share a row tile: BM divides K
+  const int target = tn_target_blocks(st);
+  const bool m128 = K % 128 == 0, n64 = C <= 64;
+  const int BMc = m128 ? 128 : 64, BNc = n64 ? 64 : 128;
+  const int tiles = cdiv(M2, BMc) * cdiv(C, BNc), ksteps = cdiv(M, BK);
+  const int splits0 = std::max(1, std::min(ksteps, target / std::max(tiles, 1)));
+  const int splits = cdiv(M, cdiv(ksteps, splits0) * BK);
+  if (splits > FBB_MAX_SPLITS) return (int)hipErrorNotSupported;
+  hipError_t e;
+  if (m128) e = n64 ? launch_tn<128, 64>(a, st, target) : launch_tn<128, 128>(a, st, target);
+  else e = n64 ? launch_tn<64, 64>(a, st, target) : launch_tn<64, 128>(a, st, target);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(fbb_wgrad_combine_kernel, dim3(K), dim3(256), 0, st, ws, (const float*)a.bsum, splits, coef,
+                     (const bf16_t*)w, dw, K, C);
+  const int64_t nz = (int64_t)M2 * C;
+  hipLaunchKernelGGL(fbb_ws_zero_kernel, dim3((unsigned)std::min<int64_t>(cdiv(nz, 256), 1024)), dim3(256), 0, st, ws,
+                     nz);
+  return (int)hipGetLastError();
 }
 
 // ---- normalize-on-load (the consumer conv applies the producing BatchNorm + ReLU to its raw input c)

@@ -1482,6 +1482,17 @@ MI_API int mi_bn_bwd_train_pre(const void* dz, const void* x, void* dx, void* dr
   return (int)hipGetLastError();
 }
 
+// the finalize of mi_bn_bwd_train_pre alone: dgamma / dbeta (+=) and coef = (k0, k1, k2) [3][C] of
+// dx = k0 dz + k1 x + k2, for a consumer that folds the BN backward into its GEMM instead of
+// reading a materialised dx (conv_panel.hip mi_panel_dgrad_fbb, gemm_conv.hip mi_conv2d_wgrad_fbb)
+MI_API int mi_bn_bwd_coef(int M, int C, const float* gamma, const float* save_mean, const float* save_invstd,
+                          float* dgamma, float* dbeta, float* coef, float* part, int pre_rows, hipStream_t st) {
+  if (C % 8 != 0 || pre_rows <= 0 || !coef) return (int)hipErrorInvalidValue;
+  const FinArgs fb = fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  slab_finalize<true>(part, pre_rows, fb, st);
+  return (int)hipGetLastError();
+}
+
 MI_API int mi_bn_bwd_eval(const void* dy, const void* y, const float* scale, void* dx, void* dres, int M, int C,
                           int relu, hipStream_t st) {
   int64_t nvec = (int64_t)M * C / 8;

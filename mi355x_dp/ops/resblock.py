@@ -251,6 +251,12 @@ def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev, mask=None, bits=None):
     the mask as bytes of 8 channel bits (_out_apply) instead of reading ``y_prev``."""
     N, C, H, W = c_prev.shape
     lib = _lib.load()
+    if isinstance(dy, _Fold):  # the output BN's input gradient folded into this data gradient
+        rows = lib.mi_panel_fbb_rows(N * H * W, C, spec.w.shape[0])
+        slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dy.dz.device)
+        dz = torch.empty_like(c_prev, memory_format=CL)
+        _dgrad_fold(dy, spec, c_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab, mbits=bits)
+        return dz, slab, rows
     rows = lib.mi_dgrad_stat_rows(N, H, W, C, dy.shape[2], dy.shape[3], spec.stride, spec.w.shape[0],
                                  spec.w.shape[2] * spec.w.shape[3])
     slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dy.device)
@@ -293,6 +299,115 @@ def _bn_bwd_pre(dz, c, bn, mean, invstd, slab, rows):
     _lib.call("mi_bn_bwd_train_pre", ptr(dz), ptr(c), ptr(dc), ptr(None), N * H * W, C, ptr(bn.w), ptr(mean),
               ptr(invstd), ptr(gw), ptr(gb), ptr(coef), ptr(slab), int(rows), stream_of(c))
     return dc, _finish_grad(bn.w, gw), _finish_grad(bn.b, gb)
+
+
+# ------------------------------------------------------------- folded BN backward
+# A BatchNorm's input gradient dX = k0 dz + k1 c + k2 (per channel; dz the masked output gradient,
+# c the BN input) is consumed by exactly two GEMMs, the data and weight gradients of the conv that
+# produced c.  For a 1x1 / stride-1 conv both take it FOLDED instead of reading a materialised dX:
+#   dgrad(dX) = [dz | c] x [diag(k0) W | diag(k1) W] + bias(k2 W)   (conv_panel.hip mi_panel_dgrad_fbb)
+#   wgrad(dX) = k0 (dz^T x) + k1 (c^T x) + k2 colsum(x)             (gemm_conv.hip mi_conv2d_wgrad_fbb)
+# so the BN-backward apply pass (read dz, c; write dX) and both consumers' reads of dX become one
+# extra read of c per consumer.  MI355X_DP_BN_FOLD=0 restores the materialised path.
+BN_FOLD = os.environ.get("MI355X_DP_BN_FOLD", "1") != "0"
+_FBB_WS = {}  # (weight id, device) -> the folded weight gradient's fp32 workspace (zero between calls)
+FOLD_USED = [0]  # diagnostics: BN backwards taken folded
+
+
+class _Fold:
+    """a BN input gradient held unmaterialised: dX = k0 dz + k1 c + k2, coef = (k0, k1, k2) [3][C]"""
+    __slots__ = ("dz", "c", "coef")
+
+    def __init__(self, dz, c, coef):
+        self.dz, self.c, self.coef = dz, c, coef
+
+    @property
+    def shape(self):
+        return self.dz.shape
+
+
+def _fold_ok(spec, x_shape) -> bool:
+    """can conv ``spec`` (input shape ``x_shape``) take its output BN's input gradient folded?  Only
+    expansions (K > C: the bottleneck conv3s): the folded data gradient reads dz and c (2 K channels)
+    where the materialised path wrote and re-read dX, which pays when K is the wide side; for K < C
+    the doubled panel depth halves the panel width and the re-reads of [dz | c] per panel cost more
+    than the apply pass they replace (tools/bench_fold.py, profiles/bn_fold_r6.md)"""
+    if not BN_FOLD:
+        return False
+    K, C, R, S = spec.w.shape
+    if R != 1 or S != 1 or spec.stride != 1 or spec.pad != 0 or K % 64 or C % 64 or K <= C:
+        return False
+    N, _, H, W = x_shape
+    return _lib.load().mi_panel_fbb_rows(N * H * W, C, K) > 0
+
+
+def _bn_bwd_fold(dz, c, bn, mean, invstd, slab, rows):
+    """BN backward from dgrad-epilogue statistics, folded: the coefficients only (+ dgamma / dbeta)"""
+    N, C, H, W = c.shape
+    gw, gb = _grad_buffer(bn.w), _grad_buffer(bn.b)
+    coef = torch.empty((3, C), dtype=F32, device=c.device)
+    FOLD_USED[0] += 1
+    _lib.call("mi_bn_bwd_coef", N * H * W, C, ptr(bn.w), ptr(mean), ptr(invstd), ptr(gw), ptr(gb), ptr(coef),
+              ptr(slab), int(rows), stream_of(c))
+    return _Fold(dz, c, coef), _finish_grad(bn.w, gw), _finish_grad(bn.b, gb)
+
+
+def _wgrad_fold(x, fold, spec):
+    """_wgrad with the output BN's input gradient folded (mi_conv2d_wgrad_fbb)"""
+    N, C, H, W = x.shape
+    K, _, R, S = spec.w.shape
+    P, Q = fold.dz.shape[2], fold.dz.shape[3]
+    g = _grad_buffer(spec.w)
+    key = (id(spec.w), x.device.index)
+    nf = _lib.load().mi_conv2d_wgrad_fbb_ws_floats(K, C)
+    ws = _FBB_WS.get(key)
+    if ws is None or ws.numel() < nf:
+        ws = _FBB_WS[key] = torch.zeros(nf, dtype=F32, device=x.device)
+    w16 = weight_bf16(spec.w)  # [K][1][1][C]: c^T x = W (x^T x)
+
+    def launch():
+        _lib.call("mi_conv2d_wgrad_fbb", ptr(x), ptr(fold.dz), ptr(w16), ptr(fold.coef), ptr(g), ptr(ws), N, H, W, C,
+                  K, stream_of(fold.dz))
+    if _side(spec.w) is not None:
+        run_wgrad(spec.w, launch, (x, fold.dz, w16, fold.coef, ws))
+        return None
+    launch()
+    return _finish_grad(spec.w, g)
+
+
+def _dgrad_fold(fold, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None, relu=0, stats=None, flags=0,
+                mbits=None, acc_src=None):
+    """_dgrad with the output BN's input gradient folded (mi_panel_dgrad_fbb); epi 5 accumulates
+    ``acc_src`` (default: ``out`` itself) into ``out``"""
+    N, C, H, W = x_shape
+    K = spec.w.shape[0]
+    _lib.call("mi_panel_dgrad_fbb", ptr(fold.dz), ptr(fold.c), ptr(fold.coef), ptr(weight_bf16_t(spec.w)), ptr(out),
+              N, H, W, C, K, int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), (int(flags) >> 1) & 1,
+              ptr(mbits), ptr(acc_src), stream_of(fold.dz))
+    return out
+
+
+def _panel_oop_rows(spec, x_shape) -> int:
+    """statistics rows of conv ``spec``'s 1x1 data gradient run on the panel kernel with an
+    out-of-place accumulate (mi_panel_dgrad acc_src), 0 if it cannot"""
+    K, C, R, S = spec.w.shape
+    if R != 1 or S != 1 or spec.stride != 1 or spec.pad != 0 or K % 64:
+        return 0
+    N, _, H, W = x_shape
+    return _lib.load().mi_panel_stat_rows2(N * H * W, C, K, 1)
+
+
+def _dgrad_panel_oop(dy, spec, x_shape, out, acc_src, epi, aux2=None, mean=None, relu=0, stats=None, flags=0,
+                     mbits=None):
+    """conv1's accumulating data gradient on the panel kernel, reading the accumulated-into gradient
+    from ``acc_src`` and writing ``out`` (epi 3: acc_src rides in aux; epi 5: acc_src)"""
+    N, C, H, W = x_shape
+    K = spec.w.shape[0]
+    aux = acc_src if epi == EPI_ACCUM else None
+    _lib.call("mi_panel_dgrad", ptr(dy), ptr(weight_bf16_t(spec.w)), ptr(out), N, H, W, C, K, 1, int(epi), ptr(aux),
+              ptr(aux2), ptr(mean), int(relu), ptr(stats), (int(flags) >> 1) & 1, ptr(mbits),
+              ptr(acc_src if epi == EPI_ACCUM_BN_BWD else None), stream_of(dy))
+    return out
 
 
 # -------------------------------------------------------------------------- the block
@@ -405,13 +520,26 @@ class _ResBlock(torch.autograd.Function):
         if hand is not None and not (hand[2] == dout._version and hand[3] == cs[-1].data_ptr()
                                      and dout.is_contiguous(memory_format=CL)):
             hand = None
+        # folded BN backward (see _Fold): conv i takes bn i's input gradient folded when it is a
+        # 1x1 / stride-1 conv the panel kernel runs at the doubled depth (never with normalize-on-load)
+        in_shapes = [x.shape] + [c.shape for c in cs[:-1]]
+        fold = [not any(ctx.nol_flags) and _fold_ok(convs[i], in_shapes[i]) for i in range(n)]
+        acc_src = None  # conv1's epi-5 accumulate source when dx may not alias dout
         if hand is not None:
             HANDOFF_USED[0] += 1
             # dout is already dz3 (masked) with bn3's statistics computed by the next block: it IS
             # the residual-path gradient, so it doubles as dyd / the initial dx (no copy)
-            dc, gw, gb = _bn_bwd_pre(dout, cs[-1], bns[n - 1], ms[-1], invs[-1], hand[0], hand[1])
+            if fold[n - 1] and (has_ds or fold[0] or _panel_oop_rows(convs[0], x.shape) > 0):
+                # folded: conv3's weight gradient reads dout on the side stream, so with an identity
+                # shortcut conv1's data gradient must not accumulate into dout in place -- it reads
+                # dout (acc_src) and writes a fresh dx (on the panel kernel, folded or not)
+                dc, gw, gb = _bn_bwd_fold(dout, cs[-1], bns[n - 1], ms[-1], invs[-1], hand[0], hand[1])
+                if not has_ds:
+                    acc_src = dout
+            else:
+                dc, gw, gb = _bn_bwd_pre(dout, cs[-1], bns[n - 1], ms[-1], invs[-1], hand[0], hand[1])
             dyd = dout if has_ds else None
-            dx = torch.empty_like(x, memory_format=CL) if has_ds else dout
+            dx = torch.empty_like(x, memory_format=CL) if (has_ds or acc_src is not None) else dout
         else:
             dx = torch.empty_like(x, memory_format=CL)
             # last BN: relu + residual; dres -> dx (identity) or the downsample BN's output gradient
@@ -431,12 +559,21 @@ class _ResBlock(torch.autograd.Function):
         for i in range(n - 1, 0, -1):
             nol = nols[i - 1]
             inp = ys[i - 1] if nol is None else cs[i - 1]
-            grads[id(convs[i].w)] = _wgrad(inp, dc, convs[i], nol)
+            if isinstance(dc, _Fold):
+                grads[id(convs[i].w)] = _wgrad_fold(inp, dc, convs[i])
+            else:
+                grads[id(convs[i].w)] = _wgrad(inp, dc, convs[i], nol)
             dz, slab, rows = _dgrad_bn(dc, convs[i], ys[i - 1], cs[i - 1], ms[i - 1], mask=nol,
                                        bits=ctx.inner_bits[i - 1])
-            dc, gw, gb = _bn_bwd_pre(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
+            if fold[i - 1]:
+                dc, gw, gb = _bn_bwd_fold(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
+            else:
+                dc, gw, gb = _bn_bwd_pre(dz, cs[i - 1], bns[i - 1], ms[i - 1], invs[i - 1], slab, rows)
             grads[id(bns[i - 1].w)], grads[id(bns[i - 1].b)] = gw, gb
-        grads[id(convs[0].w)] = _wgrad(x, dc, convs[0])
+        if isinstance(dc, _Fold):
+            grads[id(convs[0].w)] = _wgrad_fold(x, dc, convs[0])
+        else:
+            grads[id(convs[0].w)] = _wgrad(x, dc, convs[0])
         if aux is not None:
             main.wait_stream(aux)  # conv1's dgrad accumulates into the shortcut's dx
             gw, gb = dsd
@@ -451,10 +588,26 @@ class _ResBlock(torch.autograd.Function):
             lib = _lib.load()
             rows = lib.mi_dgrad_stat_rows(N, H, W, C, dc.shape[2], dc.shape[3], convs[0].stride,
                                           convs[0].w.shape[0], convs[0].w.shape[2] * convs[0].w.shape[3])
+            if isinstance(dc, _Fold):
+                rows = lib.mi_panel_fbb_rows(N * H * W, C, convs[0].w.shape[0])
+            elif acc_src is not None:
+                rows = _panel_oop_rows(convs[0], x.shape)
             slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dx.device)
-            _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab, flags=acc_flags,
-                   mbits=bits_prev)
+            if isinstance(dc, _Fold):
+                _dgrad_fold(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab, flags=acc_flags,
+                            mbits=bits_prev, acc_src=acc_src)
+            elif acc_src is not None:
+                _dgrad_panel_oop(dc, convs[0], x.shape, dx, acc_src, EPI_ACCUM_BN_BWD, c_prev, m_prev, 1, slab,
+                                 flags=acc_flags, mbits=bits_prev)
+            else:
+                _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM_BN_BWD, x, c_prev, m_prev, 1, slab, flags=acc_flags,
+                       mbits=bits_prev)
             _HANDOFF[(dx.data_ptr(), dx.device.index)] = (slab, rows, dx._version, c_prev.data_ptr())
+        elif isinstance(dc, _Fold):
+            # dx += dgrad_1 (epi 3 reads the accumulated-into gradient from aux)
+            _dgrad_fold(dc, convs[0], x.shape, dx, EPI_ACCUM, acc_src if acc_src is not None else dx, flags=acc_flags)
+        elif acc_src is not None:
+            _dgrad_panel_oop(dc, convs[0], x.shape, dx, acc_src, EPI_ACCUM, flags=acc_flags)
         else:
             _dgrad(dc, convs[0], x.shape, dx, EPI_ACCUM, dx, flags=acc_flags)   # dx += dgrad_1
         ctx.prev_bnsrc = None

@@ -175,3 +175,100 @@ def test_panel_dgrad1x1(lib, shape, epi, mask, stats, flags):
         assert torch.isfinite(sl_p).all(), "statistics rows left unwritten"
         for k in (0, 1):
             assert rel_err(sl_p[:, k].sum(0), sl_o[:, k].sum(0)) < 1e-4
+
+
+# folded BN backward: (N, H, C = dx channels, K = dz / c channels)
+FBB_SHAPES = [(4, 56, 64, 256), (4, 56, 256, 64), (4, 28, 512, 128), (3, 14, 1024, 256), (2, 13, 64, 64)]
+
+
+def _fbb_inputs(N, H, C, K, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    dz = torch.randn(N, K, H, H, device="cuda", generator=g).to(BF).contiguous(memory_format=CL)
+    c = (torch.randn(N, K, H, H, device="cuda", generator=g) * 2 + 0.3).to(BF).contiguous(memory_format=CL)
+    coef = torch.stack([torch.rand(K, device="cuda", generator=g) + 0.5,
+                        torch.randn(K, device="cuda", generator=g) * 0.1,
+                        torch.randn(K, device="cuda", generator=g) * 0.1]).contiguous()
+    w = (torch.randn(K, C, 1, 1, device="cuda", generator=g) * (1.0 / K) ** 0.5).to(BF).contiguous(memory_format=CL)
+    dX = dz.float() * coef[0].view(1, K, 1, 1) + c.float() * coef[1].view(1, K, 1, 1) + coef[2].view(1, K, 1, 1)
+    return dz, c, coef, w, dX
+
+
+@pytest.mark.parametrize("epi", [0, 4, 5])
+@pytest.mark.parametrize("shape", FBB_SHAPES)
+def test_panel_dgrad_fbb(lib, shape, epi):
+    """the 1x1 data gradient of a BN's input gradient folded into the GEMM ([dz | c] against
+    [diag(k0) W | diag(k1) W] plus the k2 bias) against fp32 math on the materialised dX, with the
+    BN-backward epilogue of the conv's own input BN (mask bytes + statistics) and the residual
+    accumulate (epi 5, in place and out of place)"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    N, H, C, K = shape
+    M = N * H * H
+    dz, c, coef, w, dX = _fbb_inputs(N, H, C, K, 7)
+    wt = torch.empty(C, 1, 1, K, dtype=BF, device="cuda")
+    st = stream_of(dz)
+    _lib.call("mi_conv_wtrans", ptr(w), ptr(wt), K, 1, C, st)
+    lib.mi_set_panel(6)
+    try:
+        rows = lib.mi_panel_fbb_rows(M, C, K)
+        if rows <= 0:
+            pytest.skip("not eligible for the folded path (panel depth)")
+        ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float(), dX, 1, 0)  # fp32 dgrad of the materialised dX
+        base = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+        yb = torch.relu(torch.randn(N, C, H, H, device="cuda")).to(BF).contiguous(memory_format=CL)
+        ybits = (yb.permute(0, 2, 3, 1).reshape(M, C // 8, 8) > 0).to(torch.int32)
+        bits = (ybits << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
+        xin = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+        mean = torch.randn(C, device="cuda") * 0.1
+        mask = (yb > 0).float()
+        outs = []
+        for oop in ((False, True) if epi == 5 else (False,)):
+            dx = base.clone() if (epi == 5 and not oop) else torch.empty_like(base)
+            sl = torch.full((rows + 8, 2, C), float("nan"), device="cuda") if epi >= 4 else None
+            _lib.call("mi_panel_dgrad_fbb", ptr(dz), ptr(c), ptr(coef), ptr(wt), ptr(dx), N, H, H, C, K, epi, ptr(None),
+                      ptr(xin), ptr(mean), 1, ptr(sl), 0, ptr(bits if epi >= 4 else None), ptr(base if oop else None),
+                      st)
+            torch.cuda.synchronize()
+            outs.append(dx)
+            if epi == 0:
+                want = ref
+            elif epi == 4:
+                want = ref.to(BF).float() * mask
+            else:
+                want = (ref.to(BF).float() + base.float()) * mask
+            assert rel_err(dx, want) < 2e-2, (oop, rel_err(dx, want))
+            if epi >= 4:
+                assert torch.isfinite(sl[:rows]).all()
+                wf = want.permute(0, 2, 3, 1).reshape(M, C)
+                xf = xin.float().permute(0, 2, 3, 1).reshape(M, C)
+                assert rel_err(sl[:rows, 0].sum(0), wf.sum(0)) < 3e-2
+                assert rel_err(sl[:rows, 1].sum(0), (wf * (xf - mean)).sum(0)) < 3e-2
+        if len(outs) == 2:
+            assert torch.equal(outs[0], outs[1])  # out of place == in place
+    finally:
+        lib.mi_set_panel(1)
+
+
+@pytest.mark.parametrize("shape", FBB_SHAPES)
+def test_wgrad_fbb(lib, shape):
+    """the weight gradient of a 1x1 conv against its output BN's input gradient, folded:
+    k0 (dz^T x) + k1 W (x^T x) + k2 colsum(x) (c = x W^T, so c^T x = W G) from ONE TN GEMM over
+    [dz | x] with the input's column sums per split, against fp32 math on the materialised dX from the
+    stored bf16 c; accumulates into dW; leaves its workspace zeroed for the next call"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    N, H, C, K = shape
+    dz, _, coef, w, _ = _fbb_inputs(N, H, C, K, 9)
+    x = torch.relu(torch.randn(N, C, H, H, device="cuda")).to(BF).contiguous(memory_format=CL)
+    c = F.conv2d(x.float(), w.float()).to(BF)  # the forward conv's stored output
+    dX = dz.float() * coef[0].view(1, K, 1, 1) + c.float() * coef[1].view(1, K, 1, 1) + coef[2].view(1, K, 1, 1)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, 1, 1), dX, 1, 0).permute(0, 2, 3, 1).contiguous()
+    ws = torch.zeros(lib.mi_conv2d_wgrad_fbb_ws_floats(K, C), device="cuda")
+    dw0 = torch.randn(K, 1, 1, C, device="cuda")
+    dw = dw0.clone()
+    st = stream_of(dz)
+    for rep in range(2):
+        _lib.call("mi_conv2d_wgrad_fbb", ptr(x), ptr(dz), ptr(w), ptr(coef), ptr(dw), ptr(ws), N, H, H, C, K, st)
+        torch.cuda.synchronize()
+        assert rel_err(dw - dw0, ref * (rep + 1)) < 1e-2, (rep, rel_err(dw - dw0, ref * (rep + 1)))
+        assert float(ws[:(K + C) * C].abs().max()) == 0.0  # T and G re-zeroed

@@ -102,6 +102,35 @@ def test_normalize_on_load_matches_materialised(name, size, batch, monkeypatch):
         assert e_nol <= 1.25 * e_mat + 0.01, (n, e_nol, e_mat)
 
 
+@pytest.mark.parametrize("name,size,batch", [("resnet50", 224, 32)])
+def test_folded_bn_backward_matches_materialised(name, size, batch, monkeypatch):
+    """BatchNorm backward folded into its consumer convs' GEMMs (ops/resblock.py
+    _Fold: the BN input gradient of 1x1 / stride-1 convs never materialised) against the same fused
+    blocks with the materialised BN-backward apply: losses and running statistics equal, every
+    gradient as close to fp32 PyTorch as the materialised path, and the folded path really taken."""
+    import mi355x_dp.ops.resblock as RB
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(batch, 3, size, size, device="cuda", generator=g)
+    y = torch.randint(0, 10, (batch,), device="cuda", generator=g)
+    monkeypatch.setattr(RB, "BN_FOLD", False)
+    used = RB.FOLD_USED[0]
+    l0, g0, b0 = _run(name, True, x, y)
+    assert RB.FOLD_USED[0] == used
+    monkeypatch.setattr(RB, "BN_FOLD", True)
+    l1, g1, b1 = _run(name, True, x, y)
+    assert RB.FOLD_USED[0] > used
+    lr, gr = _fp32_ref(name, x, y)
+    assert l1 == l0  # the forward is untouched
+    for n in b0:
+        assert rel_err(b1[n], b0[n]) < 1e-3, n
+    worst = []
+    for n in g0:
+        e_mat, e_fold = rel_err(g0[n], gr[n]), rel_err(g1[n], gr[n])
+        worst.append((e_fold - e_mat, n, e_fold, e_mat))
+        assert e_fold <= 1.25 * e_mat + 0.01, (n, e_fold, e_mat)
+    print(sorted(worst)[-3:])
+
+
 def test_fused_block_used_in_training():
     import mi355x_dp.models.resnet as R
     from mi355x_dp.models import get_model
