@@ -1456,8 +1456,9 @@ MI_API int mi_bn_bwd_train(const void* dy, const void* y, const void* x, void* d
   hipLaunchKernelGGL(bn_bwd_stats_kernel, grid, dim3(NT), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
                      (const bf16_t*)x, save_mean, part, M, C, rpb, relu);
   const FinArgs fb = fin_bwd_args(M, C, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
-  if (launch_bn_bwd_fused(part, nblk, fb, dy, y, x, dx, dres, relu, st)) return (int)hipGetLastError();
+  if (dx && launch_bn_bwd_fused(part, nblk, fb, dy, y, x, dx, dres, relu, st)) return (int)hipGetLastError();
   slab_finalize<true>(part, nblk, fb, st);
+  if (!dx && !dres) return (int)hipGetLastError();  // statistics + coefficients only (a folded consumer)
   int64_t nvec = (int64_t)M * C / 8;
   launch_bn_bwd_apply(dy, y, x, coef, dx, dres, nvec, C, relu, st);
   return (int)hipGetLastError();

@@ -491,9 +491,26 @@ class _ResBlock(torch.autograd.Function):
     def _shortcut_backward(x, dyd, dx, cd, md, isd, convs, bns, grads):
         """projection shortcut backward on the current stream: its BN backward (affine gradients
         returned raw), weight gradient, and data gradient written into dx -> (acc_flags, (gw, gb))"""
+        ds = convs[-1]
+        if _fold_ok(ds, x.shape):
+            # a stride-1 expansion (layer 1's 64 -> 256): statistics + coefficients, then the BN's
+            # input gradient folded into the shortcut conv's data and weight gradients (see _Fold)
+            N, C, H, W = cd.shape
+            M = N * H * W
+            lib = _lib.load()
+            gw, gb = _grad_buffer(bns[-1].w), _grad_buffer(bns[-1].b)
+            coef = torch.empty((3, C), dtype=F32, device=cd.device)
+            part = torch.empty((lib.mi_bn_partial_rows(M, C) + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32,
+                               device=cd.device)
+            FOLD_USED[0] += 1
+            _lib.call("mi_bn_bwd_train", ptr(dyd), ptr(dyd), ptr(cd), ptr(None), ptr(None), M, C, ptr(bns[-1].w),
+                      ptr(md), ptr(isd), ptr(gw), ptr(gb), ptr(coef), ptr(part), 0, stream_of(cd))
+            fold = _Fold(dyd, cd, coef)
+            grads[id(ds.w)] = _wgrad_fold(x, fold, ds)
+            _dgrad_fold(fold, ds, x.shape, dx)                      # dx = dgrad_ds
+            return 0, (gw, gb)
         dcd, gw, gb = _bn_bwd(dyd, dyd, cd, bns[-1], md, isd, relu=0, finish=False)
         grads[id(convs[-1].w)] = _wgrad(x, dcd, convs[-1])
-        ds = convs[-1]
         if ds.stride == 2 and ds.pad == 0 and ds.w.shape[2] == 1 and ds.w.shape[3] == 1:
             # 1x1 / stride-2 shortcut: its data gradient lives on the even pixels only -- write
             # just those and let conv1's dgrad read the sum there (DGRAD_SPARSE / DGRAD_ACC_EVEN)
