@@ -89,8 +89,15 @@ __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0
 // above the barrier that publishes their part (the builtin s_barrier is not a memory op)
 __device__ __forceinline__ void phase_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int MODE>
+// WR: rows per wave row -- 128 (256-row tiles) or 112 (224-row tiles: a 196-tile grid on 256 CUs becomes
+// 224 tiles of 7/8 the work; g256_bm).  The LDS parts keep their 128-row layout: with WR 112 the
+// second quadrant row holds 48 real rows (rows 48..63 of each wave row's slice are zero-filled and
+// never multiplied), IQ1 = 3 fragment rows instead of 4.
+template <int MODE, int WR = 128>
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
+  static_assert(WR == 128 || WR == 112, "256- or 224-row tiles");
+  constexpr int IQ1 = (WR - 64) / 16;  // fragment rows of quadrant row 1
+  constexpr int NI = 4 + IQ1;          // accumulator rows per wave
   __shared__ __attribute__((aligned(16))) uint4 smem[2 * 4 * PART_U4];  // 128 KB
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -115,7 +122,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   const int gsz = min(a.tiles_m - first_m, GROUP_M);
   const int tm = first_m + (bid % (GROUP_M * a.tiles_n)) % gsz;
   const int tn = (bid % (GROUP_M * a.tiles_n)) / gsz;
-  const int m0 = tm * G_BM, n0 = tn * G_BN;
+  const int m0 = tm * (2 * WR), n0 = tn * G_BN;
   const int nkl = kt1 - kt0;  // this block's k-tiles
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
@@ -137,13 +144,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     klim[i] = gk < a.K ? (a.K - gk + G_BK - 1) / G_BK : 0;
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
-      const int m = m0 + (p >> 6) * 128 + part * 64 + (p & 63);
+      const bool rin = part * 64 + (p & 63) < WR;  // a row of this tile (WR 112: not the padding)
+      const int m = m0 + (p >> 6) * WR + part * 64 + (p & 63);
       b_vo[part][i] = (uint32_t)((n0 + (p >> 5) * 64 + part * 32 + (p & 31)) * a.ldb + gk) * 2u;
       if constexpr (MODE == 0) {
-        a_vo[part][i] = (uint32_t)(m * a.lda + gk) * 2u;
+        a_vo[part][i] = rin ? (uint32_t)(m * a.lda + gk) * 2u : 0xF0000000u;  // padding: past the range
         a_hw[part][i] = 0;
       } else {
-        const uint32_t mm = m < a.M ? (uint32_t)m : 0u;
+        const uint32_t mm = (rin && m < a.M) ? (uint32_t)m : 0u;
         const uint32_t img = fdiv(mm, a.fPQ);
         const uint32_t rem = mm - img * a.fPQ.d;
         const uint32_t pp = fdiv(rem, a.fQ);
@@ -152,7 +160,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const int wb = MODE == 1 ? (int)qq * a.stride - a.pad : (int)qq + a.pad;
         // element offset of the gathered pixel (hb, wb) channel gk (may be negative: padding)
         a_vo[part][i] = (uint32_t)((((int)img * a.H + hb) * a.W + wb) * a.Cs + gk);
-        a_hw[part][i] = m < a.M ? (hb << 16) | (wb & 0xffff) : (int)0x80008000;  // invalid row: h = -32768
+        a_hw[part][i] = (rin && m < a.M) ? (hb << 16) | (wb & 0xffff) : (int)0x80008000;  // invalid: h = -32768
       }
     }
   }
@@ -191,9 +199,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[NI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -204,7 +212,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   auto read_a = [&](bf16x8 (&f)[4][2], int t, int mq) {
     const uint4* src = smem + ((t & 1) * 4 + mq) * PART_U4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < (mq == 0 ? 4 : IQ1); ++i)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
         f[i][kk] = __builtin_bit_cast(bf16x8, src[(wm * 64 + i * 16 + fr) * 8 + ((kk * 4 + fq) ^ (fr & 7))]);
@@ -221,7 +229,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < (mq == 0 ? 4 : IQ1); ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] =
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     constexpr int SC1 = 16;  // cache-policy bits of the buffer intrinsics: sc1
     const uint32_t mine = (uint32_t)(split * tile_f * 4) + tid * 16;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rsw, mine + (i * 4 + j) * 8192, 0, SC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
     for (int q = 0; q < a.tail_split; ++q) {
       const uint32_t part = (uint32_t)(q * tile_f * 4) + tid * 16;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsw, part + (i * 4 + j) * 8192, 0, SC1);
@@ -316,8 +324,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   // lane holds D[n = 16j + 4fq + r][m = 16i + fr] of each 16x16 tile (weights-first MFMA)
   if (a.out_f32) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + fr;
+    for (int i = 0; i < NI; ++i) {
+      const int m = m0 + wm * WR + i * 16 + fr;
       if (m >= a.M) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -358,7 +366,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < (mq == 0 ? 4 : IQ1); ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 v = acc[mq * 4 + i][j];
@@ -380,8 +388,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 #pragma unroll
       for (int u = 0; u < EPI_U; ++u) {
         const int rl = (g * EPI_U + u) * 8 + (lane >> 3);
-        const int m = m0 + wm * 128 + mq * 64 + rl;
-        ok[sl][u] = m < a.M && n < a.N;
+        const int m = m0 + wm * WR + mq * 64 + rl;
+        ok[sl][u] = m < a.M && n < a.N && mq * 64 + rl < WR;
         offs[sl][u] = ok[sl][u] ? (size_t)m * a.ldc + n : 0;
         bool acc_ok = true;
         if (BN_EPI && ok[sl][u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
@@ -795,6 +803,50 @@ static hipError_t plan_tail(G256Args& a, int nk, hipStream_t st) {
   return hipSuccess;
 }
 
+// Row tile of the NT kernel: 224 rows (WR 112) when its wave quantization beats 256 rows by >= 3 %
+// -- e.g. M = 50,176 (ResNet layer 3, batch 256): 196 tiles of 256 rows leave 60 of 256 CUs idle,
+// 224 tiles of 224 rows finish in 7/8 of the time (ResNet-50 +0.9 %, ResNet-152 +1.5 % same box,
+// profiles/g256_bm224_r6.md).  Cost model: rounds of the grid after plan_tail's split decision x the
+// tile height.  Auto applies to the conv modes only: on ViT-B/16 (its N = K = 768 GEMMs would take
+// 224 rows) it measured -0.5 %.  MI355X_DP_G256_BM224 (mi_set_g256_bm224): 0 never, 1 auto (default),
+// 2 always (plain GEMMs included).
+static int g_bm224 = -1;
+
+MI_API int mi_set_g256_bm224(int mode) {
+  g_bm224 = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
+  return 0;
+}
+
+static double g256_cost(int M, int N, int nk, int bm) {
+  const int tiles = cdiv(M, bm) * cdiv(N, G_BN);
+  const int full = (tiles / g_num_cus) * g_num_cus, tail = tiles - full;
+  double rounds = (double)(full / g_num_cus);
+  if (tail > 0) {
+    int split = 1;
+    if (g_tail_split_env && tail * 4 <= g_num_cus * 3) {
+      split = std::min(4, g_num_cus / tail);
+      while (split > 1 && nk / split < g_tail_min_kt) --split;
+    }
+    rounds += 1.0 / split;
+  }
+  return rounds * bm;
+}
+
+static int g256_wr(int M, int N, int K, bool conv) {
+  if (g_num_cus == 0) plan_defaults();
+  if (g_bm224 < 0) {
+    const char* e = std::getenv("MI355X_DP_G256_BM224");
+    g_bm224 = e ? std::max(0, std::min(2, std::atoi(e))) : 1;
+  }
+  if (g_bm224 == 0 || (g_bm224 == 1 && !conv)) return 128;
+  if (g_bm224 == 2) return 112;
+  const int nk = cdiv(K, G_BK);
+  return g256_cost(M, N, nk, 224) < 0.97 * g256_cost(M, N, nk, 256) ? 112 : 128;
+}
+
+// statistics slab rows of the conv kernel (mode 1 / 2) for an M x N x K conv: 2 per row tile
+MI_API int mi_g256_stat_rows(int M, int N, int K) { return 2 * cdiv(M, 2 * g256_wr(M, N, K, true)); }
+
 static int grid_of(const G256Args& a) {
   const int tiles = a.tiles_m * a.tiles_n;
   return a.tail_split > 1 ? a.full_blocks + (tiles - a.full_blocks) * a.tail_split : tiles;
@@ -846,12 +898,14 @@ MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bia
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = bias; a.aux = (bf16_t*)aux; a.epi = epi;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.out_f32 = out_f32; a.accumulate = accumulate;
-  a.tiles_m = cdiv(M, G_BM); a.tiles_n = cdiv(N, G_BN);
+  const int wr = g256_wr(M, N, K, false);
+  a.tiles_m = cdiv(M, 2 * wr); a.tiles_n = cdiv(N, G_BN);
   a.a_bytes = rsrc_bytes256((int64_t)M * lda);
   a.b_bytes = rsrc_bytes256((int64_t)N * ldb);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
   if (hipError_t e = plan_tail(a, cdiv(K, G_BK), st); e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gemm256_nt_kernel<0>, dim3(grid_of(a)), dim3(512), 0, st, a);
+  if (wr == 112) hipLaunchKernelGGL((gemm256_nt_kernel<0, 112>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((gemm256_nt_kernel<0, 128>), dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -886,7 +940,7 @@ MI_API int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, i
 // Implicit-GEMM convolution on the 256x256 pipeline.  mode 1 = forward: gathered = x [Nb,H,W,Cs],
 // rows = output pixels [Nb,P,Q], B = w [N][R][S][Cs]; mode 2 = stride-1 data gradient:
 // gathered = dy [Nb,H,W,Cs] (H,W = the forward output grid, Cs = forward K), rows = dx pixels
-// [Nb,P,Q], B = wt [N][R][S][Cs].  Cs % 64 == 0.  stats: [2 * cdiv(M, 256)][2][N] partials
+// [Nb,P,Q], B = wt [N][R][S][Cs].  Cs % 64 == 0.  stats: [mi_g256_stat_rows(M, N, K)][2][N] partials
 // (forward: sum / sum of squares; epi 4: BN-backward sums).  C bf16 [M][N].
 MI_API int mi_gemm256_conv2(int mode, const void* A, const void* B, void* C, float* stats, int epi, void* aux,
                             const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs, int P,
@@ -933,17 +987,22 @@ MI_API int mi_gemm256_conv3(int mode, const void* A, const void* B, void* C, flo
   a.H = H; a.W = W; a.Cs = Cs; a.S = S; a.stride = stride; a.pad = pad;
   a.fPQ = make_fastdiv((uint32_t)(P * Q)); a.fQ = make_fastdiv((uint32_t)Q);
   a.fS = make_fastdiv((uint32_t)S); a.fCpt = make_fastdiv((uint32_t)(Cs / 64));
-  a.tiles_m = cdiv(a.M, G_BM); a.tiles_n = cdiv(N, G_BN);
+  const int wr = g256_wr(a.M, N, a.K, true);
+  a.tiles_m = cdiv(a.M, 2 * wr); a.tiles_n = cdiv(N, G_BN);
   a.a_bytes = rsrc_bytes256((int64_t)Nb * H * W * Cs);
   a.b_bytes = rsrc_bytes256((int64_t)N * a.K);
   if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
   if (hipError_t e = plan_tail(a, cdiv(a.K, G_BK), st); e != hipSuccess) return (int)e;
   if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
-    fprintf(stderr, "[gemm] g256conv mode=%d M=%d N=%d K=%d Cs=%d R=%d s=%d epi=%d stats=%d blocks=%d\n", mode, a.M,
-            a.N, a.K, Cs, R, stride, epi, stats != nullptr, grid_of(a));
-  if (mode == 1)
-    hipLaunchKernelGGL(gemm256_nt_kernel<1>, dim3(grid_of(a)), dim3(512), 0, st, a);
+    fprintf(stderr, "[gemm] g256conv mode=%d M=%d N=%d K=%d Cs=%d R=%d s=%d epi=%d stats=%d blocks=%d bm=%d\n", mode,
+            a.M, a.N, a.K, Cs, R, stride, epi, stats != nullptr, grid_of(a), 2 * wr);
+  if (mode == 1 && wr == 112)
+    hipLaunchKernelGGL((gemm256_nt_kernel<1, 112>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  else if (mode == 1)
+    hipLaunchKernelGGL((gemm256_nt_kernel<1, 128>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  else if (wr == 112)
+    hipLaunchKernelGGL((gemm256_nt_kernel<2, 112>), dim3(grid_of(a)), dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL(gemm256_nt_kernel<2>, dim3(grid_of(a)), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((gemm256_nt_kernel<2, 128>), dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -1753,6 +1753,7 @@ extern "C" int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, 
                                const void* aux2, const float* mean, int bn_relu, int Nb, int H, int W, int Cs,
                                int P, int Q, int R, int S, int stride, int pad, int N, hipStream_t st);
 static int g_gemm256_env = -1, g_conv256_min_tiles = -1, g_conv256_min_k = 64;
+extern "C" int mi_g256_stat_rows(int M, int N, int K);  // gemm256.hip: 2 per 224- or 256-row tile
 static bool use_gemm256_conv(int M, int N, int Cs, int Kt) {
   if (g_gemm256_env < 0) {
     const char* e = std::getenv("MI355X_DP_GEMM256");
@@ -1826,7 +1827,7 @@ static bool use_stem_kernel(int C, int K, int R, int S, int stride, int pad, int
 MI_API int mi_conv_stat_rows_g(int Nb, int H, int W, int C, int K, int R, int S, int stride, int pad, int P, int Q) {
   const int M = Nb * P * Q;
   if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return mi_stem_conv_stat_rows(Nb, P);
-  if (C % 64 == 0 && use_gemm256_conv(M, K, C, R * S * C)) return 2 * cdiv(M, 256);
+  if (C % 64 == 0 && use_gemm256_conv(M, K, C, R * S * C)) return mi_g256_stat_rows(M, K, R * S * C);
   if (const int pr = panel_rows_fwd(M, K, C, R, S, pad, H, W, P, Q, stride); pr > 0) return pr;
   const int rp = C % 64 == 0 ? halo_rp(M, K, R, S, stride, pad, C, H, W, P, Q) : 0;
   if (rp > 0) return Nb * cdiv(P, rp);
@@ -1836,7 +1837,7 @@ MI_API int mi_conv_stat_rows_g(int Nb, int H, int W, int C, int K, int R, int S,
 // Statistics-slab rows written by a conv forward (M output pixels, N channels, Cs input channels),
 // for shapes outside the halo tiling (1x1 / strided convs, GEMMs).
 MI_API int mi_conv_stat_rows(int M, int N, int Cs, int RS) {
-  if (use_gemm256_conv(M, N, Cs, RS * Cs)) return 2 * cdiv(M, 256);
+  if (use_gemm256_conv(M, N, Cs, RS * Cs)) return mi_g256_stat_rows(M, N, RS * Cs);
   if (RS == 1 && Cs % 64 == 0)  // a 1x1 (pad 0) conv forward on the panel kernel
     if (const int pr = mi_panel_stat_rows(M, N, Cs); pr > 0) return pr;
   const int bm = nt_choice(M, N) == 2 ? 64 : 128;
@@ -1909,7 +1910,7 @@ MI_API int mi_conv2d_dgrad(const void* dy, const void* wt, void* dx,
 // Statistics-slab rows written by mi_conv2d_dgrad_ex with stats (all parity classes).
 MI_API int mi_dgrad_stat_rows(int Nb, int H, int W, int C, int P, int Q, int stride, int K, int RS) {
   const int M = Nb * H * W;
-  if (stride == 1 && use_gemm256_conv(M, C, K, RS * K)) return 2 * cdiv(M, 256);
+  if (stride == 1 && use_gemm256_conv(M, C, K, RS * K)) return mi_g256_stat_rows(M, C, RS * K);
   if (const int pr = panel_rows_dgrad(M, C, K, RS, stride); pr > 0) return pr;
   const int bm = nt_choice(M, C) == 2 ? 64 : 128;
   if (stride == 1 && RS == 9) {

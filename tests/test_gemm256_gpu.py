@@ -15,6 +15,30 @@ def _native():
     torch.manual_seed(0)
 
 
+@pytest.fixture(params=[0, 2], ids=["bm256", "bm224"])
+def bm224(request):
+    """the NT kernel's row tile: 256 rows (mode 0) or forced 224 rows (mode 2; auto picks it where the
+    wave quantization pays, gemm256.hip g256_wr)"""
+    from mi355x_dp.ops import _lib
+    lib = _lib.load()
+    lib.mi_set_g256_bm224(request.param)
+    yield request.param
+    lib.mi_set_g256_bm224(1)
+
+
+def test_gemm256_row_tile_choice():
+    """auto mode (conv kernels): 224-row tiles for the 196-tile ResNet layer-3 / layer-4 grids, 256
+    rows where the split tail already fills the chip"""
+    from mi355x_dp.ops import _lib
+    lib = _lib.load()
+    lib.mi_set_g256_bm224(1)
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("cost model checked for 256 CUs")
+    assert lib.mi_g256_stat_rows(50176, 256, 2304) == 2 * 224   # ceil(50176 / 224) tiles x 2 wave rows
+    assert lib.mi_g256_stat_rows(12544, 512, 4608) == 2 * 56    # layer 4: 112 tiles, tail split 2
+    assert lib.mi_g256_stat_rows(50432, 768, 3072) == 2 * 197  # 256 rows: tail split-K fills the chip
+
+
 def rel_err(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6))
 
@@ -31,7 +55,7 @@ def run(A, B, C, bias=None, aux=None, epi=0, out_f32=0, acc=0):
 
 @pytest.mark.parametrize("M,N,K", [(512, 512, 64), (1000, 776, 200), (50432 // 8, 3072, 768), (300, 256, 3072),
                                    (257, 264, 72), (4096, 4096, 4096)])
-def test_gemm256_shapes(M, N, K):
+def test_gemm256_shapes(M, N, K, bm224):
     A = (torch.rand(M, K, device="cuda") * 2 - 1).to(BF)
     B = (torch.rand(N, K, device="cuda") * 2 - 1).to(BF)
     bias = torch.randn(N, device="cuda")
@@ -46,7 +70,7 @@ def test_gemm256_shapes(M, N, K):
 
 
 @pytest.mark.parametrize("epi", [1, 2, 3])
-def test_gemm256_epilogues(epi):
+def test_gemm256_epilogues(epi, bm224):
     M, N, K = 600, 512, 256
     A = (torch.rand(M, K, device="cuda") * 2 - 1).to(BF)
     B = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.1).to(BF)
@@ -99,7 +123,7 @@ def conv256_forced():
 
 
 @pytest.mark.parametrize("shape", CONV256)
-def test_conv256_fwd_stats_and_dgrad(shape, conv256_forced):
+def test_conv256_fwd_stats_and_dgrad(shape, conv256_forced, bm224):
     """conv forward (+ BN statistics epilogue) and stride-1 dgrad (plain / accumulate / BN-backward
     epilogues) on the 256x256 kernel vs the 128x128 kernel and an fp32 reference"""
     from mi355x_dp.ops import _lib
@@ -113,7 +137,7 @@ def test_conv256_fwd_stats_and_dgrad(shape, conv256_forced):
     st = stream_of(x)
     M = N * P * P
     rows = lib.mi_conv_stat_rows(M, K, C, R * R)
-    assert rows == 2 * ((M + 255) // 256)
+    assert rows == 2 * ((M + 255) // 256 if bm224 == 0 else (M + 223) // 224)
     slab = torch.full((rows + 64, 2, K), float("nan"), device="cuda")
     y = torch.empty(N, K, P, P, dtype=BF, device="cuda", memory_format=CL)
     _lib.call("mi_conv2d_fwd", ptr(x), ptr(w), ptr(y), ptr(None), ptr(slab), N, H, H, C, K, R, R, s, p, P, P, 0, st)

@@ -12,6 +12,4 @@ run() {  # tag, env...
 for r in a b; do
   run def_$r MI355X_DP_PANEL=1 || exit $?
   run p3x3_$r MI355X_DP_PANEL=5 || exit $?
-  run side256_$r MI355X_DP_TN_BLOCKS_SIDE=256 || exit $?
-  run side512_$r MI355X_DP_TN_BLOCKS_SIDE=512 || exit $?
 done
