@@ -72,6 +72,10 @@ struct G256Args {
   int* counters;
   int aux_even;         // epi 3 / 5: accumulated-into gradient defined only at even (h, w) (gemm_conv.hip)
   const uint8_t* mbits; // epi 4 / 5: ReLU mask bytes (8 channels each) instead of aux (gemm_conv.hip NTArgs)
+  // folded BN backward (mode 2, 1x1): k-tiles [khalf_kt, 2 khalf_kt) gather c (A2) where the first
+  // half gathers dz (A); B = [diag(k0) W | diag(k1) W], bias = k2 W (mi_gemm256_dgrad_fbb)
+  const bf16_t* A2;
+  int a2_bytes, khalf_kt;
 };
 
 // Wave priority: static s_setprio 1 for the second-dispatched half (waves 4-7) before the main loop
@@ -127,6 +131,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.b_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA2 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(MODE == 2 && a.khalf_kt ? a.A2 : a.A), (short)0, MODE == 2 && a.khalf_kt ? a.a2_bytes : 0, 0x00020000);
 
   // per-thread load geometry, fixed across k-tiles: 2 chunks per part, LDS rows p = (i*512+tid)/8.
   // plain: byte offset at k-tile t = base + 128 t while t < klim (chunk inside K), else the
@@ -178,23 +184,34 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
                                                  16, vo, 0, 0, 0);
       }
     } else {
-      // wave-uniform tap / channel block of k-tile t
-      const int tt = ta < kt1 ? ta : 0;
+      // wave-uniform tap / channel block of k-tile t (folded BN backward: the second half of the
+      // k-tiles gathers c from A2 -- a branch, the operand choice must stay scalar)
+      const int tt0 = __builtin_amdgcn_readfirstlane(ta < kt1 ? ta : 0);
+      const bool second = MODE == 2 && a.khalf_kt && tt0 >= a.khalf_kt;
+      const int tt = second ? tt0 - a.khalf_kt : tt0;
       const int tap = (int)fdiv((uint32_t)tt, a.fCpt);
       const int c0 = (tt - tap * (int)a.fCpt.d) * 64;
       const int r = (int)fdiv((uint32_t)tap, a.fS);
       const int sx = tap - r * a.S;
       const int dh = MODE == 1 ? r : -r, dw = MODE == 1 ? sx : -sx;
       const int toff = (dh * a.W + dw) * a.Cs + c0;
+      uint32_t vos[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int hw = a_hw[part][i];
         const int h = (hw >> 16) + dh, w = ((int)(short)(hw & 0xffff)) + dw;
         const bool ok = ta < kt1 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        const uint32_t vo = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
-        MI_ASSERT(vo == OOB || vo + 16u <= (uint32_t)a.a_bytes, vo);  // valid taps never rely on zero fill
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vo, 0, 0,
-                                                 0);
+        vos[i] = ok ? (uint32_t)((int)a_vo[part][i] + toff) * 2u : OOB;
+        MI_ASSERT(vos[i] == OOB || vos[i] + 16u <= (uint32_t)(second ? a.a2_bytes : a.a_bytes), vos[i]);
+      }
+      if (second) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA2, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vos[i], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(void, dst + i * 512 + wid * 64), 16, vos[i], 0, 0, 0);
       }
     }
   };
@@ -1004,5 +1021,67 @@ MI_API int mi_gemm256_conv3(int mode, const void* A, const void* B, void* C, flo
     hipLaunchKernelGGL((gemm256_nt_kernel<2, 112>), dim3(grid_of(a)), dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL((gemm256_nt_kernel<2, 128>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// ---- folded BatchNorm backward on the 256-wide data-gradient kernel (ops/resblock.py _Fold; the
+// conv_panel.hip mi_panel_dgrad_fbb twin for convs too deep for the panel): the 1x1 / stride-1 data
+// gradient of a BN input gradient k0 dz + k1 c + k2 as ONE GEMM over [dz | c] (2K deep) against
+// wq = [diag(k0) W | diag(k1) W] (bf16 [C][2K], written here) plus the bias k2 W (fp32 [C]).
+__global__ __launch_bounds__(256) void fbb_wprep_kernel(const bf16_t* __restrict__ wt, const float* __restrict__ coef,
+                                                        bf16_t* __restrict__ wq, float* __restrict__ bias, int K) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  float b = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float w = bf2f(wt[(size_t)c * K + k]);
+    wq[(size_t)c * 2 * K + k] = f2bf(w * coef[k]);
+    wq[(size_t)c * 2 * K + K + k] = f2bf(w * coef[K + k]);
+    b = fmaf(w, coef[2 * K + k], b);
+  }
+  red[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bias[c] = red[0];
+}
+
+// dz / c NHWC [Nb,H,W,K], wt bf16 [C][K] (the dgrad weight layout), wq: C * 2K bf16 and bias: C
+// floats of workspace; epilogue / statistics as mi_gemm256_conv3 mode 2 (stats rows:
+// mi_g256_stat_rows(M, C, 2K)).
+MI_API int mi_gemm256_dgrad_fbb(const void* dz, const void* c, const float* coef, const void* wt, void* wq, float* bias,
+                                void* dx, float* stats, int epi, void* aux, const void* aux2, const float* mean,
+                                int bn_relu, int Nb, int H, int W, int C, int K, int aux_even, const void* mbits,
+                                hipStream_t st) {
+  if (K % 64 != 0 || C % 8 != 0 || !coef || !wq || !bias || !(epi == 0 || epi == 3 || epi == 4 || epi == 5) ||
+      (epi == 3 && !aux) || (epi >= 4 && bn_relu && !aux && !mbits) || (mbits && (epi < 4 || !bn_relu)) ||
+      (epi >= 4 && stats && (!aux2 || !mean)))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fbb_wprep_kernel, dim3(C), dim3(256), 0, st, (const bf16_t*)wt, coef, (bf16_t*)wq, bias, K);
+  G256Args a{};
+  a.mbits = (const uint8_t*)mbits;
+  a.A = (const bf16_t*)dz; a.A2 = (const bf16_t*)c; a.B = (const bf16_t*)wq; a.C = dx; a.bias = bias;
+  a.aux = (bf16_t*)aux; a.aux2 = (const bf16_t*)aux2; a.mean = mean; a.bn_relu = bn_relu; a.epi = epi;
+  a.stats = stats;
+  a.aux_even = aux_even;
+  a.M = Nb * H * W; a.N = C; a.K = 2 * K; a.lda = 0; a.ldb = 2 * K; a.ldc = C;
+  a.out_f32 = 0; a.accumulate = 0;
+  a.H = H; a.W = W; a.Cs = K; a.S = 1; a.stride = 1; a.pad = 0;
+  a.khalf_kt = K / 64;
+  a.fPQ = make_fastdiv((uint32_t)(H * W)); a.fQ = make_fastdiv((uint32_t)W);
+  a.fS = make_fastdiv(1u); a.fCpt = make_fastdiv((uint32_t)(K / 64));
+  const int wr = g256_wr(a.M, C, a.K, true);
+  a.tiles_m = cdiv(a.M, 2 * wr); a.tiles_n = cdiv(C, G_BN);
+  a.a_bytes = a.a2_bytes = rsrc_bytes256((int64_t)a.M * K);
+  a.b_bytes = rsrc_bytes256((int64_t)C * a.K);
+  if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  if (hipError_t e = plan_tail(a, cdiv(a.K, G_BK), st); e != hipSuccess) return (int)e;
+  if (const char* t = std::getenv("MI355X_DP_TRACE_GEMM"); t && t[0] == '1')
+    fprintf(stderr, "[gemm] g256dgrad-fbb M=%d N=%d K=%d epi=%d stats=%d blocks=%d bm=%d\n", a.M, C, a.K, epi,
+            stats != nullptr, grid_of(a), 2 * wr);
+  if (wr == 112) hipLaunchKernelGGL((gemm256_nt_kernel<2, 112>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((gemm256_nt_kernel<2, 128>), dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -2044,6 +2044,27 @@ MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
   return (int)dispatch_tn(a, st);
 }
 
+// ---- folded BatchNorm backward, data-gradient routing: the panel kernel when the doubled depth fits
+// its LDS (conv_panel.hip), else the 256-wide kernel where the unfolded data gradient runs there
+// (gemm256.hip mi_gemm256_dgrad_fbb); 0: not eligible (the caller materialises dX)
+extern "C" int mi_panel_fbb_rows(int M, int C, int K);
+extern "C" int mi_gemm256_dgrad_fbb(const void* dz, const void* c, const float* coef, const void* wt, void* wq,
+                                    float* bias, void* dx, float* stats, int epi, void* aux, const void* aux2,
+                                    const float* mean, int bn_relu, int Nb, int H, int W, int C, int K, int aux_even,
+                                    const void* mbits, hipStream_t st);
+MI_API int mi_conv_fbb_route(int M, int C, int K) {
+  if (K % 64 != 0 || C % 64 != 0) return 0;
+  if (mi_panel_fbb_rows(M, C, K) > 0) return 1;
+  if (use_gemm256_conv(M, C, K, K)) return 2;
+  return 0;
+}
+
+// statistics slab rows of the folded data gradient (route 1 or 2), 0 if not eligible
+MI_API int mi_conv_fbb_rows(int M, int C, int K) {
+  const int r = mi_conv_fbb_route(M, C, K);
+  return r == 1 ? mi_panel_fbb_rows(M, C, K) : (r == 2 ? mi_g256_stat_rows(M, C, 2 * K) : 0);
+}
+
 // ---- folded BatchNorm backward, weight-gradient side (conv_panel.hip mi_panel_dgrad_fbb): the weight
 // gradient of a 1x1 / stride-1 conv against its output's BN input gradient dX = k0 dz + k1 c + k2 (per
 // output channel k) without dX.  With c = x W^T, c^T x = W (x^T x), so

@@ -252,7 +252,7 @@ def _dgrad_bn(dy, spec, y_prev, c_prev, mean_prev, mask=None, bits=None):
     N, C, H, W = c_prev.shape
     lib = _lib.load()
     if isinstance(dy, _Fold):  # the output BN's input gradient folded into this data gradient
-        rows = lib.mi_panel_fbb_rows(N * H * W, C, spec.w.shape[0])
+        rows = lib.mi_conv_fbb_rows(N * H * W, C, spec.w.shape[0])
         slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dy.dz.device)
         dz = torch.empty_like(c_prev, memory_format=CL)
         _dgrad_fold(dy, spec, c_prev.shape, dz, EPI_BN_BWD, y_prev, c_prev, mean_prev, 1, slab, mbits=bits)
@@ -310,6 +310,12 @@ def _bn_bwd_pre(dz, c, bn, mean, invstd, slab, rows):
 # so the BN-backward apply pass (read dz, c; write dX) and both consumers' reads of dX become one
 # extra read of c per consumer.  MI355X_DP_BN_FOLD=0 restores the materialised path.
 BN_FOLD = os.environ.get("MI355X_DP_BN_FOLD", "1") != "0"
+# widest BN (K) folded: 256 (default) keeps the fold to layer 1 (the panel route); 1024 adds the
+# layer-3 expansions on the 256-wide kernel (mi_gemm256_dgrad_fbb), which measured slower: ResNet-50
+# 13,506 / 13,502 vs 13,654 / 13,679 img/s, ResNet-152 5,585 / 5,564 vs 5,917 / 5,900 -- the 196-tile
+# data gradient is MFMA-bound, so doubling its depth costs more than the apply pass it replaces
+# (profiles/bn_fold_r6.md)
+BN_FOLD_MAXK = int(os.environ.get("MI355X_DP_BN_FOLD_MAXK", "256"))
 _FBB_WS = {}  # (weight id, device) -> the folded weight gradient's fp32 workspace (zero between calls)
 FOLD_USED = [0]  # diagnostics: BN backwards taken folded
 
@@ -335,10 +341,13 @@ def _fold_ok(spec, x_shape) -> bool:
     if not BN_FOLD:
         return False
     K, C, R, S = spec.w.shape
-    if R != 1 or S != 1 or spec.stride != 1 or spec.pad != 0 or K % 64 or C % 64 or K <= C:
+    # (C <= 256: the folded weight gradient's combine multiplies W by the C x C Gram matrix of x)
+    if (R != 1 or S != 1 or spec.stride != 1 or spec.pad != 0 or K % 64 or C % 64 or K <= C or C > 256
+            or K > BN_FOLD_MAXK):
         return False
     N, _, H, W = x_shape
-    return _lib.load().mi_panel_fbb_rows(N * H * W, C, K) > 0
+    # the panel kernel at the doubled depth, or the 256-wide kernel where the unfolded dgrad runs
+    return _lib.load().mi_conv_fbb_route(N * H * W, C, K) > 0
 
 
 def _bn_bwd_fold(dz, c, bn, mean, invstd, slab, rows):
@@ -381,6 +390,15 @@ def _dgrad_fold(fold, spec, x_shape, out, epi=0, aux=None, aux2=None, mean=None,
     ``acc_src`` (default: ``out`` itself) into ``out``"""
     N, C, H, W = x_shape
     K = spec.w.shape[0]
+    route = _lib.load().mi_conv_fbb_route(N * H * W, C, K)
+    if route == 2:  # the 256-wide kernel: scaled weights [C][2K] and the k2 bias written per call
+        assert acc_src is None, "out-of-place accumulate: panel route only"
+        wq = torch.empty((C, 2 * K), dtype=BF16, device=fold.dz.device)
+        bias = torch.empty(C, dtype=F32, device=fold.dz.device)
+        _lib.call("mi_gemm256_dgrad_fbb", ptr(fold.dz), ptr(fold.c), ptr(fold.coef), ptr(weight_bf16_t(spec.w)),
+                  ptr(wq), ptr(bias), ptr(out), ptr(stats), int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), N, H,
+                  W, C, K, (int(flags) >> 1) & 1, ptr(mbits), stream_of(fold.dz))
+        return out
     _lib.call("mi_panel_dgrad_fbb", ptr(fold.dz), ptr(fold.c), ptr(fold.coef), ptr(weight_bf16_t(spec.w)), ptr(out),
               N, H, W, C, K, int(epi), ptr(aux), ptr(aux2), ptr(mean), int(relu), ptr(stats), (int(flags) >> 1) & 1,
               ptr(mbits), ptr(acc_src), stream_of(fold.dz))
@@ -606,7 +624,7 @@ class _ResBlock(torch.autograd.Function):
             rows = lib.mi_dgrad_stat_rows(N, H, W, C, dc.shape[2], dc.shape[3], convs[0].stride,
                                           convs[0].w.shape[0], convs[0].w.shape[2] * convs[0].w.shape[3])
             if isinstance(dc, _Fold):
-                rows = lib.mi_panel_fbb_rows(N * H * W, C, convs[0].w.shape[0])
+                rows = lib.mi_conv_fbb_rows(N * H * W, C, convs[0].w.shape[0])
             elif acc_src is not None:
                 rows = _panel_oop_rows(convs[0], x.shape)
             slab = torch.empty((rows + lib.mi_bn_slab_extra_rows(), 2, C), dtype=F32, device=dx.device)

@@ -272,3 +272,42 @@ def test_wgrad_fbb(lib, shape):
         torch.cuda.synchronize()
         assert rel_err(dw - dw0, ref * (rep + 1)) < 1e-2, (rep, rel_err(dw - dw0, ref * (rep + 1)))
         assert float(ws[:(K + C) * C].abs().max()) == 0.0  # T and G re-zeroed
+
+
+@pytest.mark.parametrize("epi", [0, 4])
+@pytest.mark.parametrize("shape", [(4, 14, 256, 1024), (3, 13, 256, 512)])
+def test_gemm256_dgrad_fbb(lib, shape, epi):
+    """the folded data gradient on the 256-wide kernel (convs too deep for the panel at 2K): [dz | c]
+    gathered from two tensors by k-tile against the scaled weights written per call, the k2 bias in
+    the epilogue, against fp32 math on the materialised dX (forced onto the 256-wide kernel)"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    N, H, C, K = shape
+    M = N * H * H
+    dz, c, coef, w, dX = _fbb_inputs(N, H, C, K, 13)
+    wt = torch.empty(C, 1, 1, K, dtype=BF, device="cuda")
+    st = stream_of(dz)
+    _lib.call("mi_conv_wtrans", ptr(w), ptr(wt), K, 1, C, st)
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float(), dX, 1, 0)
+    yb = torch.relu(torch.randn(N, C, H, H, device="cuda")).to(BF).contiguous(memory_format=CL)
+    ybits = (yb.permute(0, 2, 3, 1).reshape(M, C // 8, 8) > 0).to(torch.int32)
+    bits = (ybits << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
+    xin = torch.randn(N, C, H, H, device="cuda").to(BF).contiguous(memory_format=CL)
+    mean = torch.randn(C, device="cuda") * 0.1
+    rows = lib.mi_g256_stat_rows(M, C, 2 * K)
+    sl = torch.full((rows + 8, 2, C), float("nan"), device="cuda") if epi == 4 else None
+    wq = torch.empty(C, 2 * K, dtype=BF, device="cuda")
+    bias = torch.empty(C, device="cuda")
+    dx = torch.empty(N, C, H, H, dtype=BF, device="cuda", memory_format=CL)
+    _lib.call("mi_gemm256_dgrad_fbb", ptr(dz), ptr(c), ptr(coef), ptr(wt), ptr(wq), ptr(bias), ptr(dx), ptr(sl), epi,
+              ptr(None), ptr(xin), ptr(mean), 1, N, H, H, C, K, 0, ptr(bits if epi == 4 else None), st)
+    torch.cuda.synchronize()
+    want = ref if epi == 0 else ref.to(BF).float() * (yb > 0).float()
+    assert rel_err(dx, want) < 2e-2, rel_err(dx, want)
+    assert rel_err(bias, (coef[2].view(1, K) * wt.view(C, K).float()).sum(1)) < 1e-4
+    if epi == 4:
+        assert torch.isfinite(sl[:rows]).all()
+        wf = want.permute(0, 2, 3, 1).reshape(M, C)
+        xf = xin.float().permute(0, 2, 3, 1).reshape(M, C)
+        assert rel_err(sl[:rows, 0].sum(0), wf.sum(0)) < 3e-2
+        assert rel_err(sl[:rows, 1].sum(0), (wf * (xf - mean)).sum(0)) < 3e-2
