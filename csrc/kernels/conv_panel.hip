@@ -116,8 +116,8 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
   // per chunk the accumulated-into gradient (or the residual), the BN input and the ReLU source
   constexpr int EL = EPI == 1 ? 3 * ST : 0;
   constexpr int RING_U4 = 8 * S * PN_SLOT_U4;
-  static_assert(WNW * WMW == 8 && (WN == 64 || WN == 128), "8 waves");
-  static_assert(EPI == 0 || WN == 64, "data-gradient operands held in registers: 64-column waves");
+  static_assert(WNW * WMW == 8 && (WN == 32 || WN == 64 || WN == 128), "8 waves");
+  static_assert(EPI == 0 || WN <= 64, "data-gradient operands held in registers: <= 64-column waves");
   // ONE LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
   // [8 waves][S slots] A rings, then the weight panel [nk][BN][8 chunks]
   __shared__ __attribute__((aligned(16))) uint4 smem[PN_LDS_U4];
@@ -382,7 +382,8 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
       for (int ii = 0; ii < 2 / HALVES; ++ii) {
         const int i = h + ii;  // fragment row block
         const int row = WN == 128 ? fr : 16 * i + fr;
-        const int sw = WN == 128 ? row : ((row >> 1) & 7);
+        // chunk swizzle within the row's CPR chunks (WN 32: 4 chunks)
+        const int sw = WN == 128 ? row : ((row >> 1) & (CPR - 1));
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const f32x4 v = acc[i][j];
@@ -398,20 +399,30 @@ __global__ __launch_bounds__(512) void panel_kernel(PanelArgs a) {
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int rr = er + RPI * u;
-        const int sw = WN == 128 ? rr : ((rr >> 1) & 7);
+        const int sw = WN == 128 ? rr : ((rr >> 1) & (CPR - 1));
         ra[u] = cbase + (uint32_t)(rr * (WN * 2) + ((ec ^ sw) * 16));
       }
-      static_assert(NU == 4, "four read-back chunks per pass");
-      u32x4 rb[4];
-      asm volatile(
-          "ds_read_b128 %0, %4\n\t"
-          "ds_read_b128 %1, %5\n\t"
-          "ds_read_b128 %2, %6\n\t"
-          "ds_read_b128 %3, %7\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(rb[0]), "=&v"(rb[1]), "=&v"(rb[2]), "=&v"(rb[3])
-          : "v"(ra[0]), "v"(ra[1]), "v"(ra[2]), "v"(ra[3])
-          : "memory");
+      static_assert(NU == 4 || NU == 2, "four (WN 32: two) read-back chunks per pass");
+      u32x4 rb[NU];
+      if constexpr (NU == 4) {
+        asm volatile(
+            "ds_read_b128 %0, %4\n\t"
+            "ds_read_b128 %1, %5\n\t"
+            "ds_read_b128 %2, %6\n\t"
+            "ds_read_b128 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(rb[0]), "=&v"(rb[1]), "=&v"(rb[2]), "=&v"(rb[3])
+            : "v"(ra[0]), "v"(ra[1]), "v"(ra[2]), "v"(ra[3])
+            : "memory");
+      } else {
+        asm volatile(
+            "ds_read_b128 %0, %2\n\t"
+            "ds_read_b128 %1, %3\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(rb[0]), "=&v"(rb[1])
+            : "v"(ra[0]), "v"(ra[1])
+            : "memory");
+      }
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int k = h * NU + u;
@@ -541,7 +552,7 @@ PanelPlan panel_plan(int M, int N, int K, bool dgrad) {
     const char* e = std::getenv("MI355X_DP_PANEL");
     g_pn_mode = (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 1;
   }
-  if (!(g_pn_mode & 3) || K % 64 != 0 || K > 576 || N % 64 != 0 || M < ((g_pn_mode & 2) ? 1 : PN_MIN_M)) return p;
+  if (!(g_pn_mode & 3) || K % 64 != 0 || K > 1024 || N % 32 != 0 || M < ((g_pn_mode & 2) ? 1 : PN_MIN_M)) return p;
   if (g_pn_cus == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -553,12 +564,14 @@ PanelPlan panel_plan(int M, int N, int K, bool dgrad) {
     p.bn = 256;
   } else if (N % 128 == 0 && 128 * kb <= 64 * 1024) {
     p.bn = 128;
-  } else if (64 * kb <= 96 * 1024) {
+  } else if (N % 64 == 0 && 64 * kb <= 96 * 1024) {
     p.bn = 64;
+  } else if (32 * kb <= 64 * 1024) {
+    p.bn = 32;  // K up to 1024 (e.g. ResNet layer 3's 1024 -> 256 convs): 32-column panels, 8 per 256 cols
   } else {
     return PanelPlan{};
   }
-  p.wn = dgrad ? 64 : std::min(p.bn, 128);
+  p.wn = p.bn == 32 ? 32 : (dgrad ? 64 : std::min(p.bn, 128));
   // ring depth from what the weight panel leaves of the 160 KB: 8 waves x S x 4 KB
   const int64_t bpanel = p.bn * kb;
   p.s = bpanel <= 32 * 1024 ? 4 : (bpanel <= 64 * 1024 ? 3 : 2);
@@ -591,11 +604,13 @@ int launch_plan(const PanelPlan& p, PanelArgs& a, hipStream_t st, const char* wh
   if constexpr (EPI == 0) {
     if (p.bn == 256) launch_panel<256, 128, 0>(a, p.s, grid, st);
     else if (p.bn == 128) launch_panel<128, 128, 0>(a, p.s, grid, st);
-    else launch_panel<64, 64, 0>(a, p.s, grid, st);
+    else if (p.bn == 64) launch_panel<64, 64, 0>(a, p.s, grid, st);
+    else launch_panel<32, 32, 0>(a, p.s, grid, st);
   } else {
     if (p.bn == 256) launch_panel<256, 64, 1>(a, p.s, grid, st);
     else if (p.bn == 128) launch_panel<128, 64, 1>(a, p.s, grid, st);
-    else launch_panel<64, 64, 1>(a, p.s, grid, st);
+    else if (p.bn == 64) launch_panel<64, 64, 1>(a, p.s, grid, st);
+    else launch_panel<32, 32, 1>(a, p.s, grid, st);
   }
   return (int)hipGetLastError();
 }

@@ -1754,6 +1754,8 @@ extern "C" int mi_gemm256_conv(int mode, const void* A, const void* B, void* C, 
                                int P, int Q, int R, int S, int stride, int pad, int N, hipStream_t st);
 static int g_gemm256_env = -1, g_conv256_min_tiles = -1, g_conv256_min_k = 64;
 extern "C" int mi_g256_stat_rows(int M, int N, int K);  // gemm256.hip: 2 per 224- or 256-row tile
+extern "C" int mi_panel_stat_rows(int M, int N, int K);
+static int g_panel_first = -1;
 static bool use_gemm256_conv(int M, int N, int Cs, int Kt) {
   if (g_gemm256_env < 0) {
     const char* e = std::getenv("MI355X_DP_GEMM256");
@@ -1766,8 +1768,23 @@ static bool use_gemm256_conv(int M, int N, int Cs, int Kt) {
     const char* c = std::getenv("MI355X_DP_CONV256_MIN_K");
     g_conv256_min_k = c ? std::atoi(c) : 512;
   }
-  return g_gemm256_env && Cs % 64 == 0 && Kt >= g_conv256_min_k && N % 8 == 0 && N >= 256 &&
-         (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_conv256_min_tiles;
+  if (!(g_gemm256_env && Cs % 64 == 0 && Kt >= g_conv256_min_k && N % 8 == 0 && N >= 256 &&
+        (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_conv256_min_tiles))
+    return false;
+  // MI355X_DP_PANEL_FIRST=1: a 1x1 conv the panel kernel takes (K up to 1024 with 32-column panels)
+  // leaves the 256-wide kernel (forward and stride-1 data gradient alike: the panel plan does not
+  // depend on the direction)
+  if (g_panel_first < 0) {
+    const char* e = std::getenv("MI355X_DP_PANEL_FIRST");
+    g_panel_first = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_panel_first && Kt == Cs && mi_panel_stat_rows(M, N, Kt) > 0) return false;
+  return true;
+}
+
+MI_API void mi_set_panel_first(int on) {
+  use_gemm256_conv(0, 0, 0, 0);  // env init
+  g_panel_first = on ? 1 : 0;
 }
 
 MI_API void mi_set_conv256_min_tiles(int t) {

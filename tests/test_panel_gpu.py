@@ -25,6 +25,8 @@ SHAPES = [
     (3, 256, 14, 1024, 1),  # layer-3 expansion, M = 588 (ragged units), 8 panels
     (2, 512, 28, 128, 1),   # K 512: BN 64 panels
     (1, 64, 7, 64, 1),      # tiny: fewer units than wave slots
+    (3, 1024, 14, 256, 1),  # K 1024: 32-column panels (64 KB, 3 slots), 8 panels
+    (2, 1024, 9, 96, 1),    # K 1024, N 96: 32-column panels, ragged M
     (4, 64, 56, 64, 1, 3),  # layer-1 3x3 (72 KB panel, 2 slots, nine gathered taps)
     (3, 64, 13, 64, 1, 3),  # 3x3, odd spatial size, ragged M
 ]
@@ -100,6 +102,7 @@ def test_panel_conv1x1_fwd(lib, shape):
 # panels (3 slots), 2 panels, ragged M
 DGRAD_SHAPES = [
     (4, 56, 256, 64), (4, 56, 64, 256), (2, 56, 256, 128), (4, 28, 512, 128), (4, 28, 128, 512), (3, 14, 1024, 256),
+    (3, 14, 256, 1024),  # K 1024: 32-column panels
     (4, 56, 64, 64, 3), (3, 13, 64, 64, 3),  # 3x3 / pad 1: the flipped taps of wt = [C][3][3][K]
 ]
 # (epi, mask: "bits" | "y" | None, stats, flags): flags bit 1 = the accumulated-into gradient exists
