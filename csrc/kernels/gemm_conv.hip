@@ -2045,12 +2045,34 @@ MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb,
   return (int)dispatch_nt(a, st);
 }
 
+// MI355X_DP_WGRAD256=T (T >= 1): a 1x1 stride-1 weight gradient with >= T output tiles of 256 x 256
+// (K x C) runs as a plain TN GEMM on the 256x256 pipeline (split-K slabs + one reduce) instead of the
+// 128-tile implicit-GEMM kernel; 0 (default): never
+extern "C" int mi_gemm256_tn(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+                             hipStream_t st);
+static int g_wgrad256 = -1;
+static bool use_wgrad256(int K, int C, int R, int S, int stride, int pad, int H, int W, int P, int Q) {
+  if (g_wgrad256 < 0) {
+    const char* e = std::getenv("MI355X_DP_WGRAD256");
+    g_wgrad256 = e ? std::max(0, std::atoi(e)) : 0;
+  }
+  return g_wgrad256 > 0 && R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W && K % 8 == 0 &&
+         C % 8 == 0 && cdiv(K, 256) * cdiv(C, 256) >= g_wgrad256;
+}
+MI_API void mi_set_wgrad256(int min_tiles) {
+  use_wgrad256(0, 0, 0, 0, 0, 0, 0, 0, 0, 0);  // env init
+  g_wgrad256 = std::max(0, min_tiles);
+}
+
 // Conv backward-weight: dw[K][R][S][C] (fp32) += sum over pixels dy^T * im2col(x).
 MI_API int mi_conv2d_wgrad(const void* x, const void* dy, float* dw,
                            int Nb, int H, int W, int C, int K, int R, int S,
                            int stride, int pad, int P, int Q, hipStream_t st) {
   if (C % 8 != 0 || K % 8 != 0) return (int)hipErrorInvalidValue;
   if (use_stem_kernel(C, K, R, S, stride, pad, Q)) return mi_stem_wgrad(x, dy, dw, Nb, H, W, P, Q, pad, st);
+  if (use_wgrad256(K, C, R, S, stride, pad, H, W, P, Q) &&
+      mi_gemm256_tn(dy, x, dw, K, C, Nb * H * W, K, C, C, st) == (int)hipSuccess)
+    return (int)hipSuccess;
   TNArgs a{};
   a.A = (const bf16_t*)dy; a.B = (const bf16_t*)x; a.C = dw;
   a.M = K; a.N = R * S * C; a.K = Nb * P * Q;

@@ -106,6 +106,31 @@ def test_gemm256_tn(M, N, K):
     assert rel_err(C, ref) < 1e-4
 
 
+@pytest.mark.parametrize("Nb,H,C,K", [(4, 14, 1024, 256), (2, 14, 256, 1024), (3, 9, 512, 264)])
+def test_conv_wgrad_on_gemm256_tn(Nb, H, C, K):
+    """MI355X_DP_WGRAD256: a 1x1 stride-1 weight gradient routed to the 256x256 TN GEMM (split-K slabs)
+    accumulates dy^T x into dw like the implicit-GEMM kernel (fp32 reference)"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    lib = _lib.load()
+    CL = torch.channels_last
+    x = (torch.rand(Nb, C, H, H, device="cuda") * 2 - 1).to(BF).contiguous(memory_format=CL)
+    dy = (torch.rand(Nb, K, H, H, device="cuda") * 2 - 1).to(BF).contiguous(memory_format=CL)
+    dw0 = torch.randn(K, C, device="cuda")
+    ref = dw0 + dy.float().permute(0, 2, 3, 1).reshape(-1, K).t() @ x.float().permute(0, 2, 3, 1).reshape(-1, C)
+    outs = []
+    for t in (0, 1):
+        lib.mi_set_wgrad256(t)
+        dw = dw0.clone()
+        try:
+            _lib.call("mi_conv2d_wgrad", ptr(x), ptr(dy), ptr(dw), Nb, H, H, C, K, 1, 1, 1, 0, H, H, stream_of(x))
+            torch.cuda.synchronize()
+        finally:
+            lib.mi_set_wgrad256(0)
+        outs.append(dw)
+        assert rel_err(dw, ref) < 1e-4, t
+
+
 CONV256 = [  # N, C, H, K, R, stride, pad
     (2, 64, 14, 256, 1, 1, 0), (2, 256, 14, 256, 3, 1, 1), (3, 128, 9, 512, 3, 2, 1), (2, 512, 7, 320, 1, 1, 0),
     (1, 64, 30, 256, 3, 1, 1)]
