@@ -97,9 +97,13 @@ __device__ __forceinline__ void phase_barrier() { asm volatile("s_barrier" ::: "
 // 224 tiles of 7/8 the work; g256_bm).  The LDS parts keep their 128-row layout: with WR 112 the
 // second quadrant row holds 48 real rows (rows 48..63 of each wave row's slice are zero-filled and
 // never multiplied), IQ1 = 3 fragment rows instead of 4.
-template <int MODE, int WR = 128>
+// SCAT (MODE 0, bf16 out): output row m goes to row 2 (m / Q) W + 2 (m % Q) of C -- the even pixels of a
+// 2H' x 2W' grid: the stride-2 1x1 data gradient of a projection shortcut written straight into the
+// even pixels of dx (Q = a.fQ.d, W = a.W; mi_gemm256_nt_scat2)
+template <int MODE, int WR = 128, bool SCAT = false>
 __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
   static_assert(WR == 128 || WR == 112, "256- or 224-row tiles");
+  static_assert(!SCAT || MODE == 0, "scattered rows: plain GEMM only");
   constexpr int IQ1 = (WR - 64) / 16;  // fragment rows of quadrant row 1
   constexpr int NI = 4 + IQ1;          // accumulator rows per wave
   __shared__ __attribute__((aligned(16))) uint4 smem[2 * 4 * PART_U4];  // 128 KB
@@ -407,7 +411,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_nt_kernel(G256Args a) {
         const int rl = (g * EPI_U + u) * 8 + (lane >> 3);
         const int m = m0 + wm * WR + mq * 64 + rl;
         ok[sl][u] = m < a.M && n < a.N && mq * 64 + rl < WR;
-        offs[sl][u] = ok[sl][u] ? (size_t)m * a.ldc + n : 0;
+        size_t row = (size_t)m;
+        if constexpr (SCAT) {
+          const uint32_t pq = fdiv((uint32_t)m, a.fQ);
+          row = (size_t)(2u * pq) * (uint32_t)a.W + 2u * ((uint32_t)m - pq * a.fQ.d);
+        }
+        offs[sl][u] = ok[sl][u] ? row * a.ldc + n : 0;
         bool acc_ok = true;
         if (BN_EPI && ok[sl][u] && a.aux_even && (a.epi == 3 || a.epi == 5)) {
           const uint32_t img = fdiv((uint32_t)m, a.fPQ), rem = (uint32_t)m - img * a.fPQ.d;
@@ -923,6 +932,27 @@ MI_API int mi_gemm256_nt(const void* A, const void* B, void* C, const float* bia
   if (hipError_t e = plan_tail(a, cdiv(K, G_BK), st); e != hipSuccess) return (int)e;
   if (wr == 112) hipLaunchKernelGGL((gemm256_nt_kernel<0, 112>), dim3(grid_of(a)), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((gemm256_nt_kernel<0, 128>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Stride-2 1x1 data gradient into the even pixels: C rows 2 (m / Q) W + 2 (m % Q) (ldc = N) get
+// A[m][K] . B[N][K]^T, bf16; the odd pixels are not written (their consumer reads the even ones only,
+// gemm_conv.hip aux_even).  A = dy [Nb*P*Q][K], B = the transposed 1x1 weight [N = C][K].
+MI_API int mi_gemm256_nt_scat2(const void* A, const void* B, void* C, int M, int N, int K, int Q, int W,
+                               hipStream_t st) {
+  if (K % 8 != 0 || N % 8 != 0 || M <= 0 || N <= 0 || Q <= 0 || W < 2 * Q) return (int)hipErrorInvalidValue;
+  G256Args a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.bias = nullptr; a.aux = nullptr; a.epi = 0;
+  a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = K; a.ldc = N;
+  a.W = W; a.fQ = make_fastdiv((uint32_t)Q);
+  const int wr = g256_wr(M, N, K, true);
+  a.tiles_m = cdiv(M, 2 * wr); a.tiles_n = cdiv(N, G_BN);
+  a.a_bytes = rsrc_bytes256((int64_t)M * K);
+  a.b_bytes = rsrc_bytes256((int64_t)N * K);
+  if (!a.a_bytes || !a.b_bytes) return (int)hipErrorInvalidValue;
+  if (hipError_t e = plan_tail(a, cdiv(K, G_BK), st); e != hipSuccess) return (int)e;
+  if (wr == 112) hipLaunchKernelGGL((gemm256_nt_kernel<0, 112, true>), dim3(grid_of(a)), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((gemm256_nt_kernel<0, 128, true>), dim3(grid_of(a)), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -1994,6 +1994,19 @@ extern "C" int mi_gemm256_conv3(int mode, const void* A, const void* B, void* C,
 // never write it.  Only where mi_conv_nol_ok holds (the 128-tile kernels).
 // mbits (epi 4 / 5 with bn_relu): the ReLU mask as bytes of 8 channel bits ([Nb*H*W][C/8], from
 // mi_bn_apply_bits) instead of reading the BN output aux (which may then be null).
+extern "C" int mi_gemm256_nt_scat2(const void* A, const void* B, void* C, int M, int N, int K, int Q, int W,
+                                   hipStream_t st);
+// MI355X_DP_DS256=0: the stride-2 1x1 shortcut data gradients stay on the 128-tile class kernel
+static int g_ds256 = -1;
+static bool use_ds256() {
+  if (g_ds256 < 0) {
+    const char* e = std::getenv("MI355X_DP_DS256");
+    g_ds256 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_ds256 != 0;
+}
+MI_API void mi_set_ds256(int on) { g_ds256 = on ? 1 : 0; }
+
 MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C, int K, int R,
                                int S, int stride, int pad, int P, int Q, int epi, const void* aux, const void* aux2,
                                const float* mean, int bn_relu, float* stats, int flags, const float* mask_scale,
@@ -2010,6 +2023,11 @@ MI_API int mi_conv2d_dgrad_ex4(const void* dy, const void* wt, void* dx, int Nb,
   if (stride == 1 && use_gemm256_conv(Nb * H * W, C, K, R * S * K))
     return mi_gemm256_conv3(2, dy, wt, dx, epi >= 4 ? stats : nullptr, epi, const_cast<void*>(aux), aux2, mean,
                             bn_relu, Nb, P, Q, K, H, W, R, S, 1, pad, C, aux_even, mbits, st);
+  // the stride-2 1x1 data gradient of a projection shortcut (only the even pixels, flags bit 0) as a
+  // plain GEMM over dy's pixels on the 256-wide kernel, rows scattered to the even pixels of dx
+  if (stride == 2 && R == 1 && S == 1 && pad == 0 && epi == 0 && (flags & 1) && !mask_c && !mbits && H == 2 * P &&
+      W == 2 * Q && use_ds256() && use_gemm256_conv(Nb * P * Q, C, K, K))
+    return mi_gemm256_nt_scat2(dy, wt, dx, Nb * P * Q, C, K, Q, W, st);
   if (R == S && pad == (R == 3 ? 1 : 0) && panel_rows_dgrad(Nb * H * W, C, K, R * S, stride) > 0) {
     if (mask_c) return (int)hipErrorNotSupported;  // mi_conv_nol_ok keeps these shapes materialised
     return mi_panel_dgrad(dy, wt, dx, Nb, H, W, C, K, R, epi, aux, aux2, mean, bn_relu, stats, aux_even, mbits,

@@ -131,6 +131,37 @@ def test_conv_wgrad_on_gemm256_tn(Nb, H, C, K):
         assert rel_err(dw, ref) < 1e-4, t
 
 
+@pytest.mark.parametrize("Nb,H,C,K", [(2, 14, 256, 512), (3, 18, 320, 576), (2, 28, 512, 1024)])
+def test_ds_dgrad_scatter_on_gemm256(Nb, H, C, K, conv256_forced):
+    """the stride-2 1x1 shortcut data gradient (even pixels only, flags bit 0) on the 256-wide kernel with
+    its rows scattered into dx's even pixels (mi_gemm256_nt_scat2) matches fp32 at the even pixels and
+    leaves the odd ones untouched, like the 128-tile class kernel it replaces"""
+    from mi355x_dp.ops import _lib
+    from mi355x_dp.ops._lib import ptr, stream_of
+    lib = conv256_forced
+    CL = torch.channels_last
+    P = H // 2
+    dy = (torch.rand(Nb, K, P, P, device="cuda") * 2 - 1).to(BF).contiguous(memory_format=CL)
+    w = ((torch.rand(K, C, 1, 1, device="cuda") * 2 - 1) * 0.1).to(BF)
+    wt = w.reshape(K, C).t().contiguous()  # [C][K]
+    ref = F.conv_transpose2d(dy.float(), w.float(), stride=2, output_padding=1)  # [Nb, C, H, H]
+    outs = []
+    for on in (1, 0):
+        lib.mi_set_ds256(on)
+        dx = torch.full((Nb, C, H, H), 7.0, device="cuda").to(BF).contiguous(memory_format=CL)
+        try:
+            _lib.call("mi_conv2d_dgrad_ex4", ptr(dy), ptr(wt), ptr(dx), Nb, H, H, C, K, 1, 1, 2, 0, P, P, 0,
+                      ptr(None), ptr(None), ptr(None), 0, ptr(None), 1, ptr(None), ptr(None), ptr(None),
+                      stream_of(dy))
+            torch.cuda.synchronize()
+        finally:
+            lib.mi_set_ds256(1)
+        outs.append(dx)
+        ev = dx[:, :, 0::2, 0::2]
+        assert rel_err(ev, ref[:, :, 0::2, 0::2]) < 2e-2, on
+        assert bool((dx[:, :, 1::2, :] == 7.0).all()) and bool((dx[:, :, :, 1::2] == 7.0).all()), on
+
+
 CONV256 = [  # N, C, H, K, R, stride, pad
     (2, 64, 14, 256, 1, 1, 0), (2, 256, 14, 256, 3, 1, 1), (3, 128, 9, 512, 3, 2, 1), (2, 512, 7, 320, 1, 1, 0),
     (1, 64, 30, 256, 3, 1, 1)]
